@@ -1,0 +1,374 @@
+// TEST INFRASTRUCTURE ONLY — Python bindings of the CPU oracle.
+// Loaded only by tests/, __graft_entry__.smoke() and bench.py (cpu_baseline).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <chrono>
+#include <thread>
+
+#include "oracle_decision.h"
+
+namespace py = pybind11;
+using namespace oracle;
+
+namespace {
+
+std::string bytesOf(const py::handle& h) { return h.cast<std::string>(); }
+
+Adjacency adjFromWire(const py::tuple& t) {
+  Adjacency a;
+  a.otherNodeName = t[0].cast<std::string>();
+  a.ifName = t[1].cast<std::string>();
+  a.nextHopV6.addr = bytesOf(t[2]);
+  a.nextHopV4.addr = bytesOf(t[3]);
+  a.metric = t[4].cast<int32_t>();
+  a.adjLabel = t[5].cast<int32_t>();
+  a.isOverloaded = t[6].cast<bool>();
+  a.rtt = t[7].cast<int32_t>();
+  a.timestamp = t[8].cast<int64_t>();
+  a.weight = t[9].cast<int64_t>();
+  a.otherIfName = t[10].cast<std::string>();
+  return a;
+}
+
+AdjacencyDatabase adjDbFromWire(const py::tuple& t) {
+  AdjacencyDatabase db;
+  db.thisNodeName = t[0].cast<std::string>();
+  db.isOverloaded = t[1].cast<bool>();
+  for (auto a : t[2].cast<py::list>()) db.adjacencies.push_back(adjFromWire(a.cast<py::tuple>()));
+  db.nodeLabel = t[3].cast<int32_t>();
+  db.area = t[4].cast<std::string>();
+  return db;
+}
+
+PrefixEntry entryFromWire(const py::tuple& t) {
+  PrefixEntry e;
+  e.prefixAddr = bytesOf(t[0]);
+  e.prefixLen = t[1].cast<int32_t>();
+  e.type = t[2].cast<int32_t>();
+  e.forwardingType = t[3].cast<int32_t>();
+  e.forwardingAlgorithm = t[4].cast<int32_t>();
+  if (!t[5].is_none()) e.minNexthop = t[5].cast<int64_t>();
+  if (!t[6].is_none()) e.prependLabel = t[6].cast<int32_t>();
+  auto m = t[7].cast<py::tuple>();
+  e.metrics = {m[0].cast<int32_t>(), m[1].cast<int32_t>(), m[2].cast<int32_t>()};
+  if (!t[8].is_none()) {
+    auto mvt = t[8].cast<py::tuple>();
+    MetricVector mv;
+    mv.version = mvt[0].cast<int64_t>();
+    for (auto ent : mvt[1]) {
+      auto et = ent.cast<py::tuple>();
+      MetricEntity me;
+      me.type = et[0].cast<int64_t>();
+      me.priority = et[1].cast<int64_t>();
+      me.op = et[2].cast<int32_t>();
+      me.isBestPathTieBreaker = et[3].cast<bool>();
+      me.metric = et[4].cast<std::vector<int64_t>>();
+      mv.metrics.push_back(me);
+    }
+    e.mv = mv;
+  }
+  if (!t[9].is_none()) e.data = bytesOf(t[9]);
+  return e;
+}
+
+py::object entryToWire(const PrefixEntry& e) {
+  py::object mv = py::none();
+  if (e.mv) {
+    py::list ents;
+    for (const auto& me : e.mv->metrics)
+      ents.append(py::make_tuple(me.type, me.priority, me.op, me.isBestPathTieBreaker,
+                                 py::tuple(py::cast(me.metric))));
+    mv = py::make_tuple(e.mv->version, ents);
+  }
+  return py::make_tuple(py::bytes(e.prefixAddr), e.prefixLen, e.type, e.forwardingType,
+                        e.forwardingAlgorithm, py::cast(e.minNexthop),
+                        py::cast(e.prependLabel),
+                        py::make_tuple(e.metrics.path_preference,
+                                       e.metrics.source_preference, e.metrics.distance),
+                        mv, e.data ? py::object(py::bytes(*e.data)) : py::none());
+}
+
+NextHopThrift nhFromWire(const py::tuple& t) {
+  NextHopThrift nh;
+  nh.address.addr = bytesOf(t[0]);
+  if (!t[1].is_none()) nh.address.ifName = t[1].cast<std::string>();
+  nh.weight = t[2].cast<int32_t>();
+  if (!t[3].is_none()) {
+    auto a = t[3].cast<py::tuple>();
+    MplsAction act;
+    act.action = a[0].cast<int32_t>();
+    if (!a[1].is_none()) act.swapLabel = a[1].cast<int32_t>();
+    if (!a[2].is_none()) act.pushLabels = a[2].cast<std::vector<int32_t>>();
+    nh.mplsAction = act;
+  }
+  nh.metric = t[4].cast<int32_t>();
+  if (!t[5].is_none()) nh.area = t[5].cast<std::string>();
+  if (!t[6].is_none()) nh.neighborNodeName = t[6].cast<std::string>();
+  return nh;
+}
+
+py::tuple nhToWire(const NextHopThrift& nh) {
+  py::object act = py::none();
+  if (nh.mplsAction) {
+    act = py::make_tuple(nh.mplsAction->action, py::cast(nh.mplsAction->swapLabel),
+                         nh.mplsAction->pushLabels
+                             ? py::object(py::tuple(py::cast(*nh.mplsAction->pushLabels)))
+                             : py::none());
+  }
+  return py::make_tuple(py::bytes(nh.address.addr), py::cast(nh.address.ifName), nh.weight,
+                        act, nh.metric, py::cast(nh.area), py::cast(nh.neighborNodeName));
+}
+
+py::list nhsToWire(const NextHopSet& s) {
+  py::list l;
+  for (const auto& nh : s) l.append(nhToWire(nh));
+  return l;
+}
+
+py::tuple unicastToWire(const RibUnicastEntry& e) {
+  return py::make_tuple(py::bytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
+                        e.doNotInstall, e.bestArea,
+                        e.bestPrefixEntry ? entryToWire(*e.bestPrefixEntry) : py::none());
+}
+
+py::tuple routeDbToWire(const DecisionRouteDb& db) {
+  py::list uc, mp;
+  for (const auto& [_, e] : db.unicastRoutes) uc.append(unicastToWire(e));
+  for (const auto& [_, e] : db.mplsRoutes) mp.append(py::make_tuple(e.label, nhsToWire(e.nexthops)));
+  return py::make_tuple(uc, mp);
+}
+
+py::tuple changeToWire(const LinkStateChange& c) {
+  return py::make_tuple(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged);
+}
+
+py::tuple linkDesc(const Link& l) {
+  const auto& a = l.firstNodeName();
+  const auto& b = l.secondNodeName();
+  return py::make_tuple(a, l.getIfaceFromNode(a), b, l.getIfaceFromNode(b));
+}
+
+py::list pathToWire(const Path& p) {
+  py::list l;
+  for (const auto& link : p) l.append(linkDesc(*link));
+  return l;
+}
+
+// std::unordered_map would be converted to a dict by pybind11/stl.h; wrap it
+struct AreaMap {
+  AreaLinkStates m;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(openr_oracle, m) {
+  m.doc() = "CPU oracle (test infrastructure): restatement of the OpenR Decision SPF / route build";
+
+  py::class_<LinkState>(m, "LinkState")
+      .def(py::init<const std::string&>())
+      .def("update_adjacency_database",
+           [](LinkState& s, py::tuple db, uint64_t up, uint64_t down) {
+             return changeToWire(s.updateAdjacencyDatabase(adjDbFromWire(db), up, down));
+           },
+           py::arg("db"), py::arg("hold_up_ttl") = 0, py::arg("hold_down_ttl") = 0)
+      .def("delete_adjacency_database",
+           [](LinkState& s, const std::string& n) { return changeToWire(s.deleteAdjacencyDatabase(n)); })
+      .def("decrement_holds", [](LinkState& s) { return changeToWire(s.decrementHolds()); })
+      .def("has_holds", &LinkState::hasHolds)
+      .def("has_node", &LinkState::hasNode)
+      .def("is_node_overloaded", &LinkState::isNodeOverloaded)
+      .def("num_links", &LinkState::numLinks)
+      .def("num_nodes", &LinkState::numNodes)
+      .def_property_readonly("spf_runs", [](const LinkState& s) { return s.spfRuns; })
+      .def("links_from_node",
+           [](const LinkState& s, const std::string& n) {
+             py::list l;
+             for (const auto& link : s.linksFromNode(n)) l.append(linkDesc(*link));
+             return l;
+           })
+      .def("get_spf_result",
+           [](const LinkState& s, const std::string& n, bool useLinkMetric) {
+             py::dict d;
+             for (const auto& [name, r] : s.getSpfResult(n, useLinkMetric)) {
+               std::vector<std::string> nhs(r.nextHops().begin(), r.nextHops().end());
+               std::sort(nhs.begin(), nhs.end());
+               py::list pls;
+               for (const auto& pl : r.pathLinks()) pls.append(py::make_tuple(linkDesc(*pl.link), pl.prevNode));
+               d[py::str(name)] = py::make_tuple(r.metric(), nhs, pls);
+             }
+             return d;
+           },
+           py::arg("node"), py::arg("use_link_metric") = true)
+      .def("run_spf_ignoring",
+           [](const LinkState& s, const std::string& src, std::vector<py::tuple> ignore) {
+             // runSpf(src, true, linksToIgnore) for links named by descriptor
+             LinkSet ign;
+             for (auto& t : ignore) {
+               auto n1 = t[0].cast<std::string>();
+               auto if1 = t[1].cast<std::string>();
+               for (const auto& link : s.linksFromNode(n1))
+                 if (link->getIfaceFromNode(n1) == if1 &&
+                     link->getOtherNodeName(n1) == t[2].cast<std::string>())
+                   ign.insert(link);
+             }
+             py::dict d;
+             for (const auto& [name, r] : s.runSpf(src, true, ign)) {
+               std::vector<std::string> nhs(r.nextHops().begin(), r.nextHops().end());
+               std::sort(nhs.begin(), nhs.end());
+               d[py::str(name)] = py::make_tuple(r.metric(), nhs);
+             }
+             return d;
+           })
+      .def("get_kth_paths",
+           [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
+             py::list out;
+             for (const auto& p : s.getKthPaths(a, b, k)) out.append(pathToWire(p));
+             return out;
+           })
+      .def("get_metric_from_a_to_b", &LinkState::getMetricFromAToB, py::arg("a"), py::arg("b"),
+           py::arg("use_link_metric") = true)
+      .def("get_hops_from_a_to_b", &LinkState::getHopsFromAToB)
+      .def("get_max_hops_to_node", &LinkState::getMaxHopsToNode)
+      .def("metric_from_node",
+           [](const LinkState& s, const std::string& n1, const std::string& if1,
+              const std::string& from) {
+             for (const auto& link : s.linksFromNode(n1))
+               if (link->getIfaceFromNode(n1) == if1) return link->getMetricFromNode(from);
+             throw std::out_of_range("no such link");
+           })
+      .def("time_spf_sources",
+           [](const LinkState& s, std::vector<std::string> srcs, int threads) {
+             // Timed all-sources SPF: one LinkState copy per thread (the memo is
+             // not thread-safe, LinkState.h:279-301), no cross-source memo.
+             py::gil_scoped_release rel;
+             threads = std::max(1, threads);
+             std::vector<LinkState> copies(threads, s);
+             const auto t0 = std::chrono::steady_clock::now();
+             std::vector<std::thread> ws;
+             size_t checksum = 0;
+             std::vector<size_t> sums(threads, 0);
+             for (int t = 0; t < threads; ++t) {
+               ws.emplace_back([&, t] {
+                 for (size_t i = t; i < srcs.size(); i += threads) {
+                   auto r = copies[t].runSpf(srcs[i], true);
+                   sums[t] += r.size();
+                 }
+               });
+             }
+             for (auto& w : ws) w.join();
+             const double sec =
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             for (auto v : sums) checksum += v;
+             return std::make_pair(sec, checksum);
+           });
+
+  m.def("path_a_in_path_b", [](std::vector<py::tuple> a, std::vector<py::tuple> b) {
+    auto mk = [](const std::vector<py::tuple>& v) {
+      Path p;
+      for (auto& t : v)
+        p.push_back(std::make_shared<Link>("a", t[0].cast<std::string>(), t[1].cast<std::string>(),
+                                           t[2].cast<std::string>(), t[3].cast<std::string>()));
+      return p;
+    };
+    return LinkState::pathAInPathB(mk(a), mk(b));
+  });
+
+  m.def("link_hash", [](const std::string& n1, const std::string& if1, const std::string& n2,
+                        const std::string& if2) { return Link("a", n1, if1, n2, if2).hash; });
+
+  m.def("unordered_int_order", [](std::vector<int> keys) {
+    // iteration order of a libstdc++ std::unordered_map<int, ...> built by
+    // inserting `keys` in order (the reference test helper's container,
+    // DecisionTestUtils.cpp:18-43)
+    std::unordered_map<int, int> mp;
+    for (int k : keys) mp.emplace(k, 0);
+    std::vector<int> order;
+    for (auto& kv : mp) order.push_back(kv.first);
+    return order;
+  });
+
+  py::class_<AreaMap>(m, "AreaLinkStates")
+      .def(py::init<>())
+      .def("add_area", [](AreaMap& a, const std::string& area) {
+        a.m.emplace(area, LinkState(area));
+      })
+      .def("area", [](AreaMap& a, const std::string& area) -> LinkState& { return a.m.at(area); },
+           py::return_value_policy::reference_internal)
+      .def("areas", [](const AreaMap& a) {
+        std::vector<std::string> v;
+        for (auto& kv : a.m) v.push_back(kv.first);
+        return v;
+      });
+
+  py::class_<PrefixState>(m, "PrefixState")
+      .def(py::init<>())
+      .def("update_prefix",
+           [](PrefixState& s, const std::string& node, const std::string& area, py::tuple e) {
+             py::list out;
+             for (const auto& c : s.updatePrefix(node, area, entryFromWire(e)))
+               out.append(py::make_tuple(py::bytes(c.first), c.second));
+             return out;
+           })
+      .def("delete_prefix",
+           [](PrefixState& s, const std::string& node, const std::string& area, py::bytes addr,
+              int32_t len) {
+             py::list out;
+             for (const auto& c : s.deletePrefix(node, area, Cidr{std::string(addr), len}))
+               out.append(py::make_tuple(py::bytes(c.first), c.second));
+             return out;
+           })
+      .def("num_prefixes", [](const PrefixState& s) { return s.prefixes().size(); });
+
+  py::class_<SpfSolver>(m, "SpfSolver")
+      .def(py::init<const std::string&, bool, bool, bool, bool>(), py::arg("my_node"),
+           py::arg("enable_v4"), py::arg("enable_ordered_fib") = false,
+           py::arg("bgp_dry_run") = false, py::arg("enable_best_route_selection") = false)
+      .def("build_route_db",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als,
+              const PrefixState& ps) -> py::object {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             if (!db) return py::none();
+             return routeDbToWire(*db);
+           })
+      .def("time_build_route_db",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als,
+              const PrefixState& ps) {
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.buildRouteDb(me, als.m, ps);
+             const double sec =
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
+             return std::make_pair(sec, n);
+           })
+      .def("create_route_for_prefix_or_get_static_route",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als,
+              const PrefixState& ps, py::bytes addr, int32_t len) -> py::object {
+             auto r = s.createRouteForPrefixOrGetStaticRoute(me, als.m, ps, Cidr{std::string(addr), len});
+             if (!r) return py::none();
+             return unicastToWire(*r);
+           })
+      .def("update_static_unicast_routes",
+           [](SpfSolver& s, std::vector<py::tuple> upd, std::vector<py::tuple> del) {
+             std::vector<std::pair<Cidr, std::vector<NextHopThrift>>> u;
+             for (auto& t : upd) {
+               std::vector<NextHopThrift> nhs;
+               for (auto n : t[2].cast<py::list>()) nhs.push_back(nhFromWire(n.cast<py::tuple>()));
+               u.push_back({Cidr{bytesOf(t[0]), t[1].cast<int32_t>()}, nhs});
+             }
+             std::vector<Cidr> d;
+             for (auto& t : del) d.push_back(Cidr{bytesOf(t[0]), t[1].cast<int32_t>()});
+             s.updateStaticUnicastRoutes(u, d);
+           })
+      .def("update_static_mpls_routes",
+           [](SpfSolver& s, std::vector<py::tuple> upd, std::vector<int32_t> del) {
+             std::vector<std::pair<int32_t, std::vector<NextHopThrift>>> u;
+             for (auto& t : upd) {
+               std::vector<NextHopThrift> nhs;
+               for (auto n : t[1].cast<py::list>()) nhs.push_back(nhFromWire(n.cast<py::tuple>()));
+               u.push_back({t[0].cast<int32_t>(), nhs});
+             }
+             s.updateStaticMplsRoutes(u, del);
+           })
+      .def_property_readonly("route_build_runs", [](const SpfSolver& s) { return s.routeBuildRuns; });
+}

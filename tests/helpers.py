@@ -1,0 +1,67 @@
+"""Test helpers restating the reference test utilities.
+
+  route_map              getRouteMap + fillRouteMap (DecisionTest.cpp:256-320)
+  nh_from_adj            createNextHopFromAdj (DecisionTest.cpp:208-222)
+  update_prefix_database updatePrefixDatabase (DecisionTest.cpp:436-463)
+"""
+from openr_amd.types import (K_TESTING_AREA, MplsActionCode, NextHopThrift,
+                             create_mpls_action, create_next_hop)
+
+
+def route_map(solver, nodes, als, ps):
+    """(node, prefix-string | label-string) -> frozenset(nexthops); a route
+    with no nexthops adds no key, exactly as fillRouteMap's per-nexthop
+    emplace does."""
+    out = {}
+    for node in nodes:
+        db = solver.build_route_db(node, als, ps)
+        if db is None:
+            continue
+        for pfx, r in db.unicastRoutes.items():
+            for nh in r.nextHops:
+                out.setdefault((node, str(pfx)), set()).add(nh)
+        for label, r in db.mplsRoutes.items():
+            for nh in r.nextHops:
+                out.setdefault((node, str(label)), set()).add(nh)
+    return {k: frozenset(v) for k, v in out.items()}
+
+
+def nh_from_adj(adj, v4, metric, action=None, area=K_TESTING_AREA) -> NextHopThrift:
+    return create_next_hop(adj.nextHopV4 if v4 else adj.nextHopV6, adj.ifName, metric,
+                           action, area, adj.otherNodeName)
+
+
+PHP = create_mpls_action(MplsActionCode.PHP)
+POP = create_mpls_action(MplsActionCode.POP_AND_LOOKUP)
+
+
+def swap(label):
+    return create_mpls_action(MplsActionCode.SWAP, label)
+
+
+def push(*labels):
+    return create_mpls_action(MplsActionCode.PUSH, None, list(labels))
+
+
+def update_prefix_database(ps, node, entries, area=K_TESTING_AREA, old=()):
+    """Replace node's advertisements: update every entry, delete keys that
+    were in ``old`` but not in ``entries``."""
+    changed = set()
+    new_keys = set()
+    for e in entries:
+        changed |= ps.update_prefix(node, area, e)
+        new_keys.add(e.prefix)
+    for e in old:
+        if e.prefix not in new_keys:
+            changed |= ps.delete_prefix(node, area, e.prefix)
+    return changed
+
+
+def pop_route(area=K_TESTING_AREA):
+    from openr_amd.types import BinaryAddress
+    return NextHopThrift(BinaryAddress(bytes(16)), 0, POP, 0, area, None)
+
+
+def adj_label_nexthops(adjs, area=K_TESTING_AREA):
+    """validateAdjLabelRoutes (DecisionTest.cpp:354-368)."""
+    return {a.adjLabel: frozenset({nh_from_adj(a, False, a.metric, PHP, area)}) for a in adjs}
