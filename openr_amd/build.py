@@ -1,0 +1,98 @@
+"""In-tree build of the native parts (no JIT cache: the .so files travel with
+the repo snapshot to the GPU box).
+
+  openr_amd/lib/libopenr_hip.so      hipcc, gfx950: C ABI + SPF kernels
+  openr_amd/_openr_host*.so          g++: drop-in LinkState / SpfSolver host
+                                     library (links libopenr_hip), pybind11
+  oracle/build/openr_oracle*.so      g++: CPU oracle (test infrastructure)
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libopenr_hip.so")
+EXT = sysconfig.get_config_var("EXT_SUFFIX")
+HOST_MOD = os.path.join(PKG, "_openr_host" + EXT)
+ARCH = os.environ.get("OPENR_HIP_ARCH", "gfx950")
+
+HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "spf_kernels.hip")]
+HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "spf_solver.cpp", "host_py.cpp")]
+
+
+def _hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: cannot build libopenr_hip for " + ARCH)
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _deps(srcs, hdr_dirs):
+    out = list(srcs)
+    for d in hdr_dirs:
+        for root, _, files in os.walk(d):
+            out += [os.path.join(root, f) for f in files if f.endswith((".h", ".hpp"))]
+    return out
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build_hip_lib(force: bool = False) -> str:
+    deps = _deps(HIP_SRCS, [os.path.join(CSRC, "kernels"), os.path.join(ROOT, "include")])
+    if force or _stale(HIP_LIB, deps):
+        os.makedirs(LIB_DIR, exist_ok=True)
+        tmp = HIP_LIB + ".tmp"
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              "-Wno-unused-value", "-Wno-unused-result", "-o", tmp] + HIP_SRCS)
+        os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_host_module(force: bool = False) -> str:
+    import pybind11
+    deps = _deps(HOST_SRCS, [os.path.join(CSRC, "host"), os.path.join(ROOT, "include")]) + [HIP_LIB]
+    if force or _stale(HOST_MOD, deps):
+        tmp = HOST_MOD + ".tmp"
+        _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+              f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+              f"-I{os.path.join(ROOT, 'include')}", "-o", tmp] + HOST_SRCS +
+             [f"-L{LIB_DIR}", "-lopenr_hip", "-Wl,-rpath,$ORIGIN/lib"])
+        os.replace(tmp, HOST_MOD)
+    return HOST_MOD
+
+
+def build_oracle() -> None:
+    """CPU oracle (test infrastructure); built here so the GPU box has it."""
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+def build_all(force: bool = False) -> None:
+    with ThreadPoolExecutor(2) as ex:
+        f_oracle = ex.submit(build_oracle)
+        build_hip_lib(force)
+        build_host_module(force)
+        f_oracle.result()
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built", HIP_LIB, HOST_MOD)

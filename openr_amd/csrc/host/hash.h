@@ -1,0 +1,46 @@
+// Hash functions whose values decide iteration order in the reference's
+// unordered containers, so that order-dependent results (KSP2 tie-breaks
+// among parallel links, LinkState.cpp:398-419 over :844) match exactly.
+//
+// folly's std::hash<std::pair<A, B>> (folly rev 1ab6a01f, not present in
+// the reference tree) is hash_combine(a, b) = hash_128_to_64(H(a), H(b))
+// with H = std::hash; strings use libstdc++'s std::hash<std::string>.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <utility>
+
+namespace openr_amd {
+
+inline uint64_t hash128to64(uint64_t upper, uint64_t lower) {
+  constexpr uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= (a >> 47);
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= (b >> 47);
+  return b * kMul;
+}
+
+inline size_t strHash(const std::string& s) { return std::hash<std::string>{}(s); }
+
+inline size_t pairHash(const std::string& a, const std::string& b) {
+  return hash128to64(strHash(a), strHash(b));
+}
+
+struct StrPairHash {
+  size_t operator()(const std::pair<std::string, std::string>& p) const {
+    return pairHash(p.first, p.second);
+  }
+};
+
+// Link::hash (LinkState.cpp:138-142): pair of (node, ifName) pairs in
+// std::minmax order
+inline size_t linkHash(const std::string& n1, const std::string& if1, const std::string& n2,
+                       const std::string& if2) {
+  return hash128to64(pairHash(n1, if1), pairHash(n2, if2));
+}
+
+}  // namespace openr_amd

@@ -1,0 +1,457 @@
+// Python bindings of the drop-in Decision host library (module
+// openr_amd._openr_host). The wire format (tuples) is shared with the test
+// oracle so that openr_amd.facade can drive either one.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <chrono>
+
+#include "spf_solver.h"
+
+namespace py = pybind11;
+using namespace openr_amd;
+
+namespace {
+
+std::string str(const py::handle& h) { return h.cast<std::string>(); }
+
+Adjacency adjFromWire(const py::tuple& t) {
+  Adjacency a;
+  a.otherNodeName = str(t[0]);
+  a.ifName = str(t[1]);
+  a.nextHopV6.addr = str(t[2]);
+  a.nextHopV4.addr = str(t[3]);
+  a.metric = t[4].cast<int32_t>();
+  a.adjLabel = t[5].cast<int32_t>();
+  a.isOverloaded = t[6].cast<bool>();
+  a.rtt = t[7].cast<int32_t>();
+  a.timestamp = t[8].cast<int64_t>();
+  a.weight = t[9].cast<int64_t>();
+  a.otherIfName = str(t[10]);
+  return a;
+}
+
+AdjacencyDatabase adjDbFromWire(const py::tuple& t) {
+  AdjacencyDatabase db;
+  db.thisNodeName = str(t[0]);
+  db.isOverloaded = t[1].cast<bool>();
+  const auto adjs = t[2].cast<py::list>();
+  db.adjacencies.reserve(adjs.size());
+  for (auto a : adjs) db.adjacencies.push_back(adjFromWire(a.cast<py::tuple>()));
+  db.nodeLabel = t[3].cast<int32_t>();
+  db.area = str(t[4]);
+  return db;
+}
+
+PrefixEntry entryFromWire(const py::tuple& t) {
+  PrefixEntry e;
+  e.addr = str(t[0]);
+  e.len = t[1].cast<int32_t>();
+  e.type = t[2].cast<int32_t>();
+  e.forwardingType = t[3].cast<int32_t>();
+  e.forwardingAlgorithm = t[4].cast<int32_t>();
+  if (!t[5].is_none()) e.minNexthop = t[5].cast<int64_t>();
+  if (!t[6].is_none()) e.prependLabel = t[6].cast<int32_t>();
+  auto m = t[7].cast<py::tuple>();
+  e.pathPreference = m[0].cast<int32_t>();
+  e.sourcePreference = m[1].cast<int32_t>();
+  e.distance = m[2].cast<int32_t>();
+  if (!t[8].is_none()) {
+    auto mvt = t[8].cast<py::tuple>();
+    MetricVector mv;
+    mv.version = mvt[0].cast<int64_t>();
+    for (auto ent : mvt[1]) {
+      auto et = ent.cast<py::tuple>();
+      mv.metrics.push_back(MetricEntity{et[0].cast<int64_t>(), et[1].cast<int64_t>(),
+                                        et[2].cast<int32_t>(), et[3].cast<bool>(),
+                                        et[4].cast<std::vector<int64_t>>()});
+    }
+    e.mv = std::move(mv);
+  }
+  if (!t[9].is_none()) e.data = str(t[9]);
+  return e;
+}
+
+py::object entryToWire(const PrefixEntry& e) {
+  py::object mv = py::none();
+  if (e.mv) {
+    py::list ents;
+    for (const auto& me : e.mv->metrics)
+      ents.append(py::make_tuple(me.type, me.priority, me.op, me.isBestPathTieBreaker,
+                                 py::tuple(py::cast(me.metric))));
+    mv = py::make_tuple(e.mv->version, ents);
+  }
+  return py::make_tuple(py::bytes(e.addr), e.len, e.type, e.forwardingType, e.forwardingAlgorithm,
+                        py::cast(e.minNexthop), py::cast(e.prependLabel),
+                        py::make_tuple(e.pathPreference, e.sourcePreference, e.distance), mv,
+                        e.data ? py::object(py::bytes(*e.data)) : py::none());
+}
+
+NextHopThrift nhFromWire(const py::tuple& t) {
+  NextHopThrift nh;
+  nh.address.addr = str(t[0]);
+  if (!t[1].is_none()) nh.address.ifName = str(t[1]);
+  nh.weight = t[2].cast<int32_t>();
+  if (!t[3].is_none()) {
+    auto a = t[3].cast<py::tuple>();
+    MplsAction act;
+    act.action = a[0].cast<int32_t>();
+    if (!a[1].is_none()) act.swapLabel = a[1].cast<int32_t>();
+    if (!a[2].is_none()) act.pushLabels = a[2].cast<std::vector<int32_t>>();
+    nh.mplsAction = std::move(act);
+  }
+  nh.metric = t[4].cast<int32_t>();
+  if (!t[5].is_none()) nh.area = str(t[5]);
+  if (!t[6].is_none()) nh.neighborNodeName = str(t[6]);
+  return nh;
+}
+
+py::tuple nhToWire(const NextHopThrift& nh) {
+  py::object act = py::none();
+  if (nh.mplsAction) {
+    act = py::make_tuple(nh.mplsAction->action, py::cast(nh.mplsAction->swapLabel),
+                         nh.mplsAction->pushLabels
+                             ? py::object(py::tuple(py::cast(*nh.mplsAction->pushLabels)))
+                             : py::none());
+  }
+  return py::make_tuple(py::bytes(nh.address.addr), py::cast(nh.address.ifName), nh.weight, act,
+                        nh.metric, py::cast(nh.area), py::cast(nh.neighborNodeName));
+}
+
+py::list nhsToWire(const NextHopSet& s) {
+  py::list l;
+  for (const auto& nh : s) l.append(nhToWire(nh));
+  return l;
+}
+
+py::tuple unicastToWire(const RibUnicastEntry& e) {
+  return py::make_tuple(py::bytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
+                        e.doNotInstall, e.bestArea,
+                        e.bestPrefixEntry ? entryToWire(*e.bestPrefixEntry) : py::none());
+}
+
+py::tuple routeDbToWire(const DecisionRouteDb& db) {
+  py::list uc, mp;
+  for (const auto& [_, e] : db.unicastRoutes) uc.append(unicastToWire(e));
+  for (const auto& [_, e] : db.mplsRoutes) mp.append(py::make_tuple(e.label, nhsToWire(e.nexthops)));
+  return py::make_tuple(uc, mp);
+}
+
+py::tuple changeToWire(const LinkStateChange& c) {
+  return py::make_tuple(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged);
+}
+
+py::tuple linkDesc(const Link& l) { return py::make_tuple(l.on1, l.oif1, l.on2, l.oif2); }
+
+std::optional<uint32_t> findLink(const LinkState& ls, const std::string& n1, const std::string& if1,
+                                 const std::string& n2) {
+  auto a = ls.nodeId(n1);
+  if (!a) return std::nullopt;
+  for (uint32_t lid : ls.linksFromNode(n1)) {
+    const Link& l = ls.link(lid);
+    if (l.ifFrom(*a) == if1 && ls.nodeName(l.other(*a)) == n2) return lid;
+  }
+  return std::nullopt;
+}
+
+py::dict rowToDict(const LinkState& ls, const SpfRow& row, bool withPaths) {
+  py::dict d;
+  if (!row.known) {
+    d[py::str(row.srcName)] = py::make_tuple(0, py::list(), py::list());
+    return d;
+  }
+  for (uint32_t v = 0; v < row.dist.size(); ++v) {
+    if (!row.reachable(v)) continue;
+    std::vector<std::string> nhs;
+    row.forEachNextHop(v, [&](uint32_t nb) { nhs.push_back(ls.nodeName(nb)); });
+    std::sort(nhs.begin(), nhs.end());
+    py::list pls;
+    if (withPaths) {
+      for (const auto& [lid, prev] : ls.pathLinks(row, v))
+        pls.append(py::make_tuple(linkDesc(ls.link(lid)), ls.nodeName(prev)));
+    }
+    d[py::str(ls.nodeName(v))] = py::make_tuple(static_cast<uint64_t>(row.dist[v]), nhs, pls);
+  }
+  return d;
+}
+
+struct AreaMap {
+  AreaLinkStates m;
+};
+
+// all-sources sweep over a LinkState's device mirror (bench / parity tools):
+// device-resident dist + first-hop rows for a fixed source list
+class SpfSweep {
+ public:
+  SpfSweep(const LinkState& ls, const std::vector<std::string>& srcs, bool useLinkMetric)
+      : ls_(ls), useLinkMetric_(useLinkMetric) {
+    for (const auto& s : srcs) {
+      auto id = ls.nodeId(s);
+      if (!id) throw std::invalid_argument("SpfSweep: unknown source " + s);
+      srcs_.push_back(*id);
+    }
+    graph_ = ls.deviceGraph();
+    ctx_ = ls.context();
+    uint32_t nn = 0, ne = 0;
+    orh_graph_info(graph_, &nn, &ne);
+    n_ = nn;
+    edges_ = ne;
+    if (orh_spf_words(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), &words_) != ORH_OK)
+      throw std::runtime_error("orh_spf_words failed");
+    const size_t nd = srcs_.size() * static_cast<size_t>(n_);
+    if (orh_device_alloc(ctx_, nd * 4, reinterpret_cast<void**>(&dDist_)) != ORH_OK ||
+        orh_device_alloc(ctx_, nd * 4 * words_, reinterpret_cast<void**>(&dNh_)) != ORH_OK)
+      throw std::runtime_error("SpfSweep: device allocation failed");
+  }
+  ~SpfSweep() {
+    orh_device_free(ctx_, dDist_);
+    orh_device_free(ctx_, dNh_);
+  }
+  void run() {  // asynchronous
+    orh_spf_request req{};
+    req.h_srcs = srcs_.data();
+    req.n_src = static_cast<uint32_t>(srcs_.size());
+    req.use_link_metric = useLinkMetric_ ? 1 : 0;
+    if (orh_spf_run(graph_, &req, words_, dDist_, dNh_) != ORH_OK)
+      throw std::runtime_error(std::string("orh_spf_run: ") + orh_last_error(ctx_));
+  }
+  double lastMs() {
+    double ms = 0;
+    if (orh_last_spf_ms(ctx_, &ms) != ORH_OK) throw std::runtime_error("orh_last_spf_ms failed");
+    return ms;
+  }
+  void sync() {
+    if (orh_sync(ctx_) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
+  }
+  py::tuple fetch(size_t i) {
+    if (i >= srcs_.size()) throw std::out_of_range("SpfSweep.fetch");
+    py::array_t<uint32_t> dist(n_), nh(static_cast<size_t>(n_) * words_);
+    orh_memcpy_d2h(ctx_, dist.mutable_data(), dDist_ + i * n_, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_ + i * static_cast<size_t>(n_) * words_,
+                   static_cast<size_t>(n_) * words_ * 4);
+    return py::make_tuple(dist, nh);
+  }
+  uint32_t words() const { return words_; }
+  uint32_t nodes() const { return n_; }
+  uint32_t edges() const { return edges_; }
+  size_t sources() const { return srcs_.size(); }
+
+ private:
+  const LinkState& ls_;
+  bool useLinkMetric_;
+  std::vector<uint32_t> srcs_;
+  orh_graph* graph_{nullptr};
+  orh_ctx* ctx_{nullptr};
+  uint32_t n_{0}, edges_{0}, words_{1};
+  uint32_t* dDist_{nullptr};
+  uint32_t* dNh_{nullptr};
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_openr_host, m) {
+  m.doc() = "OpenR Decision SPF / route build on MI355X (host library over libopenr_hip)";
+
+  py::class_<LinkState>(m, "LinkState")
+      .def("update_adjacency_database",
+           [](LinkState& s, py::tuple db, uint64_t up, uint64_t down) {
+             return changeToWire(s.updateAdjacencyDatabase(adjDbFromWire(db), up, down));
+           },
+           py::arg("db"), py::arg("hold_up_ttl") = 0, py::arg("hold_down_ttl") = 0)
+      .def("update_adjacency_databases",
+           [](LinkState& s, py::list dbs) {
+             py::list out;
+             for (auto d : dbs) out.append(changeToWire(s.updateAdjacencyDatabase(adjDbFromWire(d.cast<py::tuple>()))));
+             return out;
+           })
+      .def("delete_adjacency_database",
+           [](LinkState& s, const std::string& n) { return changeToWire(s.deleteAdjacencyDatabase(n)); })
+      .def("decrement_holds", [](LinkState& s) { return changeToWire(s.decrementHolds()); })
+      .def("has_holds", &LinkState::hasHolds)
+      .def("has_node", &LinkState::hasNode)
+      .def("is_node_overloaded", &LinkState::isNodeOverloaded)
+      .def("num_links", &LinkState::numLinks)
+      .def("num_nodes", &LinkState::numNodes)
+      .def_property_readonly("spf_runs", &LinkState::spfRuns)
+      .def("links_from_node",
+           [](const LinkState& s, const std::string& n) {
+             py::list l;
+             for (uint32_t lid : s.linksFromNode(n)) l.append(linkDesc(s.link(lid)));
+             return l;
+           })
+      .def("get_spf_result",
+           [](const LinkState& s, const std::string& n, bool useLinkMetric) {
+             return rowToDict(s, s.getSpfResult(n, useLinkMetric), true);
+           },
+           py::arg("node"), py::arg("use_link_metric") = true)
+      .def("run_spf_ignoring",
+           [](const LinkState& s, const std::string& src, std::vector<py::tuple> ignore) {
+             std::vector<uint32_t> ign;
+             for (auto& t : ignore) {
+               if (auto lid = findLink(s, str(t[0]), str(t[1]), str(t[2]))) ign.push_back(*lid);
+             }
+             auto row = s.runSpf(src, true, ign);
+             py::dict d;
+             for (auto item : rowToDict(s, row, false)) {
+               auto v = item.second.cast<py::tuple>();
+               d[item.first] = py::make_tuple(v[0], v[1]);
+             }
+             return d;
+           })
+      .def("get_kth_paths",
+           [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
+             py::list out;
+             for (const auto& p : s.getKthPaths(a, b, k)) {
+               py::list path;
+               for (uint32_t lid : p) path.append(linkDesc(s.link(lid)));
+               out.append(path);
+             }
+             return out;
+           })
+      .def("get_metric_from_a_to_b", &LinkState::getMetricFromAToB, py::arg("a"), py::arg("b"),
+           py::arg("use_link_metric") = true)
+      .def("get_hops_from_a_to_b",
+           [](const LinkState& s, const std::string& a, const std::string& b) {
+             return s.getMetricFromAToB(a, b, false);
+           })
+      .def("get_max_hops_to_node", &LinkState::getMaxHopsToNode)
+      .def("metric_from_node",
+           [](const LinkState& s, const std::string& n1, const std::string& if1,
+              const std::string& from) {
+             auto a = s.nodeId(n1);
+             auto f = s.nodeId(from);
+             if (a && f) {
+               for (uint32_t lid : s.linksFromNode(n1))
+                 if (s.link(lid).ifFrom(*a) == if1) return s.link(lid).metricFrom(*f);
+             }
+             throw std::out_of_range("no such link");
+           })
+      .def("node_names",
+           [](const LinkState& s) {
+             std::vector<std::string> v;
+             for (uint32_t i = 0; i < s.numNodeIds(); ++i) v.push_back(s.nodeName(i));
+             return v;
+           })
+      .def("sweep", [](const LinkState& s, const std::vector<std::string>& srcs, bool useLinkMetric) {
+             return new SpfSweep(s, srcs, useLinkMetric);
+           },
+           py::arg("srcs"), py::arg("use_link_metric") = true,
+           py::return_value_policy::take_ownership, py::keep_alive<0, 1>());
+
+  py::class_<SpfSweep>(m, "SpfSweep")
+      .def("run", &SpfSweep::run)
+      .def("last_ms", &SpfSweep::lastMs)
+      .def("sync", &SpfSweep::sync)
+      .def("fetch", &SpfSweep::fetch)
+      .def_property_readonly("words", &SpfSweep::words)
+      .def_property_readonly("nodes", &SpfSweep::nodes)
+      .def_property_readonly("edges", &SpfSweep::edges)
+      .def_property_readonly("sources", &SpfSweep::sources);
+
+  m.def("path_a_in_path_b", [](std::vector<py::tuple>, std::vector<py::tuple>) -> bool {
+    throw std::runtime_error("path_a_in_path_b: use LinkState paths (ids are per LinkState)");
+  });
+
+  py::class_<AreaMap>(m, "AreaLinkStates")
+      .def(py::init<>())
+      .def("add_area",
+           [](AreaMap& a, const std::string& area) {
+             a.m.emplace(std::piecewise_construct, std::forward_as_tuple(area),
+                         std::forward_as_tuple(area));
+           })
+      .def("area", [](AreaMap& a, const std::string& area) -> LinkState& { return a.m.at(area); },
+           py::return_value_policy::reference_internal)
+      .def("areas", [](const AreaMap& a) {
+        std::vector<std::string> v;
+        for (const auto& kv : a.m) v.push_back(kv.first);
+        return v;
+      });
+
+  py::class_<PrefixState>(m, "PrefixState")
+      .def(py::init<>())
+      .def("update_prefix",
+           [](PrefixState& s, const std::string& node, const std::string& area, py::tuple e) {
+             py::list out;
+             for (const auto& c : s.updatePrefix(node, area, entryFromWire(e)))
+               out.append(py::make_tuple(py::bytes(c.first), c.second));
+             return out;
+           })
+      .def("update_prefixes",
+           [](PrefixState& s, py::list items) {
+             size_t n = 0;
+             for (auto it : items) {
+               auto t = it.cast<py::tuple>();
+               n += s.updatePrefix(str(t[0]), str(t[1]), entryFromWire(t[2].cast<py::tuple>())).size();
+             }
+             return n;
+           })
+      .def("delete_prefix",
+           [](PrefixState& s, const std::string& node, const std::string& area, py::bytes addr,
+              int32_t len) {
+             py::list out;
+             for (const auto& c : s.deletePrefix(node, area, Cidr{std::string(addr), len}))
+               out.append(py::make_tuple(py::bytes(c.first), c.second));
+             return out;
+           })
+      .def("num_prefixes", [](const PrefixState& s) { return s.prefixes().size(); });
+
+  py::class_<SpfSolver>(m, "SpfSolver")
+      .def(py::init<const std::string&, bool, bool, bool, bool>(), py::arg("my_node"),
+           py::arg("enable_v4"), py::arg("enable_ordered_fib") = false,
+           py::arg("bgp_dry_run") = false, py::arg("enable_best_route_selection") = false)
+      .def("build_route_db",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als,
+              const PrefixState& ps) -> py::object {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             if (!db) return py::none();
+             return routeDbToWire(*db);
+           })
+      .def("time_build_route_db",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps) {
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.buildRouteDb(me, als.m, ps);
+             const double sec =
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
+             return std::make_pair(sec, n);
+           })
+      .def("create_route_for_prefix_or_get_static_route",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              py::bytes addr, int32_t len) -> py::object {
+             auto r = s.createRouteForPrefixOrGetStaticRoute(me, als.m, ps,
+                                                             Cidr{std::string(addr), len});
+             if (!r) return py::none();
+             return unicastToWire(*r);
+           })
+      .def("update_static_unicast_routes",
+           [](SpfSolver& s, std::vector<py::tuple> upd, std::vector<py::tuple> del) {
+             std::vector<std::pair<Cidr, std::vector<NextHopThrift>>> u;
+             for (auto& t : upd) {
+               std::vector<NextHopThrift> nhs;
+               for (auto n : t[2].cast<py::list>()) nhs.push_back(nhFromWire(n.cast<py::tuple>()));
+               u.push_back({Cidr{str(t[0]), t[1].cast<int32_t>()}, nhs});
+             }
+             std::vector<Cidr> d;
+             for (auto& t : del) d.push_back(Cidr{str(t[0]), t[1].cast<int32_t>()});
+             s.updateStaticUnicastRoutes(u, d);
+           })
+      .def("update_static_mpls_routes",
+           [](SpfSolver& s, std::vector<py::tuple> upd, std::vector<int32_t> del) {
+             std::vector<std::pair<int32_t, std::vector<NextHopThrift>>> u;
+             for (auto& t : upd) {
+               std::vector<NextHopThrift> nhs;
+               for (auto n : t[1].cast<py::list>()) nhs.push_back(nhFromWire(n.cast<py::tuple>()));
+               u.push_back({t[0].cast<int32_t>(), nhs});
+             }
+             s.updateStaticMplsRoutes(u, del);
+           })
+      .def_property_readonly("route_build_runs", &SpfSolver::routeBuildRuns);
+
+  m.def("device_count", [] {
+    int n = 0;
+    orh_device_count(&n);
+    return n;
+  });
+}

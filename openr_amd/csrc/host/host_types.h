@@ -1,0 +1,168 @@
+// Value types of the drop-in Decision host library (product code).
+//
+// Field-for-field restatements of the thrift structs the path consumes and
+// produces (openr/if/Types.thrift:74-430, Network.thrift:48-131) plus the
+// route-db containers of openr/decision/RibEntry.h and Decision.h:78-119.
+// Hashing follows the reference's containers where iteration order is
+// observable (folly pair hash for PrefixEntries / Link, see hash.h).
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <utility>
+#include <vector>
+
+#include "hash.h"
+
+namespace openr_amd {
+
+using Metric = uint64_t;  // LinkStateMetric (LinkState.h:22)
+using NodeAndArea = std::pair<std::string, std::string>;
+
+struct BinaryAddress {
+  std::string addr;  // 4 or 16 raw bytes
+  std::optional<std::string> ifName;
+  bool operator==(const BinaryAddress& o) const { return addr == o.addr && ifName == o.ifName; }
+  bool operator!=(const BinaryAddress& o) const { return !(*this == o); }
+};
+
+struct Adjacency {
+  std::string otherNodeName, ifName;
+  BinaryAddress nextHopV6, nextHopV4;
+  int32_t metric{0}, adjLabel{0};
+  bool isOverloaded{false};
+  int32_t rtt{0};
+  int64_t timestamp{0}, weight{1};
+  std::string otherIfName;
+};
+
+struct AdjacencyDatabase {
+  std::string thisNodeName;
+  bool isOverloaded{false};
+  std::vector<Adjacency> adjacencies;
+  int32_t nodeLabel{0};
+  std::string area;
+};
+
+struct MetricEntity {
+  int64_t type{0}, priority{0};
+  int32_t op{0};
+  bool isBestPathTieBreaker{false};
+  std::vector<int64_t> metric;
+  bool operator==(const MetricEntity& o) const {
+    return type == o.type && priority == o.priority && op == o.op &&
+        isBestPathTieBreaker == o.isBestPathTieBreaker && metric == o.metric;
+  }
+};
+
+struct MetricVector {
+  int64_t version{0};
+  std::vector<MetricEntity> metrics;
+  bool operator==(const MetricVector& o) const {
+    return version == o.version && metrics == o.metrics;
+  }
+};
+
+enum : int32_t { kPrefixTypeBgp = 3 };
+enum : int32_t { kFwdIp = 0, kFwdSrMpls = 1 };
+enum : int32_t { kAlgoSpEcmp = 0, kAlgoKsp2EdEcmp = 1 };
+enum : int32_t { kPush = 0, kSwap = 1, kPhp = 2, kPopAndLookup = 3 };
+
+struct PrefixEntry {
+  std::string addr;  // masked network bytes
+  int32_t len{0};
+  int32_t type{1};
+  int32_t forwardingType{kFwdIp};
+  int32_t forwardingAlgorithm{kAlgoSpEcmp};
+  std::optional<int64_t> minNexthop;
+  std::optional<int32_t> prependLabel;
+  int32_t pathPreference{0}, sourcePreference{0}, distance{0};
+  std::optional<MetricVector> mv;
+  std::optional<std::string> data;
+  bool operator==(const PrefixEntry& o) const {
+    return addr == o.addr && len == o.len && type == o.type &&
+        forwardingType == o.forwardingType && forwardingAlgorithm == o.forwardingAlgorithm &&
+        minNexthop == o.minNexthop && prependLabel == o.prependLabel &&
+        pathPreference == o.pathPreference && sourcePreference == o.sourcePreference &&
+        distance == o.distance && mv == o.mv && data == o.data;
+  }
+};
+
+struct MplsAction {
+  int32_t action{0};
+  std::optional<int32_t> swapLabel;
+  std::optional<std::vector<int32_t>> pushLabels;
+  bool operator==(const MplsAction& o) const {
+    return action == o.action && swapLabel == o.swapLabel && pushLabels == o.pushLabels;
+  }
+};
+
+struct NextHopThrift {
+  BinaryAddress address;
+  int32_t weight{0};
+  std::optional<MplsAction> mplsAction;
+  int32_t metric{0};
+  std::optional<std::string> area;
+  std::optional<std::string> neighborNodeName;
+  bool operator==(const NextHopThrift& o) const {
+    return address == o.address && weight == o.weight && mplsAction == o.mplsAction &&
+        metric == o.metric && area == o.area && neighborNodeName == o.neighborNodeName;
+  }
+};
+
+struct NextHopHash {
+  size_t operator()(const NextHopThrift& nh) const {
+    size_t h = strHash(nh.address.addr) * 31 + std::hash<int32_t>()(nh.metric);
+    if (nh.address.ifName) h = h * 31 + strHash(*nh.address.ifName);
+    if (nh.mplsAction) {
+      h = h * 31 + static_cast<size_t>(nh.mplsAction->action);
+      if (nh.mplsAction->swapLabel) h = h * 31 + static_cast<size_t>(*nh.mplsAction->swapLabel);
+      if (nh.mplsAction->pushLabels)
+        for (auto l : *nh.mplsAction->pushLabels) h = h * 31 + static_cast<size_t>(l);
+    }
+    return h;
+  }
+};
+
+using NextHopSet = std::unordered_set<NextHopThrift, NextHopHash>;
+using Cidr = std::pair<std::string, int32_t>;  // (masked address bytes, length)
+
+struct CidrHash {
+  size_t operator()(const Cidr& c) const {
+    return hash128to64(strHash(c.first), std::hash<int32_t>()(c.second));
+  }
+};
+
+struct RibUnicastEntry {
+  Cidr prefix;
+  NextHopSet nexthops;
+  std::optional<PrefixEntry> bestPrefixEntry;
+  std::string bestArea;
+  bool doNotInstall{false};
+};
+
+struct RibMplsEntry {
+  int32_t label{0};
+  NextHopSet nexthops;
+};
+
+struct DecisionRouteDb {
+  std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutes;
+  std::unordered_map<int32_t, RibMplsEntry> mplsRoutes;
+};
+
+struct LinkStateChange {
+  bool topologyChanged{false};
+  bool linkAttributesChanged{false};
+  bool nodeLabelChanged{false};
+};
+
+// isMplsLabelValid (openr/common/Util.h:202-205): 20-bit label
+inline bool isMplsLabelValid(int32_t label) {
+  return (static_cast<uint32_t>(label) & 0xfff00000u) == 0;
+}
+
+}  // namespace openr_amd

@@ -1,0 +1,625 @@
+// Drop-in LinkState over libopenr_hip (see link_state.h).
+#include "link_state.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <stdexcept>
+
+namespace openr_amd {
+
+namespace {
+
+void check(orh_ctx* ctx, int rc, const char* what) {
+  if (rc != ORH_OK) {
+    throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) +
+                             "): " + (ctx ? orh_last_error(ctx) : ""));
+  }
+}
+
+uint32_t toDeviceMetric(Metric m) {
+  // the device keeps 32-bit metrics; thrift adjacency metrics are i32, so
+  // only non-positive values (which widen to 0 or > 2^32) are out of range
+  if (m == 0 || m > 0xFFFFFFFFull) {
+    throw std::domain_error("libopenr_hip: link metric " + std::to_string(m) +
+                            " is outside [1, 2^32-1] (zero/negative adjacency metrics are "
+                            "not supported by the device SPF)");
+  }
+  return static_cast<uint32_t>(m);
+}
+
+}  // namespace
+
+orh_ctx* defaultContext() {
+  static std::once_flag once;
+  static orh_ctx* ctx = nullptr;
+  static int rc = ORH_OK;
+  std::call_once(once, [] {
+    int dev = 0;
+    if (const char* e = std::getenv("ORH_DEVICE")) dev = std::atoi(e);
+    rc = orh_create(dev, 0, &ctx);
+  });
+  if (!ctx) {
+    throw std::runtime_error("libopenr_hip: no usable HIP device (orh_create rc=" +
+                             std::to_string(rc) + "); the Decision SPF path requires a GPU");
+  }
+  return ctx;
+}
+
+// ---- HoldableValue (LinkState.cpp:87-121) ---------------------------------
+template <>
+bool Holdable<bool>::update(bool v, Metric upTtl, Metric downTtl) {
+  if (v == val_) return false;
+  if (hasHold()) {
+    held_.reset();
+    ttl_ = 0;
+  } else {
+    ttl_ = (val_ && !v) ? upTtl : downTtl;  // clearing overload brings the link up
+    if (ttl_ != 0) held_ = val_;
+  }
+  val_ = v;
+  return !hasHold();
+}
+
+template <>
+bool Holdable<Metric>::update(Metric v, Metric upTtl, Metric downTtl) {
+  if (v == val_) return false;
+  if (hasHold()) {
+    held_.reset();
+    ttl_ = 0;
+  } else {
+    ttl_ = (v < val_) ? upTtl : downTtl;  // a lower metric brings traffic up
+    if (ttl_ != 0) held_ = val_;
+  }
+  val_ = v;
+  return !hasHold();
+}
+
+bool Link::less(const Link& o) const {
+  if (hash != o.hash) return hash < o.hash;
+  return std::tie(on1, oif1, on2, oif2) < std::tie(o.on1, o.oif1, o.on2, o.oif2);
+}
+
+// ---- construction -------------------------------------------------------
+LinkState::LinkState(const std::string& area, orh_ctx* ctx)
+    : area_(area), ctx_(ctx ? ctx : defaultContext()) {
+  check(ctx_, orh_graph_create(ctx_, &graph_), "orh_graph_create");
+}
+
+LinkState::~LinkState() {
+  if (graph_) orh_graph_destroy(graph_);
+}
+
+uint32_t LinkState::ensureNode(const std::string& n) {
+  auto it = ids_.find(n);
+  if (it != ids_.end()) return it->second;
+  const uint32_t id = static_cast<uint32_t>(names_.size());
+  ids_.emplace(n, id);
+  names_.push_back(n);
+  nodeLinks_.push_back(std::make_unique<LinkSet>(0, LinkIdHash{&links_}));
+  structDirty_ = true;
+  return id;
+}
+
+std::optional<uint32_t> LinkState::nodeId(const std::string& n) const {
+  auto it = ids_.find(n);
+  if (it == ids_.end()) return std::nullopt;
+  return it->second;
+}
+
+LinkState::LinkSet& LinkState::setOf(uint32_t v) { return *nodeLinks_[v]; }
+
+size_t LinkState::numNodes() const {
+  size_t n = 0;  // nodes with a link set entry (linkMap_ keys)
+  for (const auto& s : nodeLinks_) n += s->empty() ? 0 : 1;
+  return n;
+}
+
+std::vector<uint32_t> LinkState::linksFromNode(const std::string& n) const {
+  auto id = nodeId(n);
+  if (!id) return {};
+  return std::vector<uint32_t>(nodeLinks_[*id]->begin(), nodeLinks_[*id]->end());
+}
+
+bool LinkState::isNodeOverloaded(const std::string& n) const {
+  auto it = nodeOverloads_.find(n);
+  return it != nodeOverloads_.end() && it->second.value();
+}
+
+std::optional<Link> LinkState::maybeMakeLink(const std::string& node, const Adjacency& adj) {
+  // bidirectional only (LinkState.cpp:531-547)
+  auto it = adjacencyDatabases_.find(adj.otherNodeName);
+  if (it == adjacencyDatabases_.end()) return std::nullopt;
+  for (const auto& o : it->second.adjacencies) {
+    if (o.otherNodeName != node || adj.otherIfName != o.ifName || adj.ifName != o.otherIfName)
+      continue;
+    Link l;
+    l.area = area_;
+    l.n1 = ensureNode(node);
+    l.n2 = ensureNode(adj.otherNodeName);
+    l.if1 = adj.ifName;
+    l.if2 = o.ifName;
+    l.metric1.reset(static_cast<Metric>(static_cast<int64_t>(adj.metric)));
+    l.metric2.reset(static_cast<Metric>(static_cast<int64_t>(o.metric)));
+    l.overload1.reset(adj.isOverloaded);
+    l.overload2.reset(o.isOverloaded);
+    l.adjLabel1 = adj.adjLabel;
+    l.adjLabel2 = o.adjLabel;
+    l.nhV41 = adj.nextHopV4;
+    l.nhV42 = o.nextHopV4;
+    l.nhV61 = adj.nextHopV6;
+    l.nhV62 = o.nextHopV6;
+    const auto a = std::make_pair(node, adj.ifName);
+    const auto b = std::make_pair(adj.otherNodeName, o.ifName);
+    const auto& lo = (b < a) ? b : a;
+    const auto& hi = (b < a) ? a : b;
+    l.on1 = lo.first;
+    l.oif1 = lo.second;
+    l.on2 = hi.first;
+    l.oif2 = hi.second;
+    l.hash = linkHash(l.on1, l.oif1, l.on2, l.oif2);
+    return l;
+  }
+  return std::nullopt;
+}
+
+uint32_t LinkState::addLink(Link&& l) {  // LinkState.cpp:421-426
+  uint32_t id;
+  if (!freeLinks_.empty()) {
+    id = freeLinks_.back();
+    freeLinks_.pop_back();
+    links_[id] = std::move(l);
+  } else {
+    id = static_cast<uint32_t>(links_.size());
+    links_.push_back(std::move(l));
+  }
+  Link& k = links_[id];
+  k.alive = true;
+  // the reference inserts into firstNodeName()'s set, then secondNodeName()'s
+  const uint32_t first = k.on1 == names_[k.n1] && k.oif1 == k.if1 ? k.n1 : k.n2;
+  const uint32_t second = k.other(first);
+  if (!setOf(first).insert(id).second || !setOf(second).insert(id).second)
+    throw std::logic_error("LinkState: duplicate link");
+  ++nLinks_;
+  structDirty_ = true;
+  return id;
+}
+
+void LinkState::removeLink(uint32_t id) {  // LinkState.cpp:429-434
+  Link& k = links_[id];
+  const uint32_t first = k.on1 == names_[k.n1] && k.oif1 == k.if1 ? k.n1 : k.n2;
+  setOf(first).erase(id);
+  setOf(k.other(first)).erase(id);
+  k.alive = false;
+  freeLinks_.push_back(id);
+  --nLinks_;
+  structDirty_ = true;
+}
+
+void LinkState::removeNode(uint32_t v) {  // LinkState.cpp:436-455
+  std::vector<uint32_t> ids(setOf(v).begin(), setOf(v).end());
+  for (uint32_t id : ids) {
+    setOf(links_[id].other(v)).erase(id);
+    links_[id].alive = false;
+    freeLinks_.push_back(id);
+    --nLinks_;
+  }
+  setOf(v).clear();
+  nodeOverloads_.erase(names_[v]);
+  structDirty_ = true;
+}
+
+std::vector<uint32_t> LinkState::orderedLinks(uint32_t v) const {
+  std::vector<uint32_t> ids(nodeLinks_[v]->begin(), nodeLinks_[v]->end());
+  std::sort(ids.begin(), ids.end(),
+            [&](uint32_t a, uint32_t b) { return links_[a].less(links_[b]); });
+  return ids;
+}
+
+bool LinkState::updateNodeOverloaded(const std::string& n, bool o, Metric up, Metric down) {
+  auto it = nodeOverloads_.find(n);
+  if (it != nodeOverloads_.end()) {
+    const bool before = it->second.value();
+    const bool changed = it->second.update(o, up, down);
+    if (it->second.value() != before) patchNodes_.insert(*nodeId(n));
+    return changed;
+  }
+  nodeOverloads_.emplace(n, Holdable<bool>(o));
+  if (o) patchNodes_.insert(ensureNode(n));
+  return false;  // a new node's overload bit is not a topology change
+}
+
+void LinkState::invalidate(bool topologyChanged) {
+  if (topologyChanged) {
+    spfResults_.clear();
+    kthPaths_.clear();
+  }
+}
+
+// ---- mutators -------------------------------------------------------------
+LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric up,
+                                                   Metric down) {
+  // LinkState.cpp:564-719
+  LinkStateChange change;
+  const std::string& node = db.thisNodeName;
+  const uint32_t v = ensureNode(node);
+  AdjacencyDatabase prior = std::move(adjacencyDatabases_[node]);
+  adjacencyDatabases_[node] = db;
+
+  const std::vector<uint32_t> oldLinks = orderedLinks(v);
+  std::vector<Link> newLinks;
+  for (const auto& adj : db.adjacencies) {
+    if (auto l = maybeMakeLink(node, adj)) newLinks.push_back(std::move(*l));
+  }
+  std::sort(newLinks.begin(), newLinks.end(),
+            [](const Link& a, const Link& b) { return a.less(b); });
+
+  change.topologyChanged |= updateNodeOverloaded(node, db.isOverloaded, up, down);
+  change.nodeLabelChanged = prior.nodeLabel != db.nodeLabel;
+
+  size_t ni = 0, oi = 0;
+  while (ni < newLinks.size() || oi < oldLinks.size()) {
+    if (ni < newLinks.size() && (oi == oldLinks.size() || newLinks[ni].less(links_[oldLinks[oi]]))) {
+      Link& l = newLinks[ni++];
+      l.holdUpTtl = up;
+      change.topologyChanged |= l.isUp();
+      addLink(std::move(l));
+      continue;
+    }
+    if (oi < oldLinks.size() && (ni == newLinks.size() || links_[oldLinks[oi]].less(newLinks[ni]))) {
+      change.topologyChanged |= links_[oldLinks[oi]].isUp();
+      removeLink(oldLinks[oi++]);
+      continue;
+    }
+    const Link& nl = newLinks[ni++];
+    const uint32_t id = oldLinks[oi++];
+    Link& ol = links_[id];
+    const bool side1 = ol.is1(v);
+    const bool nside1 = nl.is1(v);
+    auto& om = side1 ? ol.metric1 : ol.metric2;
+    const Metric nm = nside1 ? nl.metric1.value() : nl.metric2.value();
+    if (nm != om.value()) {
+      change.topologyChanged |= om.update(nm, up, down);
+      patchLinks_.insert(id);
+    }
+    auto& oo = side1 ? ol.overload1 : ol.overload2;
+    const bool no = nside1 ? nl.overload1.value() : nl.overload2.value();
+    if (no != oo.value()) {
+      const bool wasUp = ol.isUp();
+      oo.update(no, up, down);
+      change.topologyChanged |= wasUp != ol.isUp();
+      patchLinks_.insert(id);
+    }
+    const int32_t nlab = nside1 ? nl.adjLabel1 : nl.adjLabel2;
+    if (nlab != ol.adjLabelFrom(v)) {
+      change.linkAttributesChanged = true;
+      (side1 ? ol.adjLabel1 : ol.adjLabel2) = nlab;
+    }
+    const BinaryAddress& n4 = nside1 ? nl.nhV41 : nl.nhV42;
+    if (n4 != ol.nhV4From(v)) {
+      change.linkAttributesChanged = true;
+      (side1 ? ol.nhV41 : ol.nhV42) = n4;
+    }
+    const BinaryAddress& n6 = nside1 ? nl.nhV61 : nl.nhV62;
+    if (n6 != ol.nhV6From(v)) {
+      change.linkAttributesChanged = true;
+      (side1 ? ol.nhV61 : ol.nhV62) = n6;
+    }
+  }
+  invalidate(change.topologyChanged);
+  return change;
+}
+
+LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
+  LinkStateChange c;  // LinkState.cpp:721-738
+  auto it = adjacencyDatabases_.find(node);
+  if (it == adjacencyDatabases_.end()) return c;
+  removeNode(*nodeId(node));
+  adjacencyDatabases_.erase(it);
+  c.topologyChanged = true;
+  invalidate(true);
+  return c;
+}
+
+LinkStateChange LinkState::decrementHolds() {  // LinkState.cpp:500-514
+  LinkStateChange c;
+  for (uint32_t id = 0; id < links_.size(); ++id) {
+    Link& l = links_[id];
+    if (!l.alive) continue;
+    bool expired = false;
+    if (l.holdUpTtl != 0) expired |= (--l.holdUpTtl == 0);
+    expired |= l.metric1.decrementTtl();
+    expired |= l.metric2.decrementTtl();
+    expired |= l.overload1.decrementTtl();
+    expired |= l.overload2.decrementTtl();
+    if (expired) patchLinks_.insert(id);
+    c.topologyChanged |= expired;
+  }
+  for (auto& [name, hv] : nodeOverloads_) {
+    if (hv.decrementTtl()) {
+      c.topologyChanged = true;
+      patchNodes_.insert(*nodeId(name));
+    }
+  }
+  invalidate(c.topologyChanged);
+  return c;
+}
+
+bool LinkState::hasHolds() const {
+  for (const auto& l : links_) {
+    if (l.alive && (l.holdUpTtl != 0 || l.metric1.hasHold() || l.metric2.hasHold() ||
+                    l.overload1.hasHold() || l.overload2.hasHold()))
+      return true;
+  }
+  for (const auto& kv : nodeOverloads_)
+    if (kv.second.hasHold()) return true;
+  return false;
+}
+
+// ---- device mirror -----------------------------------------------------------
+void LinkState::flushMirror() const {
+  const uint32_t N = static_cast<uint32_t>(names_.size());
+  if (structDirty_) {
+    rowPtr_.assign(N + 1, 0);
+    col_.clear();
+    linkOfEntry_.clear();
+    std::vector<uint32_t> wout, win, meta;
+    entriesOfLink_.assign(links_.size(), {0u, 0u});
+    for (uint32_t v = 0; v < N; ++v) {
+      for (uint32_t id : *nodeLinks_[v]) {  // LinkSet iteration order
+        const Link& l = links_[id];
+        const uint32_t u = l.other(v);
+        const uint32_t e = static_cast<uint32_t>(col_.size());
+        col_.push_back(u);
+        linkOfEntry_.push_back(id);
+        const bool up = l.isUp();
+        wout.push_back(up ? toDeviceMetric(l.metricFrom(v)) : 1u);
+        win.push_back(up ? toDeviceMetric(l.metricFrom(u)) : 1u);
+        meta.push_back(id | (up ? 0u : ORH_META_DOWN));
+        auto& eo = entriesOfLink_[id];
+        (l.is1(v) ? eo.first : eo.second) = e;
+      }
+      rowPtr_[v + 1] = static_cast<uint32_t>(col_.size());
+    }
+    std::vector<uint8_t> ovl(N, 0);
+    for (uint32_t v = 0; v < N; ++v) ovl[v] = isNodeOverloaded(names_[v]) ? 1 : 0;
+    orh_csr c{};
+    c.n_nodes = N;
+    c.n_edges = static_cast<uint32_t>(col_.size());
+    c.n_links = static_cast<uint32_t>(links_.size());
+    c.row_ptr = rowPtr_.data();
+    c.col = col_.data();
+    c.w_out = wout.data();
+    c.w_in = win.data();
+    c.meta = meta.data();
+    c.node_overloaded = ovl.data();
+    check(ctx_, orh_graph_load(graph_, &c), "orh_graph_load");
+    structDirty_ = false;
+    patchLinks_.clear();
+    patchNodes_.clear();
+    return;
+  }
+  if (!patchLinks_.empty()) {
+    std::vector<uint32_t> idx, wout, win, meta;
+    for (uint32_t id : patchLinks_) {
+      const Link& l = links_[id];
+      if (!l.alive) continue;
+      const bool up = l.isUp();
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t v = s == 0 ? l.n1 : l.n2;
+        const uint32_t e = s == 0 ? entriesOfLink_[id].first : entriesOfLink_[id].second;
+        idx.push_back(e);
+        wout.push_back(up ? toDeviceMetric(l.metricFrom(v)) : 1u);
+        win.push_back(up ? toDeviceMetric(l.metricFrom(l.other(v))) : 1u);
+        meta.push_back(id | (up ? 0u : ORH_META_DOWN));
+      }
+    }
+    check(ctx_, orh_graph_patch_edges(graph_, static_cast<uint32_t>(idx.size()), idx.data(),
+                                      wout.data(), win.data(), meta.data()),
+          "orh_graph_patch_edges");
+    patchLinks_.clear();
+  }
+  if (!patchNodes_.empty()) {
+    std::vector<uint32_t> idx;
+    std::vector<uint8_t> ovl;
+    for (uint32_t v : patchNodes_) {
+      idx.push_back(v);
+      ovl.push_back(isNodeOverloaded(names_[v]) ? 1 : 0);
+    }
+    check(ctx_, orh_graph_patch_nodes(graph_, static_cast<uint32_t>(idx.size()), idx.data(),
+                                      ovl.data()),
+          "orh_graph_patch_nodes");
+    patchNodes_.clear();
+  }
+}
+
+orh_graph* LinkState::deviceGraph() const {
+  flushMirror();
+  return graph_;
+}
+
+SpfRow LinkState::spfOnDevice(uint32_t src, bool useLinkMetric,
+                              const std::vector<uint32_t>* ignore) const {
+  flushMirror();
+  SpfRow row;
+  row.srcName = names_[src];
+  row.src = src;
+  row.known = true;
+  row.useLinkMetric = useLinkMetric;
+  check(ctx_, orh_spf_words(graph_, &src, 1, &row.words), "orh_spf_words");
+  const uint32_t N = static_cast<uint32_t>(names_.size());
+  row.dist.resize(N);
+  row.nh.resize(static_cast<size_t>(N) * row.words);
+  uint32_t ptr[2] = {0, ignore ? static_cast<uint32_t>(ignore->size()) : 0u};
+  orh_spf_request req{};
+  req.h_srcs = &src;
+  req.n_src = 1;
+  req.use_link_metric = useLinkMetric ? 1 : 0;
+  if (ignore && !ignore->empty()) {
+    req.h_ignore_ptr = ptr;
+    req.h_ignore_links = ignore->data();
+  }
+  check(ctx_, orh_spf_batch(graph_, &req, row.words, row.dist.data(), row.nh.data()),
+        "orh_spf_batch");
+  uint32_t n = 0;
+  check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &n), "orh_graph_neighbors");
+  row.nbrs.resize(n);
+  check(ctx_, orh_graph_neighbors(graph_, src, row.nbrs.data(), n, &n), "orh_graph_neighbors");
+  ++spfRuns_;
+  return row;
+}
+
+const SpfRow& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) const {
+  auto key = std::make_pair(node, useLinkMetric);
+  auto it = spfResults_.find(key);
+  if (it != spfResults_.end()) return it->second;
+  auto id = nodeId(node);
+  SpfRow row;
+  if (id) {
+    row = spfOnDevice(*id, useLinkMetric, nullptr);
+  } else {
+    // unknown source: the reference result holds only the source itself
+    row.srcName = node;
+    row.known = false;
+    row.useLinkMetric = useLinkMetric;
+    ++spfRuns_;
+  }
+  return spfResults_.emplace(key, std::move(row)).first->second;
+}
+
+SpfRow LinkState::runSpf(const std::string& node, bool useLinkMetric,
+                         const std::vector<uint32_t>& ignore) const {
+  auto id = nodeId(node);
+  if (!id) {
+    SpfRow row;
+    row.srcName = node;
+    row.useLinkMetric = useLinkMetric;
+    ++spfRuns_;
+    return row;
+  }
+  return spfOnDevice(*id, useLinkMetric, &ignore);
+}
+
+std::optional<Metric> LinkState::getMetricFromAToB(const std::string& a, const std::string& b,
+                                                   bool useLinkMetric) const {
+  if (a == b) return 0;  // LinkState.cpp:740-751
+  const SpfRow& row = getSpfResult(a, useLinkMetric);
+  auto id = nodeId(b);
+  if (!id || !row.reachable(*id)) return std::nullopt;
+  return row.metric(*id);
+}
+
+Metric LinkState::getMaxHopsToNode(const std::string& node) const {
+  const SpfRow& row = getSpfResult(node, false);  // LinkState.cpp:753-760
+  Metric mx = 0;
+  if (!row.known) return 0;
+  for (uint32_t d : row.dist)
+    if (d != ORH_UNREACHABLE) mx = std::max<Metric>(mx, d);
+  return mx;
+}
+
+// ---- K-shortest edge-disjoint paths -----------------------------------------
+std::vector<std::pair<uint32_t, uint32_t>> LinkState::pathLinks(
+    const SpfRow& row, uint32_t v, const std::unordered_set<uint32_t>* ignore) const {
+  // predecessors (link, prev) of v in the order runSpf appends them: by
+  // extraction order of prev = (dist, name) for metrics >= 1, then prev's
+  // LinkSet iteration order (LinkState.cpp:821-873)
+  struct Cand {
+    uint32_t dist;
+    const std::string* name;
+    uint32_t pos;
+    uint32_t link;
+    uint32_t prev;
+  };
+  std::vector<Cand> cands;
+  if (!row.reachable(v) || v == row.src) return {};
+  for (uint32_t id : *nodeLinks_[v]) {
+    const Link& l = links_[id];
+    if (!l.isUp() || (ignore && ignore->count(id))) continue;
+    const uint32_t u = l.other(v);
+    if (!row.reachable(u)) continue;
+    if (u != row.src && isNodeOverloaded(names_[u])) continue;
+    const Metric w = row.useLinkMetric ? l.metricFrom(u) : 1;
+    if (static_cast<Metric>(row.dist[u]) + w != row.dist[v]) continue;
+    uint32_t pos = 0;
+    for (uint32_t x : *nodeLinks_[u]) {
+      if (x == id) break;
+      ++pos;
+    }
+    cands.push_back({row.dist[u], &names_[u], pos, id, u});
+  }
+  std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
+    if (a.dist != b.dist) return a.dist < b.dist;
+    if (*a.name != *b.name) return *a.name < *b.name;
+    return a.pos < b.pos;
+  });
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  for (const auto& c : cands) out.emplace_back(c.link, c.prev);
+  return out;
+}
+
+std::optional<Path> LinkState::traceOnePath(uint32_t src, uint32_t dst, const SpfRow& row,
+                                            std::unordered_set<uint32_t>& visited,
+                                            const std::unordered_set<uint32_t>* ignore) const {
+  // greedy DFS dst -> src; a link is consumed on first touch (LinkState.cpp:398-419)
+  if (src == dst) return Path{};
+  for (const auto& [lid, prev] : pathLinks(row, dst, ignore)) {
+    if (visited.insert(lid).second) {
+      auto p = traceOnePath(src, prev, row, visited, ignore);
+      if (p) {
+        p->push_back(lid);
+        return p;
+      }
+    }
+  }
+  return std::nullopt;
+}
+
+const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
+                                                size_t k) const {
+  if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");
+  auto key = std::make_tuple(src, dst, k);
+  auto it = kthPaths_.find(key);
+  if (it != kthPaths_.end()) return it->second;
+
+  std::unordered_set<uint32_t> ignore;
+  for (size_t i = 1; i < k; ++i)
+    for (const auto& p : getKthPaths(src, dst, i))
+      for (uint32_t lid : p) ignore.insert(lid);
+
+  std::vector<Path> paths;
+  SpfRow fresh;
+  const SpfRow* row;
+  if (ignore.empty()) {
+    row = &getSpfResult(src, true);
+  } else {
+    std::vector<uint32_t> ign(ignore.begin(), ignore.end());
+    fresh = runSpf(src, true, ign);
+    row = &fresh;
+  }
+  auto s = nodeId(src);
+  auto d = nodeId(dst);
+  const bool hasDst = (src == dst) || (s && d && row->reachable(*d));
+  if (hasDst && s && d) {
+    std::unordered_set<uint32_t> visited;
+    const auto* ign = ignore.empty() ? nullptr : &ignore;
+    auto p = traceOnePath(*s, *d, *row, visited, ign);
+    while (p && !p->empty()) {
+      paths.push_back(std::move(*p));
+      p = traceOnePath(*s, *d, *row, visited, ign);
+    }
+  }
+  return kthPaths_.emplace(key, std::move(paths)).first->second;
+}
+
+bool LinkState::pathAInPathB(const Path& a, const Path& b) {  // LinkState.h:395-410
+  if (a.size() > b.size()) return false;
+  for (size_t i = 0; i + a.size() <= b.size(); ++i) {
+    size_t k = 0;
+    while (k < a.size() && a[k] == b[i + k]) ++k;
+    if (k == a.size()) return true;
+  }
+  return false;
+}
+
+}  // namespace openr_amd

@@ -1,0 +1,226 @@
+// Drop-in LinkState for the OpenR Decision module, backed by libopenr_hip.
+//
+// Public behaviour follows openr/decision/LinkState.h:177-469:
+//   updateAdjacencyDatabase / deleteAdjacencyDatabase / decrementHolds with
+//   the same LinkStateChange flags, bidirectional-link rule, ordered-FIB
+//   holds and memo invalidation; getSpfResult / getKthPaths /
+//   getMetricFromAToB / getMaxHopsToNode with the same results.
+//
+// What differs is where the SPF runs: the host keeps the graph store with
+// dense node / link ids and mirrors it into a device CSR (orh_graph); every
+// SPF (memoized per source, or fresh with links ignored for KSP2) is an
+// orh_spf_* call on the GPU. The host never runs Dijkstra. Attribute-only
+// changes (metric, overload, holds) are applied to the mirror as in-place
+// patches; structural changes (links added or removed) re-upload it.
+//
+// Per-node link sets are std::unordered_set<link id> hashed with the
+// reference Link::hash, so their iteration order -- which the reference's
+// KSP2 trace depends on (LinkState.cpp:844, :398-419) -- is reproduced.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <optional>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../../include/openr_hip.h"
+#include "host_types.h"
+
+namespace openr_amd {
+
+// process-wide libopenr_hip context of the device this process drives
+// (ORH_DEVICE env or device 0); throws if no GPU is available
+orh_ctx* defaultContext();
+
+template <class T>
+class Holdable {  // HoldableValue, LinkState.h:36-58
+ public:
+  explicit Holdable(T v) : val_(v) {}
+  void reset(T v) {
+    val_ = v;
+    held_.reset();
+    ttl_ = 0;
+  }
+  const T& value() const { return held_ ? *held_ : val_; }
+  bool hasHold() const { return held_.has_value(); }
+  bool decrementTtl() {
+    if (held_ && --ttl_ == 0) {
+      held_.reset();
+      return true;
+    }
+    return false;
+  }
+  bool update(T v, Metric upTtl, Metric downTtl);
+
+ private:
+  T val_;
+  std::optional<T> held_;
+  Metric ttl_{0};
+};
+
+struct Link {
+  std::string area;
+  uint32_t n1{0}, n2{0};  // node ids of the constructor's (nodeName1, nodeName2)
+  std::string if1, if2;
+  Holdable<Metric> metric1{1}, metric2{1};
+  Holdable<bool> overload1{false}, overload2{false};
+  int32_t adjLabel1{0}, adjLabel2{0};
+  BinaryAddress nhV41, nhV42, nhV61, nhV62;
+  Metric holdUpTtl{0};
+  // orderedNames_ = minmax((name1, if1), (name2, if2))
+  std::string on1, oif1, on2, oif2;
+  size_t hash{0};
+  bool alive{false};
+
+  bool isUp() const { return holdUpTtl == 0 && !overload1.value() && !overload2.value(); }
+  bool is1(uint32_t node) const { return node == n1; }
+  uint32_t other(uint32_t node) const { return node == n1 ? n2 : n1; }
+  const std::string& ifFrom(uint32_t node) const { return is1(node) ? if1 : if2; }
+  Metric metricFrom(uint32_t node) const {
+    return is1(node) ? metric1.value() : metric2.value();
+  }
+  int32_t adjLabelFrom(uint32_t node) const { return is1(node) ? adjLabel1 : adjLabel2; }
+  bool overloadFrom(uint32_t node) const {
+    return is1(node) ? overload1.value() : overload2.value();
+  }
+  const BinaryAddress& nhV4From(uint32_t node) const { return is1(node) ? nhV41 : nhV42; }
+  const BinaryAddress& nhV6From(uint32_t node) const { return is1(node) ? nhV61 : nhV62; }
+  bool less(const Link& o) const;  // Link::operator< (LinkState.cpp:347-353)
+  bool same(const Link& o) const {
+    return hash == o.hash && on1 == o.on1 && oif1 == o.oif1 && on2 == o.on2 && oif2 == o.oif2;
+  }
+};
+
+using Path = std::vector<uint32_t>;  // link ids, src -> dst
+
+// One source's SPF result as produced by the device: dist row + first-hop
+// bitmask row over the source's distinct neighbours (orh_graph_neighbors).
+struct SpfRow {
+  std::string srcName;
+  uint32_t src{0};
+  bool known{false};  // src has a node id in this area
+  bool useLinkMetric{true};
+  uint32_t words{1};
+  std::vector<uint32_t> dist;  // ORH_UNREACHABLE when absent
+  std::vector<uint32_t> nh;    // [N * words]
+  std::vector<uint32_t> nbrs;  // bit k <-> node id nbrs[k]
+
+  bool reachable(uint32_t v) const { return known && v < dist.size() && dist[v] != ORH_UNREACHABLE; }
+  Metric metric(uint32_t v) const { return dist[v]; }
+  template <class F>
+  void forEachNextHop(uint32_t v, F&& f) const {
+    for (uint32_t k = 0; k < words; ++k) {
+      uint32_t m = nh[static_cast<size_t>(v) * words + k];
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1;
+        f(nbrs[k * 32 + b]);
+      }
+    }
+  }
+};
+
+class LinkState {
+ public:
+  explicit LinkState(const std::string& area, orh_ctx* ctx = nullptr);
+  ~LinkState();
+  LinkState(LinkState&&) = delete;
+  LinkState(const LinkState&) = delete;
+
+  const std::string& getArea() const { return area_; }
+
+  LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl = 0,
+                                          Metric holdDownTtl = 0);
+  LinkStateChange deleteAdjacencyDatabase(const std::string& node);
+  LinkStateChange decrementHolds();
+  bool hasHolds() const;
+
+  // memoized SPF from `node` (LinkState.cpp:793-803)
+  const SpfRow& getSpfResult(const std::string& node, bool useLinkMetric = true) const;
+  // fresh SPF with links ignored (runSpf(src, true, linksToIgnore))
+  SpfRow runSpf(const std::string& node, bool useLinkMetric,
+                const std::vector<uint32_t>& ignoreLinks) const;
+  const std::vector<Path>& getKthPaths(const std::string& src, const std::string& dst,
+                                       size_t k) const;
+  std::optional<Metric> getMetricFromAToB(const std::string& a, const std::string& b,
+                                          bool useLinkMetric = true) const;
+  Metric getMaxHopsToNode(const std::string& node) const;
+
+  // pathLinks of `v` in `row` in the reference's insertion order
+  std::vector<std::pair<uint32_t, uint32_t>> pathLinks(
+      const SpfRow& row, uint32_t v, const std::unordered_set<uint32_t>* ignore = nullptr) const;
+  static bool pathAInPathB(const Path& a, const Path& b);
+
+  bool hasNode(const std::string& n) const { return adjacencyDatabases_.count(n) != 0; }
+  bool isNodeOverloaded(const std::string& n) const;
+  std::optional<uint32_t> nodeId(const std::string& n) const;
+  const std::string& nodeName(uint32_t id) const { return names_[id]; }
+  uint32_t numNodeIds() const { return static_cast<uint32_t>(names_.size()); }
+  std::vector<uint32_t> linksFromNode(const std::string& n) const;  // LinkSet order
+  const Link& link(uint32_t id) const { return links_[id]; }
+  size_t numLinks() const { return nLinks_; }
+  size_t numNodes() const;
+  const std::unordered_map<std::string, AdjacencyDatabase>& getAdjacencyDatabases() const {
+    return adjacencyDatabases_;
+  }
+  uint64_t spfRuns() const { return spfRuns_; }
+
+  // device mirror access (bench / batch callers)
+  orh_graph* deviceGraph() const;  // flushes pending deltas first
+  orh_ctx* context() const { return ctx_; }
+
+ private:
+  struct LinkIdHash {
+    const std::vector<Link>* links;
+    size_t operator()(uint32_t id) const { return (*links)[id].hash; }
+  };
+  using LinkSet = std::unordered_set<uint32_t, LinkIdHash>;
+
+  uint32_t ensureNode(const std::string& n);
+  std::optional<Link> maybeMakeLink(const std::string& node, const Adjacency& adj);
+  uint32_t addLink(Link&& l);
+  void removeLink(uint32_t id);
+  void removeNode(uint32_t v);
+  bool updateNodeOverloaded(const std::string& n, bool o, Metric up, Metric down);
+  std::vector<uint32_t> orderedLinks(uint32_t v) const;
+  LinkSet& setOf(uint32_t v);
+  void invalidate(bool topologyChanged);
+  void flushMirror() const;
+  SpfRow spfOnDevice(uint32_t src, bool useLinkMetric,
+                     const std::vector<uint32_t>* ignore) const;
+  std::optional<Path> traceOnePath(uint32_t src, uint32_t dst, const SpfRow& row,
+                                   std::unordered_set<uint32_t>& visited,
+                                   const std::unordered_set<uint32_t>* ignore) const;
+
+  std::string area_;
+  orh_ctx* ctx_;
+  mutable orh_graph* graph_{nullptr};
+
+  std::unordered_map<std::string, uint32_t> ids_;
+  std::vector<std::string> names_;
+  std::vector<Link> links_;
+  std::vector<uint32_t> freeLinks_;
+  size_t nLinks_{0};
+  std::vector<std::unique_ptr<LinkSet>> nodeLinks_;
+  std::unordered_map<std::string, Holdable<bool>> nodeOverloads_;
+  std::unordered_map<std::string, AdjacencyDatabase> adjacencyDatabases_;
+
+  // device mirror bookkeeping
+  mutable bool structDirty_{true};
+  mutable std::unordered_set<uint32_t> patchLinks_;
+  mutable std::unordered_set<uint32_t> patchNodes_;
+  mutable std::vector<uint32_t> rowPtr_;  // host copy of the uploaded CSR
+  mutable std::vector<uint32_t> col_, linkOfEntry_;
+  mutable std::vector<std::pair<uint32_t, uint32_t>> entriesOfLink_;
+
+  // memo (LinkState.h:279-301)
+  mutable std::map<std::pair<std::string, bool>, SpfRow> spfResults_;
+  mutable std::map<std::tuple<std::string, std::string, size_t>, std::vector<Path>> kthPaths_;
+  mutable uint64_t spfRuns_{0};
+};
+
+}  // namespace openr_amd

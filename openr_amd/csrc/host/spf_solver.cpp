@@ -1,0 +1,638 @@
+// Drop-in SpfSolver / PrefixState over device SPF rows (see spf_solver.h).
+#include "spf_solver.h"
+
+#include <algorithm>
+#include <limits>
+#include <list>
+#include <stdexcept>
+#include <tuple>
+
+namespace openr_amd {
+
+namespace {
+
+MplsAction mpls(int32_t code, std::optional<int32_t> swap = std::nullopt,
+                std::optional<std::vector<int32_t>> push = std::nullopt) {
+  // createMplsAction + checkMplsAction (Util.cpp:482-512, :793-803)
+  if (code == kPush && (!push || push->empty())) throw std::logic_error("PUSH without labels");
+  if (code == kSwap && (!swap || !isMplsLabelValid(*swap))) throw std::logic_error("bad SWAP");
+  if (push)
+    for (int32_t l : *push)
+      if (!isMplsLabelValid(l)) throw std::logic_error("bad PUSH label");
+  return MplsAction{code, swap, std::move(push)};
+}
+
+NextHopThrift nextHop(const BinaryAddress& addr, std::optional<std::string> ifName,
+                      int32_t metric, std::optional<MplsAction> action,
+                      std::optional<std::string> area, std::optional<std::string> nbr) {
+  NextHopThrift nh;  // createNextHop (Util.cpp:775-789): metric is int32
+  nh.address.addr = addr.addr;
+  nh.address.ifName = std::move(ifName);
+  nh.metric = metric;
+  nh.mplsAction = std::move(action);
+  nh.area = std::move(area);
+  nh.neighborNodeName = std::move(nbr);
+  return nh;
+}
+
+// SpfResult::count(name) on a device row
+bool rowHas(const LinkState& ls, const SpfRow& row, const std::string& name) {
+  if (name == row.srcName) return true;
+  auto id = ls.nodeId(name);
+  return id && row.reachable(*id);
+}
+
+std::optional<Metric> rowMetric(const LinkState& ls, const SpfRow& row, const std::string& name) {
+  if (name == row.srcName) return 0;
+  auto id = ls.nodeId(name);
+  if (!id || !row.reachable(*id)) return std::nullopt;
+  return row.metric(*id);
+}
+
+bool maskHas(const SpfRow& row, const std::vector<uint32_t>& mask, uint32_t nbr) {
+  auto it = std::lower_bound(row.nbrs.begin(), row.nbrs.end(), nbr);
+  if (it == row.nbrs.end() || *it != nbr) return false;
+  const size_t k = static_cast<size_t>(it - row.nbrs.begin());
+  return (mask[k >> 5] >> (k & 31)) & 1u;
+}
+
+enum class Cmp { kWinner, kTieWinner, kTie, kTieLooser, kLooser, kError };
+
+Cmp invert(Cmp c) {
+  switch (c) {
+    case Cmp::kWinner: return Cmp::kLooser;
+    case Cmp::kTieWinner: return Cmp::kTieLooser;
+    case Cmp::kTie: return Cmp::kTie;
+    case Cmp::kTieLooser: return Cmp::kTieWinner;
+    case Cmp::kLooser: return Cmp::kWinner;
+    default: return Cmp::kError;
+  }
+}
+bool decisive(Cmp c) { return c == Cmp::kWinner || c == Cmp::kLooser || c == Cmp::kError; }
+Cmp loner(const MetricEntity& e) {
+  if (e.op == 1) return e.isBestPathTieBreaker ? Cmp::kTieWinner : Cmp::kWinner;
+  if (e.op == 2) return e.isBestPathTieBreaker ? Cmp::kTieLooser : Cmp::kLooser;
+  return Cmp::kTie;
+}
+
+// MetricVectorUtils::compareMetricVectors (Util.cpp:1044-1094)
+Cmp compareMv(MetricVector l, MetricVector r) {
+  if (l.version != r.version) return Cmp::kError;
+  auto prio = [](const MetricEntity& a, const MetricEntity& b) { return a.priority > b.priority; };
+  if (!std::is_sorted(l.metrics.begin(), l.metrics.end(), prio))
+    std::sort(l.metrics.begin(), l.metrics.end(), prio);
+  if (!std::is_sorted(r.metrics.begin(), r.metrics.end(), prio))
+    std::sort(r.metrics.begin(), r.metrics.end(), prio);
+  Cmp res = Cmp::kTie;
+  auto upd = [&](Cmp u) {
+    if (decisive(u) || res == Cmp::kTie) res = u;
+  };
+  size_t i = 0, j = 0;
+  while (!decisive(res) && i < l.metrics.size() && j < r.metrics.size()) {
+    const auto& a = l.metrics[i];
+    const auto& b = r.metrics[j];
+    if (a.type == b.type) {
+      if (a.isBestPathTieBreaker != b.isBestPathTieBreaker) {
+        upd(Cmp::kError);
+      } else if (a.metric.size() != b.metric.size()) {
+        upd(Cmp::kError);
+      } else {
+        Cmp c = Cmp::kTie;
+        for (size_t k = 0; k < a.metric.size(); ++k) {
+          if (a.metric[k] != b.metric[k]) {
+            const bool win = a.metric[k] > b.metric[k];
+            c = a.isBestPathTieBreaker ? (win ? Cmp::kTieWinner : Cmp::kTieLooser)
+                                       : (win ? Cmp::kWinner : Cmp::kLooser);
+            break;
+          }
+        }
+        upd(c);
+      }
+      ++i;
+      ++j;
+    } else if (a.priority > b.priority) {
+      upd(loner(a));
+      ++i;
+    } else if (a.priority < b.priority) {
+      upd(invert(loner(b)));
+      ++j;
+    } else {
+      upd(Cmp::kError);
+    }
+  }
+  while (!decisive(res) && i < l.metrics.size()) upd(loner(l.metrics[i++]));
+  while (!decisive(res) && j < r.metrics.size()) upd(invert(loner(r.metrics[j++])));
+  return res;
+}
+
+}  // namespace
+
+// ---- PrefixState (PrefixState.cpp:17-56) ------------------------------------
+std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
+                                            const PrefixEntry& e) {
+  Cidr key{e.addr, e.len};
+  auto [it, inserted] = prefixes_[key].emplace(NodeAndArea{node, area}, e);
+  if (!inserted && it->second == e) return {};
+  if (!inserted) it->second = e;
+  return {key};
+}
+
+std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::string& area,
+                                            const Cidr& prefix) {
+  auto it = prefixes_.find(prefix);
+  if (it == prefixes_.end() || !it->second.erase(NodeAndArea{node, area})) return {};
+  if (it->second.empty()) prefixes_.erase(it);
+  return {prefix};
+}
+
+// ---- SpfSolver ----------------------------------------------------------------
+SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool enableOrderedFib, bool bgpDryRun,
+                     bool enableBestRouteSelection)
+    : myNodeName_(me),
+      enableV4_(enableV4),
+      enableOrderedFib_(enableOrderedFib),
+      bgpDryRun_(bgpDryRun),
+      enableBestRouteSelection_(enableBestRouteSelection) {}
+
+void SpfSolver::updateStaticUnicastRoutes(
+    const std::vector<std::pair<Cidr, std::vector<NextHopThrift>>>& upd,
+    const std::vector<Cidr>& del) {
+  for (const auto& [p, nhs] : upd) staticUnicastRoutes_[p] = nhs;
+  for (const auto& p : del) staticUnicastRoutes_.erase(p);
+}
+
+void SpfSolver::updateStaticMplsRoutes(
+    const std::vector<std::pair<int32_t, std::vector<NextHopThrift>>>& upd,
+    const std::vector<int32_t>& del) {
+  for (const auto& [l, nhs] : upd) staticMplsRoutes_[l] = nhs;
+  for (int32_t l : del) staticMplsRoutes_.erase(l);
+}
+
+std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps, const Cidr& prefix) {
+  if (auto r = createRouteForPrefix(me, als, ps, prefix)) return r;
+  auto it = staticUnicastRoutes_.find(prefix);
+  if (it == staticUnicastRoutes_.end()) return std::nullopt;
+  RibUnicastEntry e;
+  e.prefix = prefix;
+  e.nexthops.insert(it->second.begin(), it->second.end());
+  return e;
+}
+
+std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string& me,
+                                                               const AreaLinkStates& als,
+                                                               const PrefixState& ps,
+                                                               const Cidr& prefix) {
+  // Decision.cpp:445-613
+  auto search = ps.prefixes().find(prefix);
+  if (search == ps.prefixes().end()) return std::nullopt;
+  PrefixEntries entries = search->second;
+  for (const auto& [area, ls] : als) {
+    const SpfRow& row = ls.getSpfResult(me);
+    for (auto it = entries.begin(); it != entries.end();) {
+      if (area != it->first.second || rowHas(ls, row, it->first.first)) {
+        ++it;
+      } else {
+        it = entries.erase(it);
+      }
+    }
+  }
+  if (entries.empty()) return std::nullopt;
+  if (prefix.first.size() == 4 && !enableV4_) return std::nullopt;
+
+  bool hasBgp = false, hasNonBgp = false, missingMv = false, selfPrepend = true;
+  for (const auto& [na, e] : entries) {
+    const bool bgp = e.type == kPrefixTypeBgp;
+    hasBgp |= bgp;
+    hasNonBgp |= !bgp;
+    if (na.first == me) selfPrepend &= e.prependLabel.has_value();
+    if (bgp && !e.mv) missingMv = true;
+  }
+  if (hasBgp && ((hasNonBgp && !enableBestRouteSelection_) || missingMv)) return std::nullopt;
+
+  const auto best = selectBestRoutes(me, entries, hasBgp, als);
+  if (!best.success || best.allNodeAreas.empty()) return std::nullopt;
+  if (best.hasNode(me) && !selfPrepend) return std::nullopt;
+
+  // getPrefixForwardingTypeAndAlgorithm (Util.cpp:452-480)
+  int32_t ft = kFwdSrMpls, fa = kAlgoKsp2EdEcmp;
+  for (const auto& [na, e] : entries) {
+    if (!best.allNodeAreas.count(na)) continue;
+    ft = std::min(ft, e.forwardingType);
+    fa = std::min(fa, e.forwardingAlgorithm);
+    if (ft == kFwdIp && fa == kAlgoSpEcmp) break;
+  }
+  if (fa == kAlgoSpEcmp) return selectBestPathsSpf(me, prefix, best, entries, hasBgp, ft, als);
+  if (fa == kAlgoKsp2EdEcmp) return selectBestPathsKsp2(me, prefix, best, entries, hasBgp, ft, als);
+  return std::nullopt;
+}
+
+BestRouteSelectionResult SpfSolver::filterDrained(BestRouteSelectionResult&& r,
+                                                  const AreaLinkStates& als) const {
+  BestRouteSelectionResult f = r;  // maybeFilterDrainedNodes, Decision.cpp:840-862
+  for (auto it = f.allNodeAreas.begin(); it != f.allNodeAreas.end();) {
+    if (als.at(it->second).isNodeOverloaded(it->first)) {
+      it = f.allNodeAreas.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  if (!f.allNodeAreas.empty() && f.bestNodeArea != r.bestNodeArea)
+    f.bestNodeArea = *f.allNodeAreas.begin();
+  return f.allNodeAreas.empty() ? std::move(r) : std::move(f);
+}
+
+BestRouteSelectionResult SpfSolver::selectBestRoutes(const std::string& me,
+                                                     const PrefixEntries& entries, bool isBgp,
+                                                     const AreaLinkStates& als) const {
+  BestRouteSelectionResult r;  // Decision.cpp:794-822
+  if (enableBestRouteSelection_) {
+    // selectBestPrefixMetrics (Util.h:491-526): max (path_pref, source_pref, -distance)
+    std::tuple<int32_t, int32_t, int32_t> best{std::numeric_limits<int32_t>::min(),
+                                               std::numeric_limits<int32_t>::min(),
+                                               std::numeric_limits<int32_t>::min()};
+    for (const auto& [na, e] : entries) {
+      std::tuple<int32_t, int32_t, int32_t> t{
+          e.pathPreference, e.sourcePreference,
+          static_cast<int32_t>(0u - static_cast<uint32_t>(e.distance))};
+      if (t < best) continue;
+      if (t > best) {
+        best = t;
+        r.allNodeAreas.clear();
+      }
+      r.allNodeAreas.insert(na);
+    }
+    r.bestNodeArea = *r.allNodeAreas.begin();  // selectBestNodeArea (Util.cpp:902-913)
+    for (const auto& na : r.allNodeAreas) {
+      if (na.first == me) {
+        r.bestNodeArea = na;
+        break;
+      }
+    }
+    r.success = true;
+  } else if (isBgp) {
+    r = runBestPathSelectionBgp(entries, als);
+  } else {
+    for (const auto& [na, _] : entries) r.allNodeAreas.insert(na);
+    r.bestNodeArea = *r.allNodeAreas.begin();
+    r.success = true;
+  }
+  return filterDrained(std::move(r), als);
+}
+
+BestRouteSelectionResult SpfSolver::runBestPathSelectionBgp(const PrefixEntries& entries,
+                                                            const AreaLinkStates& als) const {
+  BestRouteSelectionResult r;  // Decision.cpp:864-902
+  std::optional<MetricVector> bestVector;
+  for (const auto& [na, e] : entries) {
+    const Cmp c = bestVector ? compareMv(*e.mv, *bestVector) : Cmp::kWinner;
+    if (c == Cmp::kTie || c == Cmp::kError) return r;
+    if (c == Cmp::kWinner) r.allNodeAreas.clear();
+    if (c == Cmp::kWinner || c == Cmp::kTieWinner) {
+      bestVector = e.mv;
+      r.bestNodeArea = na;
+    }
+    if (c != Cmp::kLooser) r.allNodeAreas.insert(na);
+  }
+  r.success = true;
+  return filterDrained(std::move(r), als);
+}
+
+bool SpfSolver::fastSpEcmp(const std::string& me, const LinkState& ls, const std::string& area,
+                           const std::set<NodeAndArea>& dsts, bool isV4,
+                           std::optional<int32_t> swapLabel, NextHopSet& out) const {
+  // getMinCostNodes + getNextHopsWithMetric + getNextHopsThrift for one area
+  // and non-per-destination forwarding (Decision.cpp:1152-1334) on the row:
+  // min over advertisers, OR of first-hop masks, then my links whose metric
+  // equals the distance to their neighbour.
+  const SpfRow& row = ls.getSpfResult(me);
+  Metric shortest = std::numeric_limits<Metric>::max();
+  std::vector<uint32_t> mask(row.words, 0u);
+  bool any = false;
+  for (const auto& [dst, _] : dsts) {
+    auto id = ls.nodeId(dst);
+    if (!row.known || !id || !row.reachable(*id)) continue;
+    const Metric d = row.metric(*id);
+    if (d > shortest) continue;
+    if (d < shortest) {
+      shortest = d;
+      std::fill(mask.begin(), mask.end(), 0u);
+    }
+    any = true;
+    for (uint32_t k = 0; k < row.words; ++k) mask[k] |= row.nh[static_cast<size_t>(*id) * row.words + k];
+  }
+  bool nonEmpty = false;
+  for (uint32_t m : mask) nonEmpty |= m != 0;
+  if (!any || !nonEmpty) return false;
+  const uint32_t myId = *ls.nodeId(me);
+  for (uint32_t lid : ls.linksFromNode(me)) {
+    const Link& l = ls.link(lid);
+    const uint32_t nbr = l.other(myId);
+    if (!maskHas(row, mask, nbr) || !l.isUp()) continue;
+    const Metric overLink = l.metricFrom(myId) + (shortest - row.metric(nbr));
+    if (overLink != shortest) continue;
+    const std::string& nbrName = ls.nodeName(nbr);
+    std::optional<MplsAction> act;
+    if (swapLabel) {
+      act = dsts.count({nbrName, area}) ? mpls(kPhp) : mpls(kSwap, swapLabel);
+    }
+    out.insert(nextHop(isV4 ? l.nhV4From(myId) : l.nhV6From(myId), l.ifFrom(myId),
+                       static_cast<int32_t>(overLink), std::move(act), l.area, nbrName));
+  }
+  return true;
+}
+
+std::pair<Metric, SpfSolver::NhMap> SpfSolver::getNextHopsWithMetric(
+    const std::string& me, const std::set<NodeAndArea>& dsts, bool perDst,
+    const AreaLinkStates& als) const {
+  // Decision.cpp:1177-1228
+  NhMap nhs;
+  Metric shortest = std::numeric_limits<Metric>::max();
+  for (const auto& [area, ls] : als) {
+    const SpfRow& row = ls.getSpfResult(me);
+    Metric areaMin = std::numeric_limits<Metric>::max();
+    std::vector<std::string> minNodes;
+    for (const auto& [dst, _] : dsts) {  // getMinCostNodes: area ignored
+      auto m = rowMetric(ls, row, dst);
+      if (!m) continue;
+      if (areaMin >= *m) {
+        if (areaMin > *m) {
+          areaMin = *m;
+          minNodes.clear();
+        }
+        if (std::find(minNodes.begin(), minNodes.end(), dst) == minNodes.end())
+          minNodes.push_back(dst);
+      }
+    }
+    if (shortest < areaMin) continue;
+    if (shortest > areaMin) {
+      shortest = areaMin;
+      nhs.clear();
+    }
+    for (const auto& dst : minNodes) {
+      const std::string dstRef = perDst ? dst : "";
+      if (dst == row.srcName) continue;  // the source has no first hops
+      const uint32_t did = *ls.nodeId(dst);
+      row.forEachNextHop(did, [&](uint32_t nb) {
+        const std::string& nbName = ls.nodeName(nb);
+        nhs[{nbName, dstRef}] = shortest - *ls.getMetricFromAToB(me, nbName);
+      });
+    }
+  }
+  return {shortest, std::move(nhs)};
+}
+
+NextHopSet SpfSolver::getNextHopsThrift(const std::string& me, const std::set<NodeAndArea>& dsts,
+                                        bool isV4, bool perDst, Metric minMetric, const NhMap& nhs,
+                                        std::optional<int32_t> swapLabel,
+                                        const AreaLinkStates& als,
+                                        const PrefixEntries* entries) const {
+  // Decision.cpp:1230-1334
+  if (nhs.empty()) throw std::logic_error("getNextHopsThrift: no nexthop nodes");
+  NextHopSet out;
+  const std::set<NodeAndArea> noDst{{"", ""}};
+  for (const auto& [area, ls] : als) {
+    auto myId = ls.nodeId(me);
+    if (!myId) continue;
+    for (uint32_t lid : ls.linksFromNode(me)) {
+      const Link& l = ls.link(lid);
+      for (const auto& [dst, dstArea] : perDst ? dsts : noDst) {
+        if (!dstArea.empty() && area != dstArea) continue;
+        const std::string& nbr = ls.nodeName(l.other(*myId));
+        auto it = nhs.find({nbr, dst});
+        if (it == nhs.end() || !l.isUp()) continue;
+        if (!dst.empty() && dsts.count({nbr, area}) && nbr != dst) continue;
+        const Metric overLink = l.metricFrom(*myId) + it->second;
+        if (overLink != minMetric) continue;
+        std::optional<MplsAction> act;
+        if (swapLabel) act = dsts.count({nbr, area}) ? mpls(kPhp) : mpls(kSwap, swapLabel);
+        if (!dst.empty()) {
+          std::vector<int32_t> push;
+          const auto& dpe = entries->at({dst, area});
+          if (dpe.prependLabel) {
+            push.push_back(*dpe.prependLabel);
+            if (!isMplsLabelValid(push.back())) continue;
+          }
+          if (dst != nbr) {
+            push.push_back(ls.getAdjacencyDatabases().at(dst).nodeLabel);
+            if (!isMplsLabelValid(push.back())) continue;
+          }
+          if (!push.empty()) act = mpls(kPush, std::nullopt, std::move(push));
+        }
+        out.insert(nextHop(isV4 ? l.nhV4From(*myId) : l.nhV6From(*myId), l.ifFrom(*myId),
+                           static_cast<int32_t>(overLink), std::move(act), l.area, nbr));
+      }
+    }
+  }
+  return out;
+}
+
+std::optional<RibUnicastEntry> SpfSolver::selectBestPathsSpf(
+    const std::string& me, const Cidr& prefix, const BestRouteSelectionResult& r,
+    const PrefixEntries& entries, bool isBgp, int32_t ft, const AreaLinkStates& als) {
+  // Decision.cpp:904-963
+  const bool isV4 = prefix.first.size() == 4;
+  const bool perDst = ft == kFwdSrMpls;
+  auto filtered = r.allNodeAreas;
+  if (r.hasNode(me) && perDst) {
+    for (const auto& [na, e] : entries) {
+      if (na.first == me && e.prependLabel) {
+        filtered.erase(na);
+        break;
+      }
+    }
+  }
+  if (!perDst && als.size() == 1) {
+    const auto& [area, ls] = *als.begin();
+    if (ls.nodeId(me)) {
+      NextHopSet nhs;
+      if (!fastSpEcmp(me, ls, area, filtered, isV4, std::nullopt, nhs)) return std::nullopt;
+      return addBestPaths(me, prefix, r, entries, isBgp, std::move(nhs));
+    }
+  }
+  auto nhm = getNextHopsWithMetric(me, filtered, perDst, als);
+  if (nhm.second.empty()) return std::nullopt;
+  return addBestPaths(me, prefix, r, entries, isBgp,
+                      getNextHopsThrift(me, r.allNodeAreas, isV4, perDst, nhm.first, nhm.second,
+                                        std::nullopt, als, &entries));
+}
+
+std::optional<RibUnicastEntry> SpfSolver::selectBestPathsKsp2(
+    const std::string& me, const Cidr& prefix, const BestRouteSelectionResult& r,
+    const PrefixEntries& entries, bool isBgp, int32_t ft, const AreaLinkStates& als) {
+  // Decision.cpp:965-1087
+  if (ft != kFwdSrMpls) return std::nullopt;
+  struct AreaPath {
+    const LinkState* ls;
+    Path path;
+  };
+  std::vector<AreaPath> paths;
+  for (const auto& [area, ls] : als) {
+    for (const auto& [node, bestArea] : r.allNodeAreas) {
+      if (node == me && bestArea == area) continue;
+      for (const auto& p : ls.getKthPaths(me, node, 1)) paths.push_back({&ls, p});
+    }
+    const size_t firstPaths = paths.size();
+    for (const auto& [node, bestArea] : r.allNodeAreas) {
+      if (area != bestArea) continue;
+      for (const auto& sp : ls.getKthPaths(me, node, 2)) {
+        bool add = true;
+        for (size_t i = 0; i < firstPaths; ++i) {
+          // link identity is per LinkState; paths of other areas never match
+          if (paths[i].ls == &ls && LinkState::pathAInPathB(paths[i].path, sp)) {
+            add = false;
+            break;
+          }
+        }
+        if (add) paths.push_back({&ls, sp});
+      }
+    }
+  }
+  if (paths.empty()) return std::nullopt;
+
+  NextHopSet nexthops;
+  for (const auto& ap : paths) {
+    const LinkState& pls = *ap.ls;
+    for (const auto& [area, ls] : als) {
+      Metric cost = 0;
+      std::list<int32_t> labels;
+      uint32_t next = *pls.nodeId(me);
+      for (uint32_t lid : ap.path) {
+        const Link& l = pls.link(lid);
+        cost += l.metricFrom(next);
+        next = l.other(next);
+        labels.push_front(ls.getAdjacencyDatabases().at(pls.nodeName(next)).nodeLabel);
+      }
+      labels.pop_back();  // PHP: the first hop's label is not pushed
+      const auto& pe = entries.at({pls.nodeName(next), area});
+      if (pe.prependLabel) labels.push_front(*pe.prependLabel);
+      const Link& first = pls.link(ap.path.front());
+      const uint32_t myId = *pls.nodeId(me);
+      std::optional<MplsAction> act;
+      if (!labels.empty())
+        act = mpls(kPush, std::nullopt, std::vector<int32_t>(labels.begin(), labels.end()));
+      nexthops.insert(nextHop(prefix.first.size() == 4 ? first.nhV4From(myId) : first.nhV6From(myId),
+                              first.ifFrom(myId), static_cast<int32_t>(cost), std::move(act),
+                              first.area, pls.nodeName(first.other(myId))));
+    }
+  }
+  return addBestPaths(me, prefix, r, entries, isBgp, std::move(nexthops));
+}
+
+std::optional<RibUnicastEntry> SpfSolver::addBestPaths(const std::string& me, const Cidr& prefix,
+                                                       const BestRouteSelectionResult& r,
+                                                       const PrefixEntries& entries, bool isBgp,
+                                                       NextHopSet&& nexthops) {
+  // Decision.cpp:1089-1150 (+ getMinNextHopThreshold :824-838)
+  std::optional<int64_t> minNh;
+  for (const auto& na : r.allNodeAreas) {
+    const auto& e = entries.at(na);
+    if (e.minNexthop && (!minNh || *e.minNexthop > *minNh)) minNh = e.minNexthop;
+  }
+  if (minNh && *minNh > static_cast<int64_t>(nexthops.size())) return std::nullopt;
+  if (r.hasNode(me)) {
+    std::optional<int32_t> prepend;
+    for (const auto& [na, e] : entries) {
+      if (na.first == me && e.prependLabel) {
+        prepend = e.prependLabel;
+        break;
+      }
+    }
+    if (!prepend) throw std::logic_error("self-advertised route without prepend label");
+    auto it = staticMplsRoutes_.find(*prepend);
+    if (it != staticMplsRoutes_.end())
+      for (const auto& nh : it->second)
+        nexthops.insert(nextHop(nh.address, std::nullopt, 0, std::nullopt, std::nullopt, std::nullopt));
+  }
+  RibUnicastEntry e;
+  e.prefix = prefix;
+  e.nexthops = std::move(nexthops);
+  e.bestPrefixEntry = entries.at(r.bestNodeArea);
+  e.bestArea = r.bestNodeArea.second;
+  e.doNotInstall = isBgp && bgpDryRun_;
+  return e;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
+                                                       const AreaLinkStates& als,
+                                                       const PrefixState& ps) {
+  // Decision.cpp:615-792
+  bool exists = false;
+  for (const auto& [_, ls] : als) exists |= ls.hasNode(me);
+  if (!exists) return std::nullopt;
+  ++routeBuildRuns_;
+
+  DecisionRouteDb db;
+  db.unicastRoutes.reserve(ps.prefixes().size());
+  for (const auto& [prefix, _] : ps.prefixes()) {
+    if (auto r = createRouteForPrefix(me, als, ps, prefix)) {
+      if (!db.unicastRoutes.emplace(prefix, std::move(*r)).second)
+        throw std::logic_error("duplicate unicast route");
+    }
+  }
+  for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
+    if (db.unicastRoutes.count(prefix)) continue;
+    RibUnicastEntry e;
+    e.prefix = prefix;
+    e.nexthops.insert(nhs.begin(), nhs.end());
+    db.unicastRoutes.emplace(prefix, std::move(e));
+  }
+
+  // node-label routes; duplicate labels resolve to the smaller node name
+  std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
+  for (const auto& [area, ls] : als) {
+    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
+      const int32_t label = adjDb.nodeLabel;
+      if (label == 0 || !isMplsLabelValid(label)) continue;
+      auto it = labelToNode.find(label);
+      if (it != labelToNode.end() && it->second.first < adjDb.thisNodeName) continue;
+      RibMplsEntry entry{label, {}};
+      if (adjDb.thisNodeName == me) {
+        NextHopThrift nh;
+        nh.address.addr = std::string(16, '\0');  // "::"
+        nh.area = area;
+        nh.mplsAction = mpls(kPopAndLookup);
+        entry.nexthops.insert(std::move(nh));
+      } else {
+        const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};
+        if (als.size() == 1 && ls.nodeId(me)) {
+          if (!fastSpEcmp(me, ls, area, dst, false, label, entry.nexthops)) continue;
+        } else {
+          auto nhm = getNextHopsWithMetric(me, dst, false, als);
+          if (nhm.second.empty()) continue;
+          entry.nexthops = getNextHopsThrift(me, dst, false, false, nhm.first, nhm.second, label,
+                                             als, nullptr);
+        }
+      }
+      labelToNode.erase(label);
+      labelToNode.emplace(label, std::make_pair(adjDb.thisNodeName, std::move(entry)));
+    }
+  }
+  for (auto& [label, ne] : labelToNode) db.mplsRoutes.emplace(label, std::move(ne.second));
+
+  // adjacency-label routes for all my links, up or not (:749-775)
+  for (const auto& [_, ls] : als) {
+    auto myId = ls.nodeId(me);
+    if (!myId) continue;
+    for (uint32_t lid : ls.linksFromNode(me)) {
+      const Link& l = ls.link(lid);
+      const int32_t label = l.adjLabelFrom(*myId);
+      if (label == 0 || !isMplsLabelValid(label)) continue;
+      RibMplsEntry e{label, {}};
+      e.nexthops.insert(nextHop(l.nhV6From(*myId), l.ifFrom(*myId),
+                                static_cast<int32_t>(l.metricFrom(*myId)), mpls(kPhp), l.area,
+                                ls.nodeName(l.other(*myId))));
+      if (!db.mplsRoutes.emplace(label, std::move(e)).second)
+        throw std::logic_error("duplicate mpls route");
+    }
+  }
+  for (const auto& [label, nhs] : staticMplsRoutes_) {
+    RibMplsEntry e{label, {}};
+    e.nexthops.insert(nhs.begin(), nhs.end());
+    if (!db.mplsRoutes.emplace(label, std::move(e)).second)
+      throw std::logic_error("duplicate mpls route");
+  }
+  return db;
+}
+
+}  // namespace openr_amd
