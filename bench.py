@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""All-sources SPF throughput + buildRouteDb latency on the 10k-node grid.
+
+Workload (BASELINE.json configs[1]): the benchmark grid
+createGrid(n=100, 1 prefix, SP_ECMP) of RoutingBenchmarkUtils.cpp:271-313,
+N = 10,000 nodes, E = 39,600 directed adjacencies, unit metrics. One step is
+one all-sources sweep: LinkState::runSpf from every node (dist row + ECMP
+first-hop mask row per source, written to HBM), with the CSR mirror already
+resident in HBM. With --gpus N (torch.distributed.run, one rank per GPU) the
+10,000 sources are split into contiguous blocks; no collective touches the
+data path (timing only: barrier + max over ranks).
+
+Also reported: buildRouteDb("1") ms (cold: right after a topology-changing
+adjacency update, so it includes the device mirror patch and the SPF; warm:
+memoized SPF), the dominant kernel's HBM roofline figures, and the CPU
+oracle (a port of the reference algorithm with its data structures) timed on
+a bounded sample of the same workload on this host.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from openr_amd.sharding import dist_env, shard_sources  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--grid", type=int, default=100)
+    p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-route-db", action="store_true")
+    return p.parse_args()
+
+
+def median_ms(fn, reps):
+    return statistics.median(fn() for _ in range(reps))
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_env()
+    os.environ.setdefault("ORH_DEVICE", str(local))  # before the host library opens a context
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    from openr_amd import host_backend
+    from openr_amd.facade import load_topology
+    from openr_amd.topology import bench_grid
+    from openr_amd.types import K_TESTING_AREA
+
+    n = args.grid
+    adj_dbs, prefixes = bench_grid(n, 1)
+    hip = host_backend()
+    als, ps = load_topology(hip, adj_dbs, prefixes)
+    ls = als[K_TESTING_AREA]
+    names = [str(i) for i in range(n * n)]
+    mine = shard_sources(names, world, rank)
+    sweep = ls._impl.sweep(mine, True)
+
+    for _ in range(args.warmup):
+        sweep.run()
+        sweep.last_ms()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for _ in range(args.steps):
+        sweep.run()
+        kernel_ms.append(sweep.last_ms())  # HIP events on the sweep's own stream
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+
+    total_sources = n * n * args.steps  # all ranks together
+    value = total_sources / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # size-independent correctness check on the timed output: unit metrics,
+    # so dist(src, v) is the Manhattan distance on the grid
+    node_ids = {name: i for i, name in enumerate(ls._impl.node_names())}
+    import numpy as np
+    ids = np.array([node_ids[str(v)] for v in range(n * n)])
+    rr, cc = np.divmod(np.arange(n * n), n)
+    for i in (0, len(mine) // 2, len(mine) - 1):
+        s = int(mine[i])
+        dist_row, _ = sweep.fetch(i)
+        if not np.array_equal(dist_row[ids], np.abs(rr - rr[s]) + np.abs(cc - cc[s])):
+            raise SystemExit(f"bench: wrong distances for source {s}")
+
+    if rank != 0:
+        barrier()
+        return
+
+    # roofline of the SPF kernel: B = 4(N+1) + 8E + N(4D + 4W)
+    N, E, W = sweep.nodes, sweep.edges, sweep.words
+    bytes_per_source = 4 * (N + 1) + 8 * E + N * (4 * 1 + 4 * W)
+    per_launch = bytes_per_source * len(mine)
+    kms = statistics.mean(kernel_ms)
+    achieved = per_launch / (kms * 1e-3) / 1e9
+
+    out = {
+        "metric": "all-source SPF runs/sec + buildRouteDb ms on 10k-node topology",
+        "value": round(value, 1),
+        "unit": "SPF-sources/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: reference benchmark grid generator (createGrid n=100)",
+        "config": {"workload": f"C2 {n}x{n} grid all-sources SPF (N={N}, E={E})",
+                   "sources_per_step": n * n, "parallelism": f"source-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel_ms": round(kms, 4),
+                     "algorithmic_bytes_per_source": bytes_per_source},
+    }
+
+    if not args.no_route_db:
+        solver = hip.spf_solver("1", True)
+        solver.build_route_db("1", als, ps)
+        db = adj_dbs[n * n // 2]
+        flips = [0]
+
+        def cold():
+            flips[0] ^= 1  # topology change: memo cleared, mirror patched
+            db.adjacencies[0].metric = 1 + flips[0]
+            ls.update_adjacency_database(db)
+            return solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3
+
+        out["build_route_db_ms"] = round(median_ms(cold, 7), 3)
+        out["build_route_db_warm_ms"] = round(median_ms(
+            lambda: solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3, 7), 3)
+        db.adjacencies[0].metric = 1
+        ls.update_adjacency_database(db)
+
+    if world == 1 and not args.no_cpu_baseline:
+        out.update(cpu_baseline(args, adj_dbs, prefixes, n, value))
+
+    print(json.dumps(out), flush=True)
+    barrier()
+
+
+def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
+    """Oracle (port of the reference LinkState::runSpf with its containers)
+    on this host: a bounded, evenly spaced sample of the same 10k sources."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "build"))
+    import importlib
+    from openr_amd.facade import Backend, load_topology
+    from openr_amd.types import K_TESTING_AREA
+    oracle = Backend(importlib.import_module("openr_oracle"), "oracle")
+    als, ps = load_topology(oracle, adj_dbs, prefixes)
+    ls = als[K_TESTING_AREA]
+    step = max(1, (n * n) // args.cpu_sample)
+    sample = [str(i) for i in range(0, n * n, step)][:args.cpu_sample]
+    sec1, _ = ls._impl.time_spf_sources(sample, 1)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    sample_mt = sample * min(threads, 4)
+    secn, _ = ls._impl.time_spf_sources(sample_mt, threads)
+    solver = oracle.spf_solver("1", True)
+    db = adj_dbs[n * n // 2]
+    flips = [0]
+
+    def cold():  # same topology-changing update as the GPU measurement
+        flips[0] ^= 1
+        db.adjacencies[0].metric = 1 + flips[0]
+        ls.update_adjacency_database(db)
+        return solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3
+
+    brdb = median_ms(cold, 3)
+    db.adjacencies[0].metric = 1
+    v1 = len(sample) / sec1
+    vn = len(sample_mt) / secn
+    return {
+        "cpu_baseline": {"value": round(vn, 2), "unit": "SPF-sources/s", "cores": threads,
+                         "kind": "port",
+                         "sample": f"{len(sample_mt)} runSpf calls ({len(sample)} evenly spaced "
+                                   f"sources x {threads} threads, one deep LinkState copy per "
+                                   f"thread), extrapolated per source"},
+        "cpu_baseline_1t": {"value": round(v1, 2), "unit": "SPF-sources/s", "cores": 1,
+                            "kind": "port", "sample": f"{len(sample)} sources"},
+        "cpu_build_route_db_ms": round(brdb, 2),
+        "speedup_vs_cpu": round(gpu_value / vn, 1),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -243,7 +243,15 @@ PYBIND11_MODULE(openr_oracle, m) {
              // not thread-safe, LinkState.h:279-301), no cross-source memo.
              py::gil_scoped_release rel;
              threads = std::max(1, threads);
-             std::vector<LinkState> copies(threads, s);
+             // deep copies (replayed adjacency databases): threads must not
+             // share Link objects, whose shared_ptr refcounts runSpf bumps
+             std::vector<LinkState> copies;
+             copies.reserve(threads);
+             for (int t = 0; t < threads; ++t) {
+               copies.emplace_back(s.getArea());
+               for (const auto& kv : s.getAdjacencyDatabases())
+                 copies.back().updateAdjacencyDatabase(kv.second);
+             }
              const auto t0 = std::chrono::steady_clock::now();
              std::vector<std::thread> ws;
              size_t checksum = 0;
