@@ -109,6 +109,8 @@ int orh_reset_counters(orh_ctx* ctx);
 /* device time (HIP events on the context stream) of the last orh_spf_run;
  * waits for that launch to finish */
 int orh_last_spf_ms(orh_ctx* ctx, double* ms_out);
+/* the same split by phase: distance rows, then first-hop masks */
+int orh_last_spf_phase_ms(orh_ctx* ctx, double* dist_ms_out, double* hop_ms_out);
 /* device memory helpers for callers without their own allocator */
 int orh_device_alloc(orh_ctx* ctx, size_t bytes, void** d_out);
 int orh_device_free(orh_ctx* ctx, void* d_ptr);

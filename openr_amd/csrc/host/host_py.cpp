@@ -222,6 +222,12 @@ class SpfSweep {
     if (orh_last_spf_ms(ctx_, &ms) != ORH_OK) throw std::runtime_error("orh_last_spf_ms failed");
     return ms;
   }
+  py::tuple phaseMs() {
+    double a = 0, b = 0;
+    if (orh_last_spf_phase_ms(ctx_, &a, &b) != ORH_OK)
+      throw std::runtime_error("orh_last_spf_phase_ms failed");
+    return py::make_tuple(a, b);
+  }
   void sync() {
     if (orh_sync(ctx_) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
   }
@@ -343,6 +349,7 @@ PYBIND11_MODULE(_openr_host, m) {
   py::class_<SpfSweep>(m, "SpfSweep")
       .def("run", &SpfSweep::run)
       .def("last_ms", &SpfSweep::lastMs)
+      .def("phase_ms", &SpfSweep::phaseMs)
       .def("sync", &SpfSweep::sync)
       .def("fetch", &SpfSweep::fetch)
       .def_property_readonly("words", &SpfSweep::words)

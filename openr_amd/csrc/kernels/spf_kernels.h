@@ -5,45 +5,74 @@
 #include <stddef.h>
 #include <stdint.h>
 
-// mirrors of the ORH_META_* bits in include/openr_hip.h
-#define ORH_META_LINK_MASK_ 0x3FFFFFFFu
-#define ORH_META_COL_OVERLOADED_ 0x40000000u
-#define ORH_META_DOWN_ 0x80000000u
+// Device edge record (uint2): x = col | flags, y = w_out.
+// A continuation record is {overflow start | CONT, count}.
+#define ORH_REC_COL_MASK 0x07FFFFFFu
+#define ORH_REC_CONT 0x08000000u     // continuation into the overflow area
+#define ORH_REC_ROW_OVL 0x10000000u  // the record's row node is overloaded
+#define ORH_REC_SKIP 0x80000000u     // link down, or an empty ELL slot
 
 namespace orh {
 
+// phase 1: distance rows. Rows [0, n_out) are written to out_dist, rows
+// [n_out, n_rows) (neighbour rows the first-hop phase needs) to scratch.
 struct SpfArgs {
   uint32_t n_nodes;
-  uint32_t words;  // nh words per node in the output
-  const uint32_t* row_ptr;
-  const uint4* edges;  // {col, w_out, w_in, meta}
-  const uint16_t* rank_in_col;  // rank of the row node among col's distinct neighbours
-  const uint8_t* node_overloaded;
-  const uint32_t* srcs;
-  const uint32_t* ignore_ptr;  // nullable
+  uint32_t n_out;
+  const uint2* recs;       // ELL slots [N * K] then overflow records
+  const uint32_t* link;    // per record: link id (ignore sets)
+  const uint32_t* srcs;    // [n_rows]
+  const uint32_t* ignore_ptr;  // [n_rows + 1], nullable
   const uint32_t* ignore_links;
   int32_t use_link_metric;
-  uint32_t lds_list_off;
-  uint32_t lds_mask_off;
+  uint32_t w0;  // the uniform metric (BFS variant)
+  uint32_t lds_pend_off;
   uint32_t* out_dist;
+  uint32_t* scratch;
+};
+
+// phase 2: first-hop masks of the requested rows from the distance rows of
+// each source and of its neighbours
+struct HopArgs {
+  uint32_t n_nodes;
+  uint32_t n_out;  // requested rows (= sources of this phase)
+  uint32_t words;
+  uint32_t ell_k;
+  uint32_t tiles;  // node tiles per source
+  const uint2* recs;
+  const uint32_t* link;
+  const uint16_t* rank_out;  // per record: col's rank among the row node's distinct neighbours
+  const uint8_t* overloaded;
+  const uint32_t* srcs;
+  const uint32_t* ignore_ptr;
+  const uint32_t* ignore_links;
+  int32_t use_link_metric;
+  const uint32_t* nbr_ptr;  // [n_out + 1] into nbr_row
+  const uint32_t* nbr_row;  // per (source, neighbour rank): row of that neighbour's distances
+  const uint32_t* dist;
+  const uint32_t* scratch;
   uint32_t* out_nh;
 };
 
-enum class SpfVariant { kUnsupported = 0, kK16, kK32, kWide };
+enum class SpfVariant { kUnsupported = 0, kBfs, kDist16, kDist32 };
 
 struct SpfPlan {
   SpfVariant variant;
-  bool id16;
-  size_t list_off;
-  size_t mask_off;
+  uint32_t ell_k;
+  uint32_t block;
+  size_t pend_off;
   size_t lds_bytes;
 };
 
-// max_nbr: largest distinct-neighbour count over the batch's sources;
-// path_bound: upper bound on any D + w computed by the kernel
-SpfPlan plan_spf(uint32_t n_nodes, uint32_t words, uint32_t max_nbr, uint64_t path_bound,
+// uniform: every live link carries the same metric (BFS levels suffice);
+// path_bound: upper bound on any tentative distance
+SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
                  size_t lds_limit);
-hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_src, hipStream_t s);
+hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
+
+// LDS bytes the first-hop kernel needs for max_nbr distinct neighbours
+size_t hop_lds_bytes(uint32_t max_nbr);
+hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s);
 
 struct RouteSelectArgs {
   uint32_t n_prefix;

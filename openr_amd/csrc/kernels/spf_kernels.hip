@@ -7,93 +7,55 @@
 //   NH(u)  = OR over predecessors (l, v) with d(v) + w_v(l) == d(u) and v a
 //          transit node of   (v == src ? {u} : NH(v))          (:857-873)
 //
-// Algorithm: one workgroup per source, level-synchronous Dijkstra that
-// settles every node of the current minimum distance D at once (exact for
-// positive integer metrics). Per level, ONE pass over the pending list
-//   - nodes at distance D are settled: their first-hop mask is pulled from
-//     already-settled predecessors (d < D), then their out-links are relaxed
-//     with LDS atomicMin (push); newly touched nodes are appended;
-//   - nodes above D are carried over;
-// and ONE __syncthreads(). The next D is the minimum over values that were
-// carried or that lowered a distance, reduced during the same pass.
+// Two phases, both batched over many sources:
 //
-// State lives in LDS. Packed variants hold a node's (dist, mask) in one word
-// so the relaxation is a single ds_min:
-//   K16: u32 = dist16 << 16 | mask16   (paths < 0xFFFF, <= 16 neighbours)
-//   K32: u64 = dist32 << 32 | mask32   (paths < 2^32-1, <= 32 neighbours)
-// KW: separate u32 dist and W mask words (any neighbour count).
-// A node's mask half is garbage (all ones) until the node settles; pushes
-// never touch settled nodes (they only write D + w > D), so the settle store
-// and concurrent ds_min on the same word commute.
+// 1. Distance rows (one workgroup per source row). The first-hop masks are
+//    NOT carried through the search, so the per-source LDS state is only what
+//    the distances need:
+//      BFS    (every live link has the same metric w0): visited + two frontier
+//             bitmaps, 3 bits per node; a node's distance (level * w0) is
+//             stored to its HBM row when it is expanded. No atomics return,
+//             no min-reduction: the next level is the next frontier.
+//      Dist16 / Dist32 (general metrics): a u16 or u32 distance per node plus
+//             a pending-set bitmap; level-synchronous Dijkstra that expands
+//             every node at the minimum pending distance D at once (exact for
+//             positive integer metrics), the next D from a DPP wave minimum.
+//    Small state buys occupancy: BFS on N = 10,000 needs 3.75 KB, so waves,
+//    not LDS, bound the resident sources per CU.
+// 2. First hops (one workgroup per (source, 1024-node tile)). With metrics
+//    >= 1 the closed form unrolls to: bit i (the source's i-th distinct
+//    neighbour n_i) is in NH(v) iff some up link s->n_i is tight
+//    (w == d_s(n_i)) and either v == n_i, or n_i is not overloaded and
+//    d_s(n_i) + d_{n_i}(v) == d_s(v), where d_{n_i} is n_i's own SPF with the
+//    same ignore set (a tight path leaves s through n_i and continues along
+//    a shortest path of n_i whose intermediates are transit nodes; paths of
+//    n_i back through s are never tight). Phase 1 therefore also computes
+//    the rows of the sources' neighbours (free for an all-sources sweep: they
+//    are sources themselves), and phase 2 is a streaming, coalesced pass over
+//    1 + deg(s) distance rows per source.
 //
-// HBM traffic per source: the CSR (16 B per directed edge + row offsets) is
-// shared by every workgroup and stays L2/MALL-resident; each source writes
-// its dist row and mask row once, coalesced, at the end.
+// Graph records are 8 bytes (col|flags, w_out), ELL-style K per node with a
+// continuation into an overflow area, so expanding a node is ONE dependent
+// global round trip (K records issued together, served from L2 where the
+// graph stays resident for every workgroup on the XCD).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "spf_kernels.h"
 
 namespace orh {
 
-constexpr int kBlock = 256;
-constexpr int kWaves = kBlock / 64;
-
-// ---------------------------------------------------------------------------
-// state policies
-// ---------------------------------------------------------------------------
-struct K16 {
-  using Word = uint32_t;
-  static constexpr Word kInf = 0xFFFFFFFFu;
-  static constexpr uint32_t kDistInf = 0xFFFFu;
-  static constexpr int kMaxNbr = 16;
-  __device__ static uint32_t dist(Word w) { return w >> 16; }
-  __device__ static uint32_t mask(Word w) { return w & 0xFFFFu; }
-  __device__ static Word tentative(uint32_t d) { return (d << 16) | 0xFFFFu; }
-  __device__ static Word settled(uint32_t d, uint32_t m) { return (d << 16) | m; }
-};
-
-struct K32 {
-  using Word = unsigned long long;
-  static constexpr Word kInf = ~0ull;
-  static constexpr uint32_t kDistInf = 0xFFFFFFFFu;
-  static constexpr int kMaxNbr = 32;
-  __device__ static uint32_t dist(Word w) { return static_cast<uint32_t>(w >> 32); }
-  __device__ static uint32_t mask(Word w) { return static_cast<uint32_t>(w); }
-  __device__ static Word tentative(uint32_t d) { return (static_cast<Word>(d) << 32) | 0xFFFFFFFFull; }
-  __device__ static Word settled(uint32_t d, uint32_t m) {
-    return (static_cast<Word>(d) << 32) | m;
-  }
-};
-
-__device__ inline uint32_t lane_id() { return __lane_id(); }
-
-// wave-aggregated append of `val` (where pred) to list[*cnt++]
-template <typename IdT>
-__device__ inline void wave_append(IdT* list, uint32_t* cnt, bool pred, uint32_t val) {
-  const unsigned long long m = __ballot(pred);
-  if (m == 0) return;
-  const int lane = lane_id();
-  const int leader = __ffsll(static_cast<long long>(m)) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(cnt, static_cast<uint32_t>(__popcll(m)));
-  base = __shfl(base, leader);
-  if (pred) {
-    const unsigned long long below = (lane == 0) ? 0ull : (m & ((1ull << lane) - 1ull));
-    list[base + __popcll(below)] = static_cast<IdT>(val);
-  }
-}
-
-__device__ inline uint32_t wave_min(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, static_cast<uint32_t>(__shfl_xor(v, off)));
-  return v;
-}
+constexpr int kBlock = 256;     // route selection, first hops
+constexpr int kMaxBlock = 1024;  // SPF
+constexpr int kOvfBatch = 8;     // overflow records in flight per expanded node
+constexpr int kHopPer = 4;       // nodes per thread in the first-hop kernel
+constexpr uint32_t kInf = 0xFFFFFFFFu;
 
 __device__ inline bool ignored(const uint32_t* ign, uint32_t n, uint32_t link) {
-  // sorted ascending; n is tiny (KSP2 / what-if sets)
-  uint32_t lo = 0, hi = n;
+  uint32_t lo = 0, hi = n;  // sorted ascending; tiny (KSP2 / what-if sets)
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     const uint32_t x = ign[mid];
@@ -103,218 +65,463 @@ __device__ inline bool ignored(const uint32_t* ign, uint32_t n, uint32_t link) {
   return false;
 }
 
-// ---------------------------------------------------------------------------
-// packed-state kernel (K16 / K32)
-// ---------------------------------------------------------------------------
-template <class P, typename IdT>
-__global__ __launch_bounds__(kBlock) void spf_packed_kernel(SpfArgs a) {
-  using Word = typename P::Word;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t N = a.n_nodes;
-  Word* word = reinterpret_cast<Word*>(smem);
-  IdT* lists = reinterpret_cast<IdT*>(smem + a.lds_list_off);
-  __shared__ uint32_t s_cnt[3];
-  __shared__ uint32_t s_min[3];
+__device__ inline uint32_t* dist_row(uint32_t* out, uint32_t* scratch, uint32_t n_out, uint32_t N,
+                                     uint32_t row) {
+  return row < n_out ? out + static_cast<size_t>(row) * N
+                     : scratch + static_cast<size_t>(row - n_out) * N;
+}
 
-  const uint32_t tid = threadIdx.x;
-  const uint32_t sidx = blockIdx.x;
-  const uint32_t src = a.srcs[sidx];
-  const uint32_t ign_b = a.ignore_ptr ? a.ignore_ptr[sidx] : 0u;
-  const uint32_t n_ign = a.ignore_ptr ? a.ignore_ptr[sidx + 1] - ign_b : 0u;
-  const uint32_t* ign = a.ignore_links + ign_b;
+// wave-wide minimum through DPP row shifts and row broadcasts (no LDS)
+__device__ inline uint32_t wave_min(uint32_t v) {
+#define ORH_DPP_MIN(ctrl, rmask)                                                         \
+  v = min(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(                           \
+                 static_cast<int>(kInf), static_cast<int>(v), ctrl, rmask, 0xF, false)))
+  ORH_DPP_MIN(0x111, 0xF);  // row_shr:1
+  ORH_DPP_MIN(0x112, 0xF);  // row_shr:2
+  ORH_DPP_MIN(0x114, 0xF);  // row_shr:4
+  ORH_DPP_MIN(0x118, 0xF);  // row_shr:8  -> lane 15 of each row holds the row minimum
+  ORH_DPP_MIN(0x142, 0xA);  // row_bcast:15 into rows 1, 3
+  ORH_DPP_MIN(0x143, 0xC);  // row_bcast:31 into rows 2, 3 -> lane 63 holds the minimum
+#undef ORH_DPP_MIN
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
 
-  for (uint32_t i = tid; i < N; i += kBlock) word[i] = P::kInf;
-  if (tid < 3) {
-    s_cnt[tid] = 0;
-    s_min[tid] = 0xFFFFFFFFu;
+struct Src {
+  uint32_t node;
+  const uint32_t* ign;
+  uint32_t n_ign;
+  __device__ Src(const SpfArgs& a, uint32_t row) : node(a.srcs[row]), ign(nullptr), n_ign(0) {
+    if (a.ignore_ptr) {
+      const uint32_t b = a.ignore_ptr[row];
+      ign = a.ignore_links + b;
+      n_ign = a.ignore_ptr[row + 1] - b;
+    }
   }
+};
+
+// a record the search may relax: up, not a continuation, not ignored
+__device__ inline bool live(const SpfArgs& a, const Src& s, const uint2& r, uint32_t q) {
+  return !(r.x & (ORH_REC_SKIP | ORH_REC_CONT)) &&
+      !(s.n_ign && ignored(s.ign, s.n_ign, a.link[q]));
+}
+
+template <int K>
+__device__ inline void load_recs(const SpfArgs& a, uint32_t v, uint2 (&rec)[K]) {
+  const uint2* slots = a.recs + static_cast<size_t>(v) * K;
+#pragma unroll
+  for (int j = 0; j < K; ++j) rec[j] = slots[j];
+}
+
+// ---------------------------------------------------------------------------
+// phase 1a: BFS levels (uniform metric)
+// ---------------------------------------------------------------------------
+template <int K>
+struct Bfs {
+  const SpfArgs& a;
+  const Src& s;
+  uint32_t* vis;
+  uint32_t* nxt;
+
+  __device__ bool edge(const uint2& r, uint32_t vw) const {
+    const uint32_t u = r.x & ORH_REC_COL_MASK;
+    const uint32_t bit = 1u << (u & 31u);
+    if (vw & bit) return false;
+    atomicOr(&vis[u >> 5], bit);
+    atomicOr(&nxt[u >> 5], bit);
+    return true;
+  }
+
+  // expand v (its K records in rec): mark unvisited neighbours for the next level
+  __device__ bool expand(uint32_t v, const uint2 (&rec)[K]) const {
+    if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) return false;  // no transit
+    bool pushed = false;
+    uint32_t vw[K];
+    bool lv[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      lv[j] = live(a, s, rec[j], v * K + j);
+      vw[j] = lv[j] ? vis[(rec[j].x & ORH_REC_COL_MASK) >> 5] : kInf;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (lv[j]) pushed |= edge(rec[j], vw[j]);
+    const uint2 last = rec[K - 1];
+    if (last.x & ORH_REC_CONT) {
+      const uint32_t start = last.x & ORH_REC_COL_MASK;
+      for (uint32_t base = 0; base < last.y; base += kOvfBatch) {
+        const uint32_t cnt = min(last.y - base, static_cast<uint32_t>(kOvfBatch));
+        uint2 ov[kOvfBatch];
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j)
+          if (j < static_cast<int>(cnt)) ov[j] = a.recs[start + base + j];
+        uint32_t ow[kOvfBatch];
+        bool ol[kOvfBatch];
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j) {
+          ol[j] = j < static_cast<int>(cnt) && live(a, s, ov[j], start + base + j);
+          ow[j] = ol[j] ? vis[(ov[j].x & ORH_REC_COL_MASK) >> 5] : kInf;
+        }
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j)
+          if (ol[j]) pushed |= edge(ov[j], ow[j]);
+      }
+    }
+    return pushed;
+  }
+};
+
+template <int K>
+__global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_any[2];
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  uint32_t* vis = lds;
+  uint32_t* f0 = lds + NB;
+  uint32_t* f1 = lds + 2 * NB;
+  const Src s(a, row);
+  uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+
+  for (uint32_t i = tid; i < 3 * NB; i += nthr) lds[i] = 0u;
+  if (tid < 2) s_any[tid] = 0u;
   __syncthreads();
   if (tid == 0) {
-    word[src] = P::settled(0, 0);
-    lists[0] = static_cast<IdT>(src);
+    vis[s.node >> 5] = 1u << (s.node & 31u);
+    f0[s.node >> 5] = 1u << (s.node & 31u);
   }
   __syncthreads();
 
-  uint32_t cur_n = 1;
+  constexpr int kBatch = 16 / K;  // nodes whose records are in flight together
   uint32_t D = 0;
-  const bool use_metric = a.use_link_metric != 0;
-  for (uint32_t level = 0;; ++level) {
-    IdT* in = lists + ((level & 1) ? N : 0);
-    IdT* out = lists + ((level & 1) ? 0 : N);
-    uint32_t* cnt_w = &s_cnt[level % 3];
-    uint32_t* min_w = &s_min[level % 3];
-    if (tid == 0) {  // slot of the next level; last read one level ago
-      s_cnt[(level + 1) % 3] = 0;
-      s_min[(level + 1) % 3] = 0xFFFFFFFFu;
-    }
-    uint32_t local_min = 0xFFFFFFFFu;
-    for (uint32_t base = 0; base < cur_n; base += kBlock) {
-      const uint32_t i = base + tid;
-      const bool active = i < cur_n;
-      const uint32_t v = active ? static_cast<uint32_t>(in[i]) : 0u;
-      const uint32_t dv = active ? P::dist(word[v]) : 0u;
-      const bool settle = active && dv == D;
-      // carry unsettled pending nodes to the next level
-      wave_append(out, cnt_w, active && !settle, v);
-      if (active && !settle) local_min = min(local_min, dv);
-      if (settle) {
-        const bool transit = (v == src) || !a.node_overloaded[v];
-        const uint32_t e0 = a.row_ptr[v], e1 = a.row_ptr[v + 1];
-        uint32_t acc = 0;
-        for (uint32_t e = e0; e < e1; ++e) {
-          const uint4 rec = a.edges[e];  // {col, w_out, w_in, meta}
-          if (rec.w & ORH_META_DOWN_) continue;
-          if (n_ign && ignored(ign, n_ign, rec.w & ORH_META_LINK_MASK_)) continue;
-          const uint32_t u = rec.x;
-          const uint32_t w_out = use_metric ? rec.y : 1u;
-          const uint32_t w_in = use_metric ? rec.z : 1u;
-          if (v != src) {  // pull the first-hop mask from settled predecessors
-            const Word wu = word[u];
-            const uint32_t du = P::dist(wu);
-            const bool pred_transit = (u == src) || !(rec.w & ORH_META_COL_OVERLOADED_);
-            if (du < D && du + w_in == D && pred_transit) {
-              acc |= (u == src) ? (1u << a.rank_in_col[e]) : P::mask(wu);
-            }
-          }
-          if (transit) {  // relax (push)
-            const uint32_t nd = D + w_out;
-            const Word old = atomicMin(&word[u], P::tentative(nd));
-            const uint32_t od = P::dist(old);
-            if (nd < od) local_min = min(local_min, nd);
-            wave_append(out, cnt_w, od == P::kDistInf, u);
+  for (uint32_t level = 0;; ++level, D += a.w0) {
+    const uint32_t par = level & 1u;
+    uint32_t* cur = par ? f1 : f0;
+    const Bfs<K> b{a, s, vis, par ? f0 : f1};
+    if (tid == 0) s_any[par ^ 1u] = 0u;  // next level's flag, read one level ago
+    bool pushed = false;
+    // a thread owns frontier words w and w + nthr: their nodes' records go
+    // out in one batch
+    for (uint32_t w = tid; w < NB; w += 2 * nthr) {
+      const uint32_t w2 = w + nthr;
+      const uint32_t t0 = cur[w];
+      const uint32_t t1 = w2 < NB ? cur[w2] : 0u;
+      if (t0) cur[w] = 0u;  // becomes the level-after-next frontier
+      if (t1) cur[w2] = 0u;
+      uint64_t todo = t0 | (static_cast<uint64_t>(t1) << 32);
+      while (todo) {
+        uint32_t vs[kBatch];
+        uint2 r[kBatch][K];
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i) {
+          if (todo) {
+            const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            vs[i] = bit < 32 ? w * 32 + bit : w2 * 32 + (bit - 32);
+            load_recs<K>(a, vs[i], r[i]);
+            out[vs[i]] = D;
+            cnt = i + 1;
           }
         }
-        if (v != src) word[v] = P::settled(D, acc);
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i)
+          if (i < cnt) pushed |= b.expand(vs[i], r[i]);
+      }
+    }
+    if (pushed) s_any[par] = 1u;
+    __syncthreads();
+    // every level expands >= 1 node, so > N levels would be a bug; the bound
+    // guarantees every wave reaches the exit
+    if (!s_any[par] || level >= N) break;
+  }
+  for (uint32_t i = tid; i < N; i += nthr)
+    if (!((vis[i >> 5] >> (i & 31u)) & 1u)) out[i] = kInf;
+}
+
+// ---------------------------------------------------------------------------
+// phase 1b: level-synchronous Dijkstra on a u16 / u32 distance per node
+// ---------------------------------------------------------------------------
+template <class T>
+struct DistWord;
+
+template <>
+struct DistWord<uint32_t> {
+  static constexpr uint32_t kInfT = 0xFFFFFFFFu;
+  __device__ static uint32_t get(const uint32_t* d, uint32_t u) { return d[u]; }
+  // lower d[u] to nd (> D); returns the previous value if it was lowered, else nd
+  __device__ static bool lower(uint32_t* d, uint32_t u, uint32_t du, uint32_t nd, bool& first) {
+    if (nd >= du) return false;
+    atomicMin(&d[u], nd);
+    first = du == kInfT;
+    return true;
+  }
+};
+
+template <>
+struct DistWord<uint16_t> {  // two nodes per u32 word; updated by compare-and-swap
+  static constexpr uint32_t kInfT = 0xFFFFu;
+  __device__ static uint32_t get(const uint32_t* d, uint32_t u) {
+    return (d[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu;
+  }
+  __device__ static bool lower(uint32_t* d, uint32_t u, uint32_t du, uint32_t nd, bool& first) {
+    if (nd >= du) return false;
+    const uint32_t sh = (u & 1u) * 16u;
+    uint32_t old = d[u >> 1];
+    for (;;) {
+      const uint32_t cur = (old >> sh) & 0xFFFFu;
+      if (nd >= cur) return false;  // lowered further by another lane
+      const uint32_t nw = (old & ~(0xFFFFu << sh)) | (nd << sh);
+      const uint32_t prev = atomicCAS(&d[u >> 1], old, nw);
+      if (prev == old) {
+        first = cur == 0xFFFFu;
+        return true;
+      }
+      old = prev;
+    }
+  }
+};
+
+template <class T, int K>
+struct Dij {
+  using DW = DistWord<T>;
+  const SpfArgs& a;
+  const Src& s;
+  uint32_t* dist;  // LDS, T per node
+  uint32_t* pend;
+
+  __device__ void edge(const uint2& r, uint32_t du, uint32_t D, uint32_t& lowered) const {
+    const uint32_t u = r.x & ORH_REC_COL_MASK;
+    const uint32_t nd = D + (a.use_link_metric ? r.y : 1u);
+    bool first = false;
+    if (DW::lower(dist, u, du, nd, first)) {
+      lowered = min(lowered, nd);
+      if (first) atomicOr(&pend[u >> 5], 1u << (u & 31u));
+    }
+  }
+
+  // relax v's out-links at distance D; returns the smallest distance it lowered
+  __device__ uint32_t expand(uint32_t v, const uint2 (&rec)[K], uint32_t D) const {
+    uint32_t lowered = kInf;
+    if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) return lowered;
+    uint32_t du[K];
+    bool lv[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      lv[j] = live(a, s, rec[j], v * K + j);
+      du[j] = lv[j] ? DW::get(dist, rec[j].x & ORH_REC_COL_MASK) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (lv[j]) edge(rec[j], du[j], D, lowered);
+    const uint2 last = rec[K - 1];
+    if (last.x & ORH_REC_CONT) {
+      const uint32_t start = last.x & ORH_REC_COL_MASK;
+      for (uint32_t base = 0; base < last.y; base += kOvfBatch) {
+        const uint32_t cnt = min(last.y - base, static_cast<uint32_t>(kOvfBatch));
+        uint2 ov[kOvfBatch];
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j)
+          if (j < static_cast<int>(cnt)) ov[j] = a.recs[start + base + j];
+        uint32_t od[kOvfBatch];
+        bool ol[kOvfBatch];
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j) {
+          ol[j] = j < static_cast<int>(cnt) && live(a, s, ov[j], start + base + j);
+          od[j] = ol[j] ? DW::get(dist, ov[j].x & ORH_REC_COL_MASK) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kOvfBatch; ++j)
+          if (ol[j]) edge(ov[j], od[j], D, lowered);
+      }
+    }
+    return lowered;
+  }
+};
+
+template <class T, int K>
+__global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
+  using DW = DistWord<T>;
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_min[2];
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  uint32_t* dist = lds;
+  uint32_t* pend = lds + a.lds_pend_off / 4;
+  const Src s(a, row);
+  const Dij<T, K> d{a, s, dist, pend};
+
+  const uint32_t dwords = a.lds_pend_off / 4;
+  for (uint32_t i = tid; i < dwords; i += nthr) dist[i] = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < NB; i += nthr) pend[i] = 0u;
+  if (tid < 2) s_min[tid] = kInf;
+  __syncthreads();
+  if (tid == 0) {
+    bool first;
+    DW::lower(dist, s.node, DW::kInfT, 0u, first);
+    pend[s.node >> 5] = 1u << (s.node & 31u);
+  }
+  __syncthreads();
+
+  constexpr int kBatch = 16 / K;
+  constexpr int kScan = 8;  // pending distances read together
+  uint32_t D = 0;
+  for (uint32_t level = 0;; ++level) {
+    const uint32_t par = level & 1u;
+    if (tid == 0) s_min[par ^ 1u] = kInf;  // next level's slot, read one level ago
+    uint32_t local_min = kInf;
+    for (uint32_t w = tid; w < NB; w += 2 * nthr) {
+      const uint32_t w2 = w + nthr;
+      uint64_t bits = pend[w] | (static_cast<uint64_t>(w2 < NB ? pend[w2] : 0u) << 32);
+      // split the pending nodes into those at D (expand now) and the rest
+      // (candidates for the next D)
+      uint64_t todo = 0;
+      while (bits) {
+        uint32_t bs[kScan], dv[kScan];
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < kScan; ++i) {
+          if (bits) {
+            bs[i] = static_cast<uint32_t>(__builtin_ctzll(bits));
+            bits &= bits - 1;
+            const uint32_t v = bs[i] < 32 ? w * 32 + bs[i] : w2 * 32 + (bs[i] - 32);
+            dv[i] = DW::get(dist, v);
+            cnt = i + 1;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kScan; ++i) {
+          if (i < cnt) {
+            if (dv[i] == D) todo |= 1ull << bs[i];
+            else local_min = min(local_min, dv[i]);
+          }
+        }
+      }
+      if (!todo) continue;
+      if (static_cast<uint32_t>(todo)) atomicAnd(&pend[w], ~static_cast<uint32_t>(todo));
+      if (todo >> 32) atomicAnd(&pend[w2], ~static_cast<uint32_t>(todo >> 32));
+      while (todo) {
+        uint32_t vs[kBatch];
+        uint2 r[kBatch][K];
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i) {
+          if (todo) {
+            const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(todo));
+            todo &= todo - 1;
+            vs[i] = bit < 32 ? w * 32 + bit : w2 * 32 + (bit - 32);
+            load_recs<K>(a, vs[i], r[i]);
+            cnt = i + 1;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i)
+          if (i < cnt) local_min = min(local_min, d.expand(vs[i], r[i], D));
       }
     }
     const uint32_t wm = wave_min(local_min);
-    if (lane_id() == 0 && wm != 0xFFFFFFFFu) atomicMin(min_w, wm);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[par], wm);
     __syncthreads();
-    cur_n = *cnt_w;
-    // every level settles at least one node: > N levels would be a bug, and
-    // the bound guarantees every wave reaches the exit
-    if (cur_n == 0 || level >= N) break;
-    D = *min_w;
+    const uint32_t next = s_min[par];
+    if (next == kInf || level >= N) break;
+    D = next;
   }
 
-  // coalesced write-out of the dist row and the first-hop mask row
-  uint32_t* od = a.out_dist + static_cast<size_t>(sidx) * N;
-  uint32_t* on = a.out_nh + static_cast<size_t>(sidx) * N * a.words;
-  for (uint32_t i = tid; i < N; i += kBlock) {
-    const Word w = word[i];
-    const uint32_t d = P::dist(w);
-    const bool reach = d != P::kDistInf;
-    od[i] = reach ? d : 0xFFFFFFFFu;
-    if (a.words == 1) {
-      on[i] = reach ? P::mask(w) : 0u;
-    } else {
-      on[static_cast<size_t>(i) * a.words] = reach ? P::mask(w) : 0u;
-      for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
-    }
+  uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const uint32_t dv = DW::get(dist, i);
+    __builtin_nontemporal_store(dv == DW::kInfT ? kInf : dv, &out[i]);
   }
 }
 
 // ---------------------------------------------------------------------------
-// wide-mask kernel (KW): separate u32 dist and W mask words per node
+// phase 2: first-hop masks
 // ---------------------------------------------------------------------------
-template <typename IdT>
-__global__ __launch_bounds__(kBlock) void spf_wide_kernel(SpfArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_cnt;
   const uint32_t N = a.n_nodes;
-  const uint32_t W = a.words;
-  uint32_t* dist = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* mask = reinterpret_cast<uint32_t*>(smem + a.lds_mask_off);
-  IdT* lists = reinterpret_cast<IdT*>(smem + a.lds_list_off);
-  __shared__ uint32_t s_cnt[3];
-  __shared__ uint32_t s_min[3];
-
   const uint32_t tid = threadIdx.x;
-  const uint32_t sidx = blockIdx.x;
-  const uint32_t src = a.srcs[sidx];
-  const uint32_t ign_b = a.ignore_ptr ? a.ignore_ptr[sidx] : 0u;
-  const uint32_t n_ign = a.ignore_ptr ? a.ignore_ptr[sidx + 1] - ign_b : 0u;
-  const uint32_t* ign = a.ignore_links + ign_b;
+  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
+  const uint32_t src = a.srcs[i];
+  const uint32_t nb0 = a.nbr_ptr[i], nb = a.nbr_ptr[i + 1] - nb0;
+  uint32_t* minw = lds;
+  uint32_t* node = lds + nb;
+  uint4* ent = reinterpret_cast<uint4*>(lds + ((2 * nb + 3) & ~3u));
+  const uint32_t* ign = nullptr;
+  uint32_t n_ign = 0;
+  if (a.ignore_ptr) {
+    ign = a.ignore_links + a.ignore_ptr[i];
+    n_ign = a.ignore_ptr[i + 1] - a.ignore_ptr[i];
+  }
 
-  for (uint32_t i = tid; i < N; i += kBlock) dist[i] = 0xFFFFFFFFu;
-  for (uint32_t i = tid; i < N * W; i += kBlock) mask[i] = 0u;
-  if (tid < 3) {
-    s_cnt[tid] = 0;
-    s_min[tid] = 0xFFFFFFFFu;
+  for (uint32_t r = tid; r < nb; r += kBlock) minw[r] = kInf;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  // the source's links: smallest live metric per distinct neighbour
+  const uint32_t K = a.ell_k;
+  auto consider = [&](uint32_t q) {
+    const uint2 r = a.recs[q];
+    if (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) return;
+    if (n_ign && ignored(ign, n_ign, a.link[q])) return;
+    const uint32_t rk = a.rank_out[q];
+    atomicMin(&minw[rk], a.use_link_metric ? r.y : 1u);
+    node[rk] = r.x & ORH_REC_COL_MASK;
+  };
+  for (uint32_t j = tid; j < K; j += kBlock) consider(src * K + j);
+  const uint2 last = a.recs[static_cast<size_t>(src) * K + K - 1];
+  if (last.x & ORH_REC_CONT)
+    for (uint32_t j = tid; j < last.y; j += kBlock) consider((last.x & ORH_REC_COL_MASK) + j);
+  __syncthreads();
+  const uint32_t* ds = dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch),
+                                a.n_out, N, i);
+  // tight first links: d_s(n) equals the cheapest live link to n
+  for (uint32_t r = tid; r < nb; r += kBlock) {
+    if (minw[r] == kInf) continue;
+    const uint32_t u = node[r];
+    const uint32_t du = ds[u];
+    if (du != minw[r]) continue;
+    const uint32_t k = atomicAdd(&s_cnt, 1u);
+    ent[k] = make_uint4(u, du, a.nbr_row[nb0 + r], r | (a.overloaded[u] ? 0x80000000u : 0u));
   }
   __syncthreads();
-  if (tid == 0) {
-    dist[src] = 0;
-    lists[0] = static_cast<IdT>(src);
-  }
-  __syncthreads();
+  const uint32_t ne = s_cnt;
 
-  uint32_t cur_n = 1;
-  uint32_t D = 0;
-  const bool use_metric = a.use_link_metric != 0;
-  for (uint32_t level = 0;; ++level) {
-    IdT* in = lists + ((level & 1) ? N : 0);
-    IdT* out = lists + ((level & 1) ? 0 : N);
-    uint32_t* cnt_w = &s_cnt[level % 3];
-    uint32_t* min_w = &s_min[level % 3];
-    if (tid == 0) {
-      s_cnt[(level + 1) % 3] = 0;
-      s_min[(level + 1) % 3] = 0xFFFFFFFFu;
-    }
-    uint32_t local_min = 0xFFFFFFFFu;
-    for (uint32_t base = 0; base < cur_n; base += kBlock) {
-      const uint32_t i = base + tid;
-      const bool active = i < cur_n;
-      const uint32_t v = active ? static_cast<uint32_t>(in[i]) : 0u;
-      const uint32_t dv = active ? dist[v] : 0u;
-      const bool settle = active && dv == D;
-      wave_append(out, cnt_w, active && !settle, v);
-      if (active && !settle) local_min = min(local_min, dv);
-      if (settle) {
-        const bool transit = (v == src) || !a.node_overloaded[v];
-        const uint32_t e0 = a.row_ptr[v], e1 = a.row_ptr[v + 1];
-        for (uint32_t e = e0; e < e1; ++e) {
-          const uint4 rec = a.edges[e];
-          if (rec.w & ORH_META_DOWN_) continue;
-          if (n_ign && ignored(ign, n_ign, rec.w & ORH_META_LINK_MASK_)) continue;
-          const uint32_t u = rec.x;
-          const uint32_t w_out = use_metric ? rec.y : 1u;
-          const uint32_t w_in = use_metric ? rec.z : 1u;
-          if (v != src) {
-            const uint32_t du = dist[u];
-            const bool pred_transit = (u == src) || !(rec.w & ORH_META_COL_OVERLOADED_);
-            if (du < D && du + w_in == D && pred_transit) {
-              if (u == src) {
-                const uint32_t r = a.rank_in_col[e];
-                mask[static_cast<size_t>(v) * W + (r >> 5)] |= 1u << (r & 31u);
-              } else {
-                for (uint32_t k = 0; k < W; ++k)
-                  mask[static_cast<size_t>(v) * W + k] |= mask[static_cast<size_t>(u) * W + k];
-              }
-            }
-          }
-          if (transit) {
-            const uint32_t nd = D + w_out;
-            const uint32_t old = atomicMin(&dist[u], nd);
-            if (nd < old) local_min = min(local_min, nd);
-            wave_append(out, cnt_w, old == 0xFFFFFFFFu, u);
-          }
-        }
+  uint32_t v[kHopPer], dv[kHopPer];
+#pragma unroll
+  for (int k = 0; k < kHopPer; ++k) {
+    v[k] = tile * (kBlock * kHopPer) + k * kBlock + tid;
+    dv[k] = v[k] < N ? ds[v[k]] : kInf;
+    if (v[k] == src) dv[k] = kInf;  // the source has no next hops
+  }
+  const uint32_t W = a.words;
+  uint32_t* nh = a.out_nh + static_cast<size_t>(i) * N * W;
+  for (uint32_t word = 0; word < W; ++word) {
+    uint32_t acc[kHopPer] = {};
+    for (uint32_t e = 0; e < ne; ++e) {
+      const uint4 en = ent[e];
+      const uint32_t r = en.w & 0x7FFFFFFFu;
+      if ((r >> 5) != word) continue;
+      const uint32_t bit = 1u << (r & 31u);
+      const bool transit = !(en.w & 0x80000000u);
+      const uint32_t* dr = dist_row(const_cast<uint32_t*>(a.dist),
+                                    const_cast<uint32_t*>(a.scratch), a.n_out, N, en.z);
+      uint32_t x[kHopPer];
+#pragma unroll
+      for (int k = 0; k < kHopPer; ++k) x[k] = (transit && dv[k] != kInf) ? dr[v[k]] : kInf;
+#pragma unroll
+      for (int k = 0; k < kHopPer; ++k) {
+        if (dv[k] == kInf) continue;
+        if (v[k] == en.x ||
+            (x[k] != kInf && static_cast<uint64_t>(en.y) + x[k] == dv[k]))
+          acc[k] |= bit;
       }
     }
-    const uint32_t wm = wave_min(local_min);
-    if (lane_id() == 0 && wm != 0xFFFFFFFFu) atomicMin(min_w, wm);
-    __syncthreads();
-    cur_n = *cnt_w;
-    // every level settles at least one node: > N levels would be a bug, and
-    // the bound guarantees every wave reaches the exit
-    if (cur_n == 0 || level >= N) break;
-    D = *min_w;
+#pragma unroll
+    for (int k = 0; k < kHopPer; ++k)
+      if (v[k] < N) __builtin_nontemporal_store(acc[k], &nh[static_cast<size_t>(v[k]) * W + word]);
   }
-
-  uint32_t* od = a.out_dist + static_cast<size_t>(sidx) * N;
-  uint32_t* on = a.out_nh + static_cast<size_t>(sidx) * N * W;
-  for (uint32_t i = tid; i < N; i += kBlock) od[i] = dist[i];
-  for (uint32_t i = tid; i < N * W; i += kBlock) on[i] = mask[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -324,12 +531,12 @@ __global__ __launch_bounds__(kBlock) void route_select_kernel(RouteSelectArgs a)
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= a.n_prefix) return;
   const uint32_t b = a.adv_ptr[p], e = a.adv_ptr[p + 1];
-  uint32_t best = 0xFFFFFFFFu;
+  uint32_t best = kInf;
   for (uint32_t i = b; i < e; ++i) best = min(best, a.dist[a.adv[i]]);
   a.min_out[p] = best;
   for (uint32_t k = 0; k < a.words; ++k) {
     uint32_t m = 0;
-    if (best != 0xFFFFFFFFu) {
+    if (best != kInf) {
       for (uint32_t i = b; i < e; ++i) {
         const uint32_t v = a.adv[i];
         if (a.dist[v] == best) m |= a.nh[static_cast<size_t>(v) * a.words + k];
@@ -340,63 +547,80 @@ __global__ __launch_bounds__(kBlock) void route_select_kernel(RouteSelectArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// launchers
+// planning and launch
 // ---------------------------------------------------------------------------
-template <typename K>
-static hipError_t launch(K kernel, const SpfArgs& a, uint32_t grid, size_t lds, hipStream_t s) {
+template <typename Kern, typename Args>
+static hipError_t launch(Kern kernel, const Args& a, uint32_t grid, uint32_t block, size_t lds,
+                         hipStream_t s) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      static_cast<int>(lds));
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, a);
   return hipGetLastError();
 }
 
 static size_t align16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
 
-SpfPlan plan_spf(uint32_t n_nodes, uint32_t words, uint32_t max_nbr, uint64_t path_bound,
+SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
                  size_t lds_limit) {
   SpfPlan p{};
-  const size_t id_bytes = n_nodes <= 0xFFFFu ? 2 : 4;
-  p.id16 = id_bytes == 2;
-  const size_t lists = 2 * static_cast<size_t>(n_nodes) * id_bytes;
-  if (max_nbr <= 16 && path_bound < 0xFFFFu) {
-    p.variant = SpfVariant::kK16;
-    p.list_off = align16(static_cast<size_t>(n_nodes) * 4);
-    p.mask_off = 0;
-  } else if (max_nbr <= 32 && path_bound < 0xFFFFFFFFull) {
-    p.variant = SpfVariant::kK32;
-    p.list_off = align16(static_cast<size_t>(n_nodes) * 8);
-    p.mask_off = 0;
+  p.ell_k = ell_k;
+  if (ell_k != 4 && ell_k != 8) return p;
+  const size_t nb = (n_nodes + 31) / 32;
+  if (uniform && path_bound < 0xFFFFFFFFull) {
+    p.variant = SpfVariant::kBfs;
+    p.lds_bytes = 3 * nb * 4;
+  } else if (path_bound < 0xFFFFull) {
+    p.variant = SpfVariant::kDist16;
+    p.pend_off = align16(static_cast<size_t>(n_nodes) * 2);
+    p.lds_bytes = p.pend_off + align16(nb * 4);
   } else if (path_bound < 0xFFFFFFFFull) {
-    p.variant = SpfVariant::kWide;
-    p.mask_off = align16(static_cast<size_t>(n_nodes) * 4);
-    p.list_off = p.mask_off + align16(static_cast<size_t>(n_nodes) * 4 * words);
+    p.variant = SpfVariant::kDist32;
+    p.pend_off = align16(static_cast<size_t>(n_nodes) * 4);
+    p.lds_bytes = p.pend_off + align16(nb * 4);
   } else {
-    p.variant = SpfVariant::kUnsupported;
     return p;
   }
-  p.lds_bytes = p.list_off + align16(lists);
+  // a thread owns two bitmap words per pass; 256 threads cover N <= 16,384
+  // in one pass and leave room for 8 workgroups per CU
+  const uint32_t half = static_cast<uint32_t>((nb + 1) / 2);
+  p.block = std::min<uint32_t>(kMaxBlock, std::max<uint32_t>(256, (half + 63) / 64 * 64));
   if (p.lds_bytes > lds_limit) p.variant = SpfVariant::kUnsupported;
   return p;
 }
 
-hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_src, hipStream_t s) {
-  a.lds_list_off = static_cast<uint32_t>(plan.list_off);
-  a.lds_mask_off = static_cast<uint32_t>(plan.mask_off);
+template <int K>
+static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   switch (plan.variant) {
-    case SpfVariant::kK16:
-      return plan.id16 ? launch(spf_packed_kernel<K16, uint16_t>, a, n_src, plan.lds_bytes, s)
-                       : launch(spf_packed_kernel<K16, uint32_t>, a, n_src, plan.lds_bytes, s);
-    case SpfVariant::kK32:
-      return plan.id16 ? launch(spf_packed_kernel<K32, uint16_t>, a, n_src, plan.lds_bytes, s)
-                       : launch(spf_packed_kernel<K32, uint32_t>, a, n_src, plan.lds_bytes, s);
-    case SpfVariant::kWide:
-      return plan.id16 ? launch(spf_wide_kernel<uint16_t>, a, n_src, plan.lds_bytes, s)
-                       : launch(spf_wide_kernel<uint32_t>, a, n_src, plan.lds_bytes, s);
+    case SpfVariant::kBfs:
+      return launch(spf_bfs_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kDist16:
+      return launch(spf_dist_kernel<uint16_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kDist32:
+      return launch(spf_dist_kernel<uint32_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
     default:
       return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  a.lds_pend_off = static_cast<uint32_t>(plan.pend_off);
+  return plan.ell_k == 8 ? launch_k<8>(plan, a, n_rows, s) : launch_k<4>(plan, a, n_rows, s);
+}
+
+size_t hop_lds_bytes(uint32_t max_nbr) {
+  return static_cast<size_t>((2 * max_nbr + 3) & ~3u) * 4 + static_cast<size_t>(max_nbr) * 16;
+}
+
+hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s) {
+  if (a.n_out == 0) return hipSuccess;
+  a.tiles = (a.n_nodes + kBlock * kHopPer - 1) / (kBlock * kHopPer);
+  const uint64_t grid = static_cast<uint64_t>(a.tiles) * a.n_out;
+  if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock,
+                std::max<size_t>(hop_lds_bytes(max_nbr), 16), s);
 }
 
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s) {

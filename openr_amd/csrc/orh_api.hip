@@ -1,8 +1,8 @@
 // libopenr_hip: C ABI (include/openr_hip.h) over the gfx950 SPF kernels.
 //
-// Owns per-device contexts (stream, events, counters) and per-area graph
-// mirrors (device CSR of 16-byte edge records, row offsets, node flags and
-// the neighbour-rank table used to number first-hop bits).
+// Owns per-device contexts (stream, events, counters, request staging,
+// scratch distance rows) and per-area graph mirrors (ELL edge records, link
+// ids, node flags and the neighbour-rank table that numbers first-hop bits).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,29 +18,42 @@
 struct orh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;  // around phase 1 | phase 2
   size_t lds_limit = 160 * 1024;
   std::string err;
   orh_counters counters{};
-  // reusable device staging for request arrays
+  // reusable device staging for request arrays, keyed by the request that
+  // filled it (a repeated sweep skips the host rebuild and the upload)
   uint32_t* d_req = nullptr;
   size_t d_req_cap = 0;
+  std::vector<uint32_t> req_key;
+  // distance rows of neighbours that are not themselves requested sources
+  uint32_t* d_scratch = nullptr;
+  size_t d_scratch_cap = 0;  // in u32
 };
 
 struct orh_graph {
   orh_ctx* ctx = nullptr;
+  uint64_t gen = 0;  // bumped on every structural load
   uint32_t n_nodes = 0, n_edges = 0, n_links = 0;
-  // host copies (needed for deltas, neighbour tables and bounds)
+  // host CSR (ABI semantics) kept for deltas, neighbour tables and bounds
   std::vector<uint32_t> row_ptr, col, w_out, w_in, meta;
   std::vector<uint8_t> overloaded;
-  std::vector<uint32_t> n_distinct;  // distinct neighbour count per node
-  uint64_t sum_max_metric = 0;       // sum over links of max(w_out, w_in)
+  std::vector<uint32_t> dn_ptr, dn;  // distinct neighbours per node, ascending id
+  std::vector<uint16_t> rank_out;    // per CSR entry: col's rank among row's distinct neighbours
+  uint64_t sum_max_metric = 0;       // sum over up CSR entries of max(w_out, w_in)
   uint32_t max_metric = 0;
-  // device mirror
-  uint32_t* d_row_ptr = nullptr;
-  uint4* d_edges = nullptr;
-  uint16_t* d_rank = nullptr;
-  uint8_t* d_overloaded = nullptr;
+  uint32_t min_out = 0, max_out = 0;  // w_out range over up CSR entries
+  // device layout: ELL slots v*K .. v*K+K-1, the last one a continuation
+  // record into the overflow area when deg(v) > K
+  uint32_t ell_k = 4;
+  uint32_t n_recs = 0;
+  std::vector<uint32_t> pos;  // CSR entry -> device record index
+  uint2* d_recs = nullptr;
+  uint32_t* d_link = nullptr;
+  uint16_t* d_rank_out = nullptr;
+  uint8_t* d_ovl = nullptr;
+  std::vector<int32_t> row_of;  // scratch for orh_spf_run (all -1 between calls)
 };
 
 namespace {
@@ -54,75 +67,139 @@ int hip_fail(orh_ctx* ctx, hipError_t e, const char* what) {
   return fail(ctx, ORH_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define ORH_HIP(ctx, call)                              \
-  do {                                                  \
-    hipError_t e_ = (call);                             \
+#define ORH_HIP(ctx, call)                                 \
+  do {                                                     \
+    hipError_t e_ = (call);                                \
     if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
   } while (0)
 
 void free_graph_device(orh_graph* g) {
-  hipFree(g->d_row_ptr);
-  hipFree(g->d_edges);
-  hipFree(g->d_rank);
-  hipFree(g->d_overloaded);
-  g->d_row_ptr = nullptr;
-  g->d_edges = nullptr;
-  g->d_rank = nullptr;
-  g->d_overloaded = nullptr;
+  (void)hipFree(g->d_recs);
+  (void)hipFree(g->d_link);
+  (void)hipFree(g->d_rank_out);
+  (void)hipFree(g->d_ovl);
+  g->d_recs = nullptr;
+  g->d_link = nullptr;
+  g->d_rank_out = nullptr;
+  g->d_ovl = nullptr;
 }
 
-// rank of the row node among col's distinct neighbours (ascending id)
-std::vector<uint16_t> build_ranks(const orh_graph* g, std::vector<uint32_t>& n_distinct) {
+// distinct neighbour lists and, per CSR entry, the neighbour's rank in its
+// row's list (= the first-hop bit of that neighbour)
+void build_neighbours(orh_graph* g) {
   const uint32_t N = g->n_nodes;
-  std::vector<std::vector<uint32_t>> nbrs(N);
-  n_distinct.assign(N, 0);
+  g->dn_ptr.assign(N + 1, 0);
+  g->dn.clear();
+  g->rank_out.assign(g->n_edges, 0);
+  std::vector<uint32_t> l;
   for (uint32_t v = 0; v < N; ++v) {
-    auto& l = nbrs[v];
-    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) l.push_back(g->col[e]);
+    l.assign(g->col.begin() + g->row_ptr[v], g->col.begin() + g->row_ptr[v + 1]);
     std::sort(l.begin(), l.end());
     l.erase(std::unique(l.begin(), l.end()), l.end());
-    n_distinct[v] = static_cast<uint32_t>(l.size());
+    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e)
+      g->rank_out[e] = static_cast<uint16_t>(
+          std::lower_bound(l.begin(), l.end(), g->col[e]) - l.begin());
+    g->dn.insert(g->dn.end(), l.begin(), l.end());
+    g->dn_ptr[v + 1] = static_cast<uint32_t>(g->dn.size());
   }
-  std::vector<uint16_t> rank(g->n_edges, 0);
-  for (uint32_t v = 0; v < N; ++v) {
-    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) {
-      const auto& l = nbrs[g->col[e]];
-      const auto it = std::lower_bound(l.begin(), l.end(), v);
-      const size_t r = static_cast<size_t>(it - l.begin());
-      rank[e] = static_cast<uint16_t>(std::min<size_t>(r, 0xFFFF));
-    }
-  }
-  return rank;
 }
 
-int upload_edges(orh_graph* g, uint32_t first, uint32_t count) {
-  std::vector<uint4> rec(count);
-  for (uint32_t i = 0; i < count; ++i) {
-    const uint32_t e = first + i;
-    rec[i] = make_uint4(g->col[e], g->w_out[e], g->w_in[e], g->meta[e]);
+uint32_t n_distinct(const orh_graph* g, uint32_t v) { return g->dn_ptr[v + 1] - g->dn_ptr[v]; }
+
+// ELL width: smallest power of two covering 90% of the node degrees, in [4, 8]
+uint32_t choose_ell_k(const orh_graph* g) {
+  std::vector<uint32_t> deg(g->n_nodes);
+  for (uint32_t v = 0; v < g->n_nodes; ++v) deg[v] = g->row_ptr[v + 1] - g->row_ptr[v];
+  if (deg.empty()) return 4;
+  std::nth_element(deg.begin(), deg.begin() + deg.size() * 9 / 10, deg.end());
+  return deg[deg.size() * 9 / 10] > 4 ? 8 : 4;
+}
+
+uint2 device_record(const orh_graph* g, uint32_t v, uint32_t e) {
+  uint32_t x = g->col[e];
+  if (g->meta[e] & ORH_META_DOWN) x |= ORH_REC_SKIP;
+  if (g->overloaded[v]) x |= ORH_REC_ROW_OVL;
+  return make_uint2(x, g->w_out[e]);
+}
+
+void build_layout(orh_graph* g, std::vector<uint2>& recs, std::vector<uint32_t>& link,
+                  std::vector<uint16_t>& rank) {
+  const uint32_t K = g->ell_k, N = g->n_nodes;
+  size_t n = static_cast<size_t>(N) * K;
+  for (uint32_t v = 0; v < N; ++v) {
+    const uint32_t d = g->row_ptr[v + 1] - g->row_ptr[v];
+    if (d > K) n += d - (K - 1);
   }
-  ORH_HIP(g->ctx, hipMemcpyAsync(g->d_edges + first, rec.data(), count * sizeof(uint4),
+  recs.assign(std::max<size_t>(n, 1), make_uint2(ORH_REC_SKIP, 1));
+  link.assign(recs.size(), 0);
+  rank.assign(recs.size(), 0);
+  g->pos.assign(g->n_edges, 0);
+  uint32_t ovf = N * K;
+  for (uint32_t v = 0; v < N; ++v) {
+    const uint32_t e0 = g->row_ptr[v], d = g->row_ptr[v + 1] - e0, base = v * K;
+    const uint32_t inl = d <= K ? d : K - 1;
+    for (uint32_t j = 0; j < inl; ++j) g->pos[e0 + j] = base + j;
+    if (d > K) {
+      recs[base + K - 1] = make_uint2(ovf | ORH_REC_CONT, d - inl);
+      for (uint32_t j = inl; j < d; ++j) g->pos[e0 + j] = ovf++;
+    }
+    for (uint32_t j = 0; j < d; ++j) {
+      const uint32_t q = g->pos[e0 + j];
+      recs[q] = device_record(g, v, e0 + j);
+      link[q] = g->meta[e0 + j] & ORH_META_LINK_MASK;
+      rank[q] = g->rank_out[e0 + j];
+    }
+  }
+  g->n_recs = static_cast<uint32_t>(recs.size());
+}
+
+int upload_record(orh_graph* g, uint32_t v, uint32_t e) {
+  const uint2 r = device_record(g, v, e);
+  ORH_HIP(g->ctx, hipMemcpyAsync(g->d_recs + g->pos[e], &r, sizeof(uint2),
                                  hipMemcpyHostToDevice, g->ctx->stream));
+  ORH_HIP(g->ctx, hipStreamSynchronize(g->ctx->stream));  // r lives on this stack frame
   return ORH_OK;
+}
+
+uint32_t row_of(const orh_graph* g, uint32_t e) {
+  return static_cast<uint32_t>(std::upper_bound(g->row_ptr.begin(), g->row_ptr.end(), e) -
+                               g->row_ptr.begin()) - 1;
 }
 
 void recompute_bounds(orh_graph* g) {
   g->sum_max_metric = 0;
   g->max_metric = 0;
+  g->min_out = 0xFFFFFFFFu;
+  g->max_out = 0;
   for (uint32_t e = 0; e < g->n_edges; ++e) {
+    if (g->meta[e] & ORH_META_DOWN) continue;
     const uint32_t m = std::max(g->w_out[e], g->w_in[e]);
     g->max_metric = std::max(g->max_metric, m);
     g->sum_max_metric += m;  // each link is counted twice (both CSR entries)
+    g->min_out = std::min(g->min_out, g->w_out[e]);
+    g->max_out = std::max(g->max_out, g->w_out[e]);
   }
+  if (g->max_out == 0) g->min_out = g->max_out = 1;  // no up link
 }
 
 int ensure_req(orh_ctx* ctx, size_t words) {
   if (words <= ctx->d_req_cap) return ORH_OK;
   hipFree(ctx->d_req);
   ctx->d_req = nullptr;
+  ctx->req_key.clear();
   const size_t cap = std::max<size_t>(words, 4096);
   ORH_HIP(ctx, hipMalloc(&ctx->d_req, cap * sizeof(uint32_t)));
   ctx->d_req_cap = cap;
+  return ORH_OK;
+}
+
+int ensure_scratch(orh_ctx* ctx, size_t words) {
+  if (words <= ctx->d_scratch_cap) return ORH_OK;
+  hipFree(ctx->d_scratch);
+  ctx->d_scratch = nullptr;
+  ctx->d_scratch_cap = 0;
+  ORH_HIP(ctx, hipMalloc(&ctx->d_scratch, words * sizeof(uint32_t)));
+  ctx->d_scratch_cap = words;
   return ORH_OK;
 }
 
@@ -150,7 +227,8 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
   ctx->device = device;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->evm) != hipSuccess ||
+      hipEventCreate(&ctx->ev1) != hipSuccess) {
     delete ctx;
     return ORH_E_DEVICE;
   }
@@ -167,7 +245,9 @@ int orh_destroy(orh_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipFree(ctx->d_req);
+  hipFree(ctx->d_scratch);
   hipEventDestroy(ctx->ev0);
+  hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
   hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -241,6 +321,8 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
     return fail(ctx, ORH_E_INVALID, "orh_graph_load: null array");
   if (c->row_ptr[0] != 0 || c->row_ptr[c->n_nodes] != c->n_edges)
     return fail(ctx, ORH_E_INVALID, "orh_graph_load: row_ptr does not span n_edges");
+  if (c->n_nodes > ORH_REC_COL_MASK)
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_load: more than 2^27 nodes");
   for (uint32_t v = 0; v < c->n_nodes; ++v)
     if (c->row_ptr[v] > c->row_ptr[v + 1])
       return fail(ctx, ORH_E_INVALID, "orh_graph_load: row_ptr not monotone");
@@ -250,7 +332,7 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
       return fail(ctx, ORH_E_UNSUPPORTED,
                   "orh_graph_load: metric 0 on an up link (closed-form SPF needs metrics >= 1)");
   }
-  hipSetDevice(ctx->device);
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   free_graph_device(g);
   g->n_nodes = c->n_nodes;
@@ -262,31 +344,35 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   g->w_in.assign(c->w_in, c->w_in + c->n_edges);
   g->meta.assign(c->meta, c->meta + c->n_edges);
   g->overloaded.assign(c->node_overloaded, c->node_overloaded + c->n_nodes);
-  for (uint32_t e = 0; e < g->n_edges; ++e) {
-    g->meta[e] = (g->meta[e] & ~ORH_META_COL_OVERLOADED) |
-        (g->overloaded[g->col[e]] ? ORH_META_COL_OVERLOADED : 0u);
-  }
+  for (auto& o : g->overloaded) o = o ? 1 : 0;
+  g->gen += 1;
+  g->row_of.assign(g->n_nodes, -1);
   recompute_bounds(g);
-  const auto rank = build_ranks(g, g->n_distinct);
-
-  const size_t ne = std::max<uint32_t>(g->n_edges, 1), nn = std::max<uint32_t>(g->n_nodes, 1);
-  if (hipMalloc(&g->d_row_ptr, (nn + 1) * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&g->d_edges, ne * sizeof(uint4)) != hipSuccess ||
-      hipMalloc(&g->d_rank, ne * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&g->d_overloaded, nn) != hipSuccess) {
+  build_neighbours(g);
+  for (uint32_t v = 0; v < g->n_nodes; ++v)
+    if (n_distinct(g, v) > 0xFFFFu)
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_load: more than 65535 neighbours");
+  g->ell_k = choose_ell_k(g);
+  std::vector<uint2> recs;
+  std::vector<uint32_t> link;
+  std::vector<uint16_t> rank;
+  build_layout(g, recs, link, rank);
+  const size_t nn = std::max<uint32_t>(g->n_nodes, 1);
+  if (hipMalloc(&g->d_recs, recs.size() * sizeof(uint2)) != hipSuccess ||
+      hipMalloc(&g->d_link, link.size() * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&g->d_rank_out, rank.size() * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&g->d_ovl, nn) != hipSuccess) {
     free_graph_device(g);
     return fail(ctx, ORH_E_NOMEM, "orh_graph_load: device allocation failed");
   }
-  ORH_HIP(ctx, hipMemcpyAsync(g->d_row_ptr, g->row_ptr.data(), g->row_ptr.size() * 4,
+  ORH_HIP(ctx, hipMemcpyAsync(g->d_recs, recs.data(), recs.size() * sizeof(uint2),
                               hipMemcpyHostToDevice, ctx->stream));
-  if (g->n_edges) {
-    int rc = upload_edges(g, 0, g->n_edges);
-    if (rc) return rc;
-    ORH_HIP(ctx, hipMemcpyAsync(g->d_rank, rank.data(), rank.size() * 2, hipMemcpyHostToDevice,
-                                ctx->stream));
-  }
+  ORH_HIP(ctx, hipMemcpyAsync(g->d_link, link.data(), link.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipMemcpyAsync(g->d_rank_out, rank.data(), rank.size() * sizeof(uint16_t),
+                              hipMemcpyHostToDevice, ctx->stream));
   if (g->n_nodes)
-    ORH_HIP(ctx, hipMemcpyAsync(g->d_overloaded, g->overloaded.data(), g->n_nodes,
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl, g->overloaded.data(), g->n_nodes,
                                 hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
@@ -296,7 +382,7 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
                           const uint32_t* w_in, const uint32_t* meta) {
   if (!g || (n && (!idx || !w_out || !w_in || !meta))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
-  if (!g->d_edges && n) return fail(ctx, ORH_E_STATE, "orh_graph_patch_edges: no graph loaded");
+  if (!g->d_recs && n) return fail(ctx, ORH_E_STATE, "orh_graph_patch_edges: no graph loaded");
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = idx[i];
     if (e >= g->n_edges) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: bad edge index");
@@ -305,43 +391,33 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
     if (!(meta[i] & ORH_META_DOWN) && (w_out[i] == 0 || w_in[i] == 0))
       return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_patch_edges: metric 0 on an up link");
   }
-  hipSetDevice(ctx->device);
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = idx[i];
     g->w_out[e] = w_out[i];
     g->w_in[e] = w_in[i];
-    g->meta[e] = (meta[i] & ~ORH_META_COL_OVERLOADED) | (g->meta[e] & ORH_META_COL_OVERLOADED);
-    int rc = upload_edges(g, e, 1);
+    g->meta[e] = meta[i] & ~ORH_META_COL_OVERLOADED;
+    int rc = upload_record(g, row_of(g, e), e);
     if (rc) return rc;
   }
   recompute_bounds(g);
-  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
 
 int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* idx, const uint8_t* ovl) {
   if (!g || (n && (!idx || !ovl))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
-  hipSetDevice(ctx->device);
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
   for (uint32_t i = 0; i < n; ++i) {
     if (idx[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_nodes: bad node");
     const uint32_t v = idx[i];
     g->overloaded[v] = ovl[i] ? 1 : 0;
-    ORH_HIP(ctx, hipMemcpyAsync(g->d_overloaded + v, &g->overloaded[v], 1,
-                                hipMemcpyHostToDevice, ctx->stream));
-    // CSR entries that point at v carry v's overload bit
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl + v, &g->overloaded[v], 1, hipMemcpyHostToDevice,
+                                ctx->stream));
+    // v's own records carry its row bit
     for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) {
-      const uint32_t u = g->col[e];
-      for (uint32_t e2 = g->row_ptr[u]; e2 < g->row_ptr[u + 1]; ++e2) {
-        if (g->col[e2] != v) continue;
-        const uint32_t m = (g->meta[e2] & ~ORH_META_COL_OVERLOADED) |
-            (g->overloaded[v] ? ORH_META_COL_OVERLOADED : 0u);
-        if (m != g->meta[e2]) {
-          g->meta[e2] = m;
-          int rc = upload_edges(g, e2, 1);
-          if (rc) return rc;
-        }
-      }
+      int rc = upload_record(g, v, e);
+      if (rc) return rc;
     }
   }
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -359,11 +435,9 @@ int orh_graph_neighbors(const orh_graph* g, uint32_t src, uint32_t* out, uint32_
                         uint32_t* n_out) {
   if (!g || !n_out) return ORH_E_INVALID;
   if (src >= g->n_nodes) return ORH_E_INVALID;
-  std::vector<uint32_t> l(g->col.begin() + g->row_ptr[src], g->col.begin() + g->row_ptr[src + 1]);
-  std::sort(l.begin(), l.end());
-  l.erase(std::unique(l.begin(), l.end()), l.end());
-  *n_out = static_cast<uint32_t>(l.size());
-  for (uint32_t i = 0; i < l.size() && i < cap; ++i) out[i] = l[i];
+  const uint32_t n = n_distinct(g, src);
+  *n_out = n;
+  for (uint32_t i = 0; i < n && i < cap; ++i) out[i] = g->dn[g->dn_ptr[src] + i];
   return ORH_OK;
 }
 
@@ -372,74 +446,184 @@ int orh_spf_words(const orh_graph* g, const uint32_t* srcs, uint32_t n, uint32_t
   uint32_t mx = 1;
   for (uint32_t i = 0; i < n; ++i) {
     if (srcs[i] >= g->n_nodes) return ORH_E_INVALID;
-    mx = std::max(mx, g->n_distinct[srcs[i]]);
+    mx = std::max(mx, n_distinct(g, srcs[i]));
   }
   *out = (mx + 31) / 32;
   return ORH_OK;
 }
 
+// Phase 1 computes a distance row for every requested source and for every
+// distinct neighbour of one (the first-hop phase reads them). Without ignore
+// sets rows are shared by node: a neighbour that is itself requested reuses
+// its output row, the others get scratch rows. With per-source ignore sets a
+// source's neighbour rows are its own (same ignore set).
 int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32_t* d_dist,
                 uint32_t* d_nh) {
   if (!g || !req || (req->n_src && (!req->h_srcs || !d_dist || !d_nh)))
     return g ? fail(g->ctx, ORH_E_INVALID, "orh_spf_run: null argument") : ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
   if (req->n_src == 0) return ORH_OK;
-  if (!g->d_row_ptr || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_spf_run: no graph loaded");
+  if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_spf_run: no graph loaded");
+  const uint32_t n_src = req->n_src, N = g->n_nodes;
   uint32_t max_nbr = 1;
-  for (uint32_t i = 0; i < req->n_src; ++i) {
-    if (req->h_srcs[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_spf_run: source out of range");
-    max_nbr = std::max(max_nbr, g->n_distinct[req->h_srcs[i]]);
+  for (uint32_t i = 0; i < n_src; ++i) {
+    if (req->h_srcs[i] >= N) return fail(ctx, ORH_E_INVALID, "orh_spf_run: source out of range");
+    max_nbr = std::max(max_nbr, n_distinct(g, req->h_srcs[i]));
   }
   if (words < (max_nbr + 31) / 32) return fail(ctx, ORH_E_INVALID, "orh_spf_run: words too small");
-  // any tentative value D + w is at most (sum of link metrics) + max metric
-  const uint64_t bound = req->use_link_metric
-      ? g->sum_max_metric / 2 + g->max_metric
-      : static_cast<uint64_t>(g->n_links) + 1;
-  const orh::SpfPlan plan = orh::plan_spf(g->n_nodes, words, max_nbr, bound, ctx->lds_limit);
+  const bool uniform = !req->use_link_metric || g->min_out == g->max_out;
+  const uint32_t w0 = req->use_link_metric ? g->max_out : 1u;
+  // any tentative value is at most (sum of link metrics) + max metric; BFS
+  // levels at most (N - 1) * w0
+  const uint64_t bound = uniform ? static_cast<uint64_t>(N) * w0
+      : req->use_link_metric ? g->sum_max_metric / 2 + g->max_metric
+                             : static_cast<uint64_t>(g->n_links) + 1;
+  const orh::SpfPlan plan = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit);
   if (plan.variant == orh::SpfVariant::kUnsupported)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: graph exceeds the LDS-resident kernels (N=" +
-                                            std::to_string(g->n_nodes) + ")");
-
-  // stage sources and ignore sets in one device buffer
-  const bool has_ign = req->h_ignore_ptr != nullptr;
-  const uint32_t n_ign = has_ign ? req->h_ignore_ptr[req->n_src] : 0u;
-  const size_t total = req->n_src + (has_ign ? (req->n_src + 1 + n_ign) : 0);
+                                            std::to_string(N) + ")");
+  if (orh::hop_lds_bytes(max_nbr) > ctx->lds_limit)
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: too many neighbours for the first-hop phase");
   hipSetDevice(ctx->device);
-  int rc = ensure_req(ctx, total);
-  if (rc) return rc;
-  std::vector<uint32_t> staging;
-  staging.reserve(total);
-  staging.insert(staging.end(), req->h_srcs, req->h_srcs + req->n_src);
+
+  const bool has_ign = req->h_ignore_ptr != nullptr;
+  const uint32_t n_ign = has_ign ? req->h_ignore_ptr[n_src] : 0u;
+  // request key: graph generation + sources + ignore sets
+  std::vector<uint32_t> key;
+  key.reserve(6 + n_src + (has_ign ? n_src + 1 + n_ign : 0));
+  const uint64_t gp = reinterpret_cast<uintptr_t>(g);
+  key.insert(key.end(), {static_cast<uint32_t>(gp), static_cast<uint32_t>(gp >> 32),
+                         static_cast<uint32_t>(g->gen), static_cast<uint32_t>(g->gen >> 32),
+                         n_src, has_ign ? 1u : 0u});
+  key.insert(key.end(), req->h_srcs, req->h_srcs + n_src);
   if (has_ign) {
-    staging.insert(staging.end(), req->h_ignore_ptr, req->h_ignore_ptr + req->n_src + 1);
-    for (uint32_t i = 0; i < req->n_src; ++i) {  // each source's set sorted for bsearch
-      std::vector<uint32_t> s(req->h_ignore_links + req->h_ignore_ptr[i],
-                              req->h_ignore_links + req->h_ignore_ptr[i + 1]);
-      std::sort(s.begin(), s.end());
-      staging.insert(staging.end(), s.begin(), s.end());
-    }
+    key.insert(key.end(), req->h_ignore_ptr, req->h_ignore_ptr + n_src + 1);
+    key.insert(key.end(), req->h_ignore_links, req->h_ignore_links + n_ign);
   }
-  ORH_HIP(ctx, hipMemcpyAsync(ctx->d_req, staging.data(), staging.size() * 4,
-                              hipMemcpyHostToDevice, ctx->stream));
+  // staged layout: srcs[n_rows] | ign_ptr[n_rows+1] ign[..] | nbr_ptr[n_src+1] nbr_row[..]
+  uint32_t n_rows = n_src;
+  size_t off_ign_ptr = 0, off_ign = 0, off_nbr_ptr = 0, off_nbr_row = 0;
+  if (key != ctx->req_key) {
+    std::vector<uint32_t> srcs(req->h_srcs, req->h_srcs + n_src), nbr_ptr(n_src + 1, 0), nbr_row;
+    std::vector<uint32_t> ign_ptr, ign;
+    std::vector<uint32_t> row_owner;  // source index whose ignore set a row uses
+    if (!has_ign) {
+      auto& ro = g->row_of;
+      for (uint32_t i = 0; i < n_src; ++i)
+        if (ro[req->h_srcs[i]] < 0) ro[req->h_srcs[i]] = static_cast<int32_t>(i);
+      for (uint32_t i = 0; i < n_src; ++i) {
+        const uint32_t s = req->h_srcs[i];
+        for (uint32_t k = g->dn_ptr[s]; k < g->dn_ptr[s + 1]; ++k) {
+          const uint32_t u = g->dn[k];
+          if (ro[u] < 0) {
+            ro[u] = static_cast<int32_t>(srcs.size());
+            srcs.push_back(u);
+          }
+          nbr_row.push_back(static_cast<uint32_t>(ro[u]));
+        }
+        nbr_ptr[i + 1] = static_cast<uint32_t>(nbr_row.size());
+      }
+      for (uint32_t u : srcs) ro[u] = -1;
+    } else {
+      ign_ptr.assign(1, 0);
+      auto add_set = [&](uint32_t i) {
+        std::vector<uint32_t> s(req->h_ignore_links + req->h_ignore_ptr[i],
+                                req->h_ignore_links + req->h_ignore_ptr[i + 1]);
+        std::sort(s.begin(), s.end());  // bsearch on device
+        ign.insert(ign.end(), s.begin(), s.end());
+        ign_ptr.push_back(static_cast<uint32_t>(ign.size()));
+      };
+      for (uint32_t i = 0; i < n_src; ++i) add_set(i);
+      for (uint32_t i = 0; i < n_src; ++i) {
+        const uint32_t s = req->h_srcs[i];
+        for (uint32_t k = g->dn_ptr[s]; k < g->dn_ptr[s + 1]; ++k) {
+          nbr_row.push_back(static_cast<uint32_t>(srcs.size()));
+          srcs.push_back(g->dn[k]);
+          add_set(i);
+        }
+        nbr_ptr[i + 1] = static_cast<uint32_t>(nbr_row.size());
+      }
+    }
+    n_rows = static_cast<uint32_t>(srcs.size());
+    std::vector<uint32_t> staging;
+    staging.reserve(srcs.size() + ign_ptr.size() + ign.size() + nbr_ptr.size() + nbr_row.size() + 1);
+    staging.push_back(n_rows);
+    staging.insert(staging.end(), srcs.begin(), srcs.end());
+    off_ign_ptr = staging.size();
+    staging.insert(staging.end(), ign_ptr.begin(), ign_ptr.end());
+    off_ign = staging.size();
+    staging.insert(staging.end(), ign.begin(), ign.end());
+    off_nbr_ptr = staging.size();
+    staging.insert(staging.end(), nbr_ptr.begin(), nbr_ptr.end());
+    off_nbr_row = staging.size();
+    staging.insert(staging.end(), nbr_row.begin(), nbr_row.end());
+    int rc = ensure_req(ctx, staging.size());
+    if (rc) return rc;
+    ORH_HIP(ctx, hipMemcpyAsync(ctx->d_req, staging.data(), staging.size() * 4,
+                                hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
+    key.push_back(static_cast<uint32_t>(off_ign_ptr));
+    key.push_back(static_cast<uint32_t>(off_ign));
+    key.push_back(static_cast<uint32_t>(off_nbr_ptr));
+    key.push_back(static_cast<uint32_t>(off_nbr_row));
+    key.push_back(n_rows);
+    ctx->req_key = std::move(key);
+  }
+  {
+    const auto& k = ctx->req_key;
+    const size_t t = k.size();
+    off_ign_ptr = k[t - 5];
+    off_ign = k[t - 4];
+    off_nbr_ptr = k[t - 3];
+    off_nbr_row = k[t - 2];
+    n_rows = k[t - 1];
+  }
+  const size_t n_extra = n_rows - n_src;
+  if (n_extra) {
+    int rc = ensure_scratch(ctx, n_extra * N);
+    if (rc) return rc;
+  }
 
   orh::SpfArgs a{};
-  a.n_nodes = g->n_nodes;
-  a.words = words;
-  a.row_ptr = g->d_row_ptr;
-  a.edges = g->d_edges;
-  a.rank_in_col = g->d_rank;
-  a.node_overloaded = g->d_overloaded;
-  a.srcs = ctx->d_req;
-  a.ignore_ptr = has_ign ? ctx->d_req + req->n_src : nullptr;
-  a.ignore_links = has_ign ? ctx->d_req + 2 * req->n_src + 1 : nullptr;
+  a.n_nodes = N;
+  a.n_out = n_src;
+  a.recs = g->d_recs;
+  a.link = g->d_link;
+  a.srcs = ctx->d_req + 1;
+  a.ignore_ptr = has_ign ? ctx->d_req + off_ign_ptr : nullptr;
+  a.ignore_links = has_ign ? ctx->d_req + off_ign : nullptr;
   a.use_link_metric = req->use_link_metric;
+  a.w0 = w0;
   a.out_dist = d_dist;
-  a.out_nh = d_nh;
+  a.scratch = ctx->d_scratch;
+
+  orh::HopArgs h{};
+  h.n_nodes = N;
+  h.n_out = n_src;
+  h.words = words;
+  h.ell_k = g->ell_k;
+  h.recs = g->d_recs;
+  h.link = g->d_link;
+  h.rank_out = g->d_rank_out;
+  h.overloaded = g->d_ovl;
+  h.srcs = a.srcs;
+  h.ignore_ptr = a.ignore_ptr;
+  h.ignore_links = a.ignore_links;
+  h.use_link_metric = req->use_link_metric;
+  h.nbr_ptr = ctx->d_req + off_nbr_ptr;
+  h.nbr_row = ctx->d_req + off_nbr_row;
+  h.dist = d_dist;
+  h.scratch = ctx->d_scratch;
+  h.out_nh = d_nh;
+
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  hipError_t e = orh::launch_spf(plan, a, req->n_src, ctx->stream);
+  hipError_t e = orh::launch_spf(plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "spf kernel launch");
+  ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
+  e = orh::launch_first_hop(h, max_nbr, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
   ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->counters.spf_runs += req->n_src;
+  ctx->counters.spf_runs += n_src;
   ctx->counters.spf_launches += 1;
   ctx->counters.last_kernel_ms = -1.0;  // resolved lazily by orh_spf_batch / orh_sync users
   return ORH_OK;
@@ -502,5 +686,16 @@ extern "C" int orh_last_spf_ms(orh_ctx* ctx, double* ms_out) {
   *ms_out = ms;
   ctx->counters.last_kernel_ms = ms;
   ctx->counters.total_kernel_ms += ms;
+  return ORH_OK;
+}
+
+extern "C" int orh_last_spf_phase_ms(orh_ctx* ctx, double* dist_ms, double* hop_ms) {
+  if (!ctx || !dist_ms || !hop_ms) return ORH_E_INVALID;
+  ORH_HIP(ctx, hipEventSynchronize(ctx->ev1));
+  float a = 0.f, b = 0.f;
+  ORH_HIP(ctx, hipEventElapsedTime(&a, ctx->ev0, ctx->evm));
+  ORH_HIP(ctx, hipEventElapsedTime(&b, ctx->evm, ctx->ev1));
+  *dist_ms = a;
+  *hop_ms = b;
   return ORH_OK;
 }

@@ -220,3 +220,51 @@ def test_ordered_fib_holds(hip, oracle):
         assert als_h[A].has_holds() == als_o[A].has_holds()
         assert als_h[A].decrement_holds() == als_o[A].decrement_holds()
     assert spf_view(als_h[A], "5") == spf_view(als_o[A], "5")
+
+
+def _star_dbs(center_links, extra_ring=True):
+    """hub "h" with `leaves` leaves, plus a stub node "s" attached to the hub;
+    leaves are chained into a ring so they also have lateral paths."""
+    adjs = {}
+
+    def link(a, b, m=1, k=0):
+        adjs.setdefault(a, []).append(create_adjacency(b, f"{a}>{b}:{k}", f"{b}>{a}:{k}",
+                                                       "fe80::1", "10.0.0.1", m, 0))
+        adjs.setdefault(b, []).append(create_adjacency(a, f"{b}>{a}:{k}", f"{a}>{b}:{k}",
+                                                       "fe80::2", "10.0.0.2", m, 0))
+
+    link("s", "h", 3)
+    for i in range(center_links):
+        link("h", f"l{i}", 1 + i % 3)
+    if extra_ring:
+        for i in range(center_links):
+            link(f"l{i}", f"l{(i + 1) % center_links}", 2)
+    return [create_adj_db(n, a, 0) for n, a in adjs.items()]
+
+
+def test_frontier_overflow_path(hip, oracle):
+    """1,500 nodes settle in one level from "s": more than the frontier buffer
+    holds, exercising the inline-settle path of phase A."""
+    dbs = _star_dbs(1500)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    for node in ("s", "l7"):
+        assert spf_view(als_h[A], node) == spf_view(als_o[A], node)
+
+
+def test_wide_mask_variant(hip, oracle):
+    """A source with 40 distinct neighbours needs two mask words (Wide)."""
+    dbs = _star_dbs(40)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    for node in ("h", "s", "l3"):
+        assert spf_view(als_h[A], node) == spf_view(als_o[A], node)
+
+
+def test_k32_variant_large_metrics(hip, oracle):
+    """Path metrics beyond 16 bits select the 64-bit packed state."""
+    dbs = random_topology(55, n=40, extra=40, max_metric=60000)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    for db in dbs[:10]:
+        assert spf_view(als_h[A], db.thisNodeName) == spf_view(als_o[A], db.thisNodeName)
