@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU-box profiling recipe (run through gpurun from the repo root):
+#   kernel trace + stats of the bench command, then one PMC pass per counter
+#   group (rocprofv3 does not split counters over passes; FETCH_SIZE and
+#   WRITE_SIZE cannot share a pass on gfx950). Output: gpurun_out/prof_<tag>/
+set -e
+TAG=${1:-run}
+shift || true
+ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline --no-route-db}
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
+  -- python3 "$REPO/bench.py" $ARGS > "$OUT/trace.log" 2>&1
+for CTR in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+  NAME=$(echo "$CTR" | cut -d' ' -f1)
+  timeout -k 10 -s KILL 120 rocprofv3 --pmc $CTR --output-format csv -d "$OUT/pmc_$NAME" -o run \
+    -- python3 "$REPO/bench.py" $ARGS > "$OUT/pmc_$NAME.log" 2>&1
+done
+echo "profile $TAG done"
