@@ -54,7 +54,7 @@ struct HopArgs {
   uint32_t* out_nh;
 };
 
-enum class SpfVariant { kUnsupported = 0, kBfs, kDist16, kDist32 };
+enum class SpfVariant { kUnsupported = 0, kBfs8, kBfs16, kBfs32, kDist16, kDist32 };
 
 struct SpfPlan {
   SpfVariant variant;

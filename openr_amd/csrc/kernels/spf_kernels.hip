@@ -12,16 +12,17 @@
 // 1. Distance rows (one workgroup per source row). The first-hop masks are
 //    NOT carried through the search, so the per-source LDS state is only what
 //    the distances need:
-//      BFS    (every live link has the same metric w0): visited + two frontier
-//             bitmaps, 3 bits per node; a node's distance (level * w0) is
-//             stored to its HBM row when it is expanded. No atomics return,
-//             no min-reduction: the next level is the next frontier.
+//      BFS    (every live link has the same metric w0): a u8/u16/u32 level
+//             per node plus two frontier bitmaps; the row (level * w0) is
+//             written to HBM once, coalesced, when the search ends. No
+//             atomics return, no min-reduction: the next level is the next
+//             frontier.
 //      Dist16 / Dist32 (general metrics): a u16 or u32 distance per node plus
 //             a pending-set bitmap; level-synchronous Dijkstra that expands
 //             every node at the minimum pending distance D at once (exact for
 //             positive integer metrics), the next D from a DPP wave minimum.
-//    Small state buys occupancy: BFS on N = 10,000 needs 3.75 KB, so waves,
-//    not LDS, bound the resident sources per CU.
+//    Small state buys occupancy: BFS on N = 10,000 needs 22.5 KB, so seven
+//    sources are resident per CU.
 // 2. First hops (one workgroup per (source, 1024-node tile)). With metrics
 //    >= 1 the closed form unrolls to: bit i (the source's i-th distinct
 //    neighbour n_i) is in NH(v) iff some up link s->n_i is tight
@@ -115,19 +116,29 @@ __device__ inline void load_recs(const SpfArgs& a, uint32_t v, uint2 (&rec)[K]) 
 // ---------------------------------------------------------------------------
 // phase 1a: BFS levels (uniform metric)
 // ---------------------------------------------------------------------------
-template <int K>
+// Per-source LDS state: the BFS level of every node (L = u8 / u16 / u32, all
+// ones = unvisited) plus two frontier bitmaps. Levels stay in LDS until the
+// search ends and the row is written to HBM once, coalesced (writing each
+// node's distance when it is reached scatters 4-byte stores over the row and
+// costs ~7x the row's bytes in partial-line writes).
+template <class L>
+struct Level {
+  static constexpr uint32_t kInfL = static_cast<L>(~static_cast<L>(0));
+};
+
+template <int K, class L>
 struct Bfs {
   const SpfArgs& a;
   const Src& s;
-  uint32_t* vis;
+  L* lvl;
   uint32_t* nxt;
+  L next_level;
 
-  __device__ bool edge(const uint2& r, uint32_t vw) const {
+  __device__ bool edge(const uint2& r, uint32_t lu) const {
+    if (lu != Level<L>::kInfL) return false;
     const uint32_t u = r.x & ORH_REC_COL_MASK;
-    const uint32_t bit = 1u << (u & 31u);
-    if (vw & bit) return false;
-    atomicOr(&vis[u >> 5], bit);
-    atomicOr(&nxt[u >> 5], bit);
+    lvl[u] = next_level;  // racing writers store the same value
+    atomicOr(&nxt[u >> 5], 1u << (u & 31u));
     return true;
   }
 
@@ -135,16 +146,16 @@ struct Bfs {
   __device__ bool expand(uint32_t v, const uint2 (&rec)[K]) const {
     if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) return false;  // no transit
     bool pushed = false;
-    uint32_t vw[K];
+    uint32_t lu[K];
     bool lv[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       lv[j] = live(a, s, rec[j], v * K + j);
-      vw[j] = lv[j] ? vis[(rec[j].x & ORH_REC_COL_MASK) >> 5] : kInf;
+      lu[j] = lv[j] ? static_cast<uint32_t>(lvl[rec[j].x & ORH_REC_COL_MASK]) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < K; ++j)
-      if (lv[j]) pushed |= edge(rec[j], vw[j]);
+      if (lv[j]) pushed |= edge(rec[j], lu[j]);
     const uint2 last = rec[K - 1];
     if (last.x & ORH_REC_CONT) {
       const uint32_t start = last.x & ORH_REC_COL_MASK;
@@ -154,50 +165,50 @@ struct Bfs {
 #pragma unroll
         for (int j = 0; j < kOvfBatch; ++j)
           if (j < static_cast<int>(cnt)) ov[j] = a.recs[start + base + j];
-        uint32_t ow[kOvfBatch];
+        uint32_t ol_[kOvfBatch];
         bool ol[kOvfBatch];
 #pragma unroll
         for (int j = 0; j < kOvfBatch; ++j) {
           ol[j] = j < static_cast<int>(cnt) && live(a, s, ov[j], start + base + j);
-          ow[j] = ol[j] ? vis[(ov[j].x & ORH_REC_COL_MASK) >> 5] : kInf;
+          ol_[j] = ol[j] ? static_cast<uint32_t>(lvl[ov[j].x & ORH_REC_COL_MASK]) : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kOvfBatch; ++j)
-          if (ol[j]) pushed |= edge(ov[j], ow[j]);
+          if (ol[j]) pushed |= edge(ov[j], ol_[j]);
       }
     }
     return pushed;
   }
 };
 
-template <int K>
+template <int K, class L>
 __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_any[2];
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
-  uint32_t* vis = lds;
-  uint32_t* f0 = lds + NB;
-  uint32_t* f1 = lds + 2 * NB;
+  L* lvl = reinterpret_cast<L*>(lds);
+  uint32_t* f0 = lds + a.lds_pend_off / 4;
+  uint32_t* f1 = f0 + NB;
   const Src s(a, row);
-  uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
 
-  for (uint32_t i = tid; i < 3 * NB; i += nthr) lds[i] = 0u;
+  const uint32_t lwords = a.lds_pend_off / 4;
+  for (uint32_t i = tid; i < lwords; i += nthr) lds[i] = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < 2 * NB; i += nthr) f0[i] = 0u;
   if (tid < 2) s_any[tid] = 0u;
   __syncthreads();
   if (tid == 0) {
-    vis[s.node >> 5] = 1u << (s.node & 31u);
+    lvl[s.node] = 0;
     f0[s.node >> 5] = 1u << (s.node & 31u);
   }
   __syncthreads();
 
   constexpr int kBatch = 16 / K;  // nodes whose records are in flight together
-  uint32_t D = 0;
-  for (uint32_t level = 0;; ++level, D += a.w0) {
+  for (uint32_t level = 0;; ++level) {
     const uint32_t par = level & 1u;
     uint32_t* cur = par ? f1 : f0;
-    const Bfs<K> b{a, s, vis, par ? f0 : f1};
+    const Bfs<K, L> b{a, s, lvl, par ? f0 : f1, static_cast<L>(level + 1)};
     if (tid == 0) s_any[par ^ 1u] = 0u;  // next level's flag, read one level ago
     bool pushed = false;
     // a thread owns frontier words w and w + nthr: their nodes' records go
@@ -220,7 +231,6 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
             todo &= todo - 1;
             vs[i] = bit < 32 ? w * 32 + bit : w2 * 32 + (bit - 32);
             load_recs<K>(a, vs[i], r[i]);
-            out[vs[i]] = D;
             cnt = i + 1;
           }
         }
@@ -231,12 +241,17 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
     }
     if (pushed) s_any[par] = 1u;
     __syncthreads();
-    // every level expands >= 1 node, so > N levels would be a bug; the bound
-    // guarantees every wave reaches the exit
+    // every level expands >= 1 node and levels stay below the type's
+    // all-ones (the planner picks L with N - 1 < kInfL), so the loop ends
+    // and every wave reaches the exit
     if (!s_any[par] || level >= N) break;
   }
-  for (uint32_t i = tid; i < N; i += nthr)
-    if (!((vis[i >> 5] >> (i & 31u)) & 1u)) out[i] = kInf;
+  uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+  const uint32_t w0 = a.w0;
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const uint32_t l = lvl[i];
+    __builtin_nontemporal_store(l == Level<L>::kInfL ? kInf : l * w0, &out[i]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -569,8 +584,13 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   if (ell_k != 4 && ell_k != 8) return p;
   const size_t nb = (n_nodes + 31) / 32;
   if (uniform && path_bound < 0xFFFFFFFFull) {
-    p.variant = SpfVariant::kBfs;
-    p.lds_bytes = 3 * nb * 4;
+    // levels are < N; the level type's all-ones marks "unvisited"
+    p.variant = n_nodes < 0xFFu ? SpfVariant::kBfs8
+        : n_nodes < 0xFFFFu     ? SpfVariant::kBfs16
+                                : SpfVariant::kBfs32;
+    const size_t lb = n_nodes < 0xFFu ? 1 : n_nodes < 0xFFFFu ? 2 : 4;
+    p.pend_off = align16(static_cast<size_t>(n_nodes) * lb);
+    p.lds_bytes = p.pend_off + 2 * nb * 4;
   } else if (path_bound < 0xFFFFull) {
     p.variant = SpfVariant::kDist16;
     p.pend_off = align16(static_cast<size_t>(n_nodes) * 2);
@@ -593,8 +613,12 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
 template <int K>
 static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   switch (plan.variant) {
-    case SpfVariant::kBfs:
-      return launch(spf_bfs_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kBfs8:
+      return launch(spf_bfs_kernel<K, uint8_t>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kBfs16:
+      return launch(spf_bfs_kernel<K, uint16_t>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kBfs32:
+      return launch(spf_bfs_kernel<K, uint32_t>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kDist16:
       return launch(spf_dist_kernel<uint16_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kDist32:
