@@ -19,6 +19,13 @@ namespace orh {
 struct SpfArgs {
   uint32_t n_nodes;
   uint32_t n_out;
+  uint32_t n_rows;
+  const uint32_t* dev_of;     // multi-source BFS: [N] host id -> Cuthill-McKee id
+  const uint32_t* host_of;    // multi-source BFS: [N] Cuthill-McKee id -> host id
+  const uint32_t* order;      // [n_rows] multi-source batch order of the rows
+  uint8_t* ms_lvl;            // multi-source BFS: node-major level bytes [batches][N][S]
+  uint32_t ms_pitch;          // multi-source BFS: frontier-array entries (> N)
+  uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
   const uint2* recs;       // ELL slots [N * K] then overflow records
   const uint32_t* link;    // per record: link id (ignore sets)
   const uint32_t* srcs;    // [n_rows]
@@ -29,6 +36,7 @@ struct SpfArgs {
   uint32_t lds_pend_off;
   uint32_t* out_dist;
   uint32_t* scratch;
+  uint64_t* diag;  // ORH_DIAG_STAMPS builds only
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -54,21 +62,27 @@ struct HopArgs {
   uint32_t* out_nh;
 };
 
-enum class SpfVariant { kUnsupported = 0, kBfs8, kBfs16, kBfs32, kDist16, kDist32 };
+enum class SpfVariant { kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32 };
 
 struct SpfPlan {
   SpfVariant variant;
   uint32_t ell_k;
   uint32_t block;
+  uint32_t mask_bytes;  // multi-source BFS: source-mask width (S = 8 * mask_bytes)
+  uint32_t ms_j;        // multi-source BFS: nodes owned per thread (template)
+  uint32_t ms_pitch;    // multi-source BFS: frontier-array entries
   size_t pend_off;
   size_t lds_bytes;
 };
 
 // uniform: every live link carries the same metric (BFS levels suffice);
 // path_bound: upper bound on any tentative distance
+// multi_source: the batch has no ignore sets, so rows may share one search
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
-                 size_t lds_limit);
+                 size_t lds_limit, bool multi_source);
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
+// bytes of node-major level scratch a multi-source plan needs for n_rows rows
+size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
 
 // LDS bytes the first-hop kernel needs for max_nbr distinct neighbours
 size_t hop_lds_bytes(uint32_t max_nbr);

@@ -255,6 +255,195 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// phase 1a': bit-parallel multi-source BFS (uniform metric, no ignore sets)
+// ---------------------------------------------------------------------------
+// One workgroup runs S = 32 (u32 masks) or 16 (u16) source rows at once, one
+// bit per source (multi-source BFS, Then et al., VLDB 2015), as a pull over
+// the nodes:
+//   nx(v) = (OR over live records v -> u of F(u)) & ~visited(v)
+// Thread t owns the device nodes t, t + B, ..., t + (J-1)B and keeps their
+// ELL columns (packed 16-bit; a dead or down slot points at an always-zero
+// LDS entry) and their visited masks in registers, so LDS holds only the two
+// frontier arrays (this level's and the next): 8 bytes per node at S = 32,
+// two workgroups per CU at N = 10,000. A node whose visited mask is full is
+// skipped (its stale frontier entry only repeats bits every neighbour
+// already holds). A node's bits reach its neighbours only if it is a
+// transit node (not overloaded; a source always transits its own bit at
+// level 0).
+//
+// Levels leave the CU as they are found, as bytes in a node-major scratch
+// lvl[(batch * N + v) * S + b] (one 32-byte block per node, written only by
+// the node's owner thread), and ms_finalize_kernel turns the scratch into
+// host-order u32 rows with coalesced stores. Levels >= 254 are written to the
+// output row directly (marker 254), so any depth is exact; 255 = unreached.
+constexpr uint32_t kLvlDirect = 254u, kLvlNone = 255u;
+
+template <class M>
+struct MsMask;
+template <>
+struct MsMask<uint32_t> {
+  static constexpr uint32_t kS = 32;
+};
+template <>
+struct MsMask<uint16_t> {
+  static constexpr uint32_t kS = 16;
+};
+
+__device__ inline uint32_t ms_col(const uint2& r, uint32_t zero) {
+  return (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) ? zero : (r.x & ORH_REC_COL_MASK);
+}
+
+template <int K, class M, int J>
+__global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr uint32_t kS = MsMask<M>::kS;
+  constexpr int KH = (K + 1) / 2;
+  const uint32_t N = a.n_nodes;
+  const uint32_t NZ = a.ms_zero;  // index of the always-zero frontier entry
+  const uint32_t tid = threadIdx.x, B = blockDim.x;
+  const uint32_t b0 = blockIdx.x * kS;
+  const uint32_t S = min(kS, a.n_rows - b0);
+  const uint32_t full = S == 32u ? 0xFFFFFFFFu : (1u << S) - 1u;
+  M* f_cur = reinterpret_cast<M*>(lds);
+  M* f_nxt = f_cur + a.ms_pitch;
+  uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;
+
+  for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
+  __syncthreads();
+  if (tid < S) {  // sources may repeat: OR the bits in
+    const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
+    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f_cur + src) & ~uintptr_t(3));
+    const uint32_t sh = (reinterpret_cast<uintptr_t>(f_cur + src) & 3u) * 8u;
+    atomicOr(w, (1u << tid) << sh);
+  }
+
+  uint32_t col[J][KH];
+  uint32_t vis[J];
+  uint32_t ovlm = 0u, ovfm = 0u;  // bit j: owned node j overloaded / has an overflow list
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = j * B + tid;
+#pragma unroll
+    for (int h = 0; h < KH; ++h) col[j][h] = NZ | (NZ << 16);
+    vis[j] = full;
+    if (v < N) {
+      const uint2* slots = a.recs + static_cast<size_t>(v) * K;
+      uint2 r[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[k] = slots[k];
+#pragma unroll
+      for (int h = 0; h < KH; ++h)
+        col[j][h] = ms_col(r[2 * h], NZ) | ((2 * h + 1 < K ? ms_col(r[2 * h + 1], NZ) : NZ) << 16);
+      if (r[0].x & ORH_REC_ROW_OVL) ovlm |= 1u << j;
+      if (r[K - 1].x & ORH_REC_CONT) ovfm |= 1u << j;
+      // every byte of the node's block starts as "unreached"
+      uint4* blk = reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS);
+#pragma unroll
+      for (int q = 0; q < static_cast<int>(kS / 16); ++q) blk[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+  }
+  __syncthreads();
+  // level 0: the sources
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = j * B + tid;
+    if (v < N) {
+      const uint32_t f = f_cur[v];
+      vis[j] = f;
+      for (uint32_t q = f; q; q &= q - 1) lvl[static_cast<size_t>(v) * kS + __builtin_ctz(q)] = 0;
+    }
+  }
+
+  const uint32_t w0 = a.w0;
+  for (uint32_t level = 1;; ++level) {
+    int prog = 0;
+    // opaque per level: keeps the compiler from hoisting J * K unpacked LDS
+    // addresses and J per-node pointers out of the level loop (VGPR budget:
+    // two 512-thread workgroups per CU need <= 128)
+    uint32_t me = tid;
+    asm volatile("" : "+v"(me));
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      if (vis[j] == full) continue;  // also every v >= N
+#pragma unroll
+      for (int h = 0; h < KH; ++h) asm volatile("" : "+v"(col[j][h]));
+      const uint32_t v = j * B + me;
+      uint32_t acc = 0u;
+#pragma unroll
+      for (int h = 0; h < KH; ++h) {
+        acc |= f_cur[col[j][h] & 0xFFFFu];
+        if (2 * h + 1 < K) acc |= f_cur[col[j][h] >> 16];
+      }
+      if ((ovfm >> j) & 1u) {
+        const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
+        const uint2* ov = a.recs + (last.x & ORH_REC_COL_MASK);
+        for (uint32_t q = 0; q < last.y; ++q) {
+          const uint32_t r = ov[q].x;
+          if (!(r & ORH_REC_SKIP)) acc |= f_cur[r & ORH_REC_COL_MASK];
+        }
+      }
+      uint32_t nx = acc & ~vis[j];
+      if (nx) {
+        vis[j] |= nx;
+        prog = 1;
+        uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
+        if (level < kLvlDirect) {
+          for (uint32_t q = nx; q; q &= q - 1) lb[__builtin_ctz(q)] = static_cast<uint8_t>(level);
+        } else {
+          const uint32_t vh = a.host_of[v];
+          for (uint32_t q = nx; q; q &= q - 1) {
+            const uint32_t b = __builtin_ctz(q);
+            lb[b] = kLvlDirect;
+            dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
+          }
+        }
+        if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
+      }
+      f_nxt[v] = static_cast<M>(nx);
+    }
+    // every level that makes progress adds >= 1 visited bit: at most S * N levels
+    if (!__syncthreads_or(prog)) break;
+    M* t = f_cur;
+    f_cur = f_nxt;
+    f_nxt = t;
+  }
+}
+
+// node-major level bytes -> host-order u32 distance rows, one workgroup per
+// (batch, 256-node host tile); per source bit b the 256 stores of a row are
+// contiguous
+template <class M>
+__global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t tiles) {
+  constexpr uint32_t kS = MsMask<M>::kS;
+  const uint32_t N = a.n_nodes;
+  const uint32_t batch = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const uint32_t i = tile * 256 + threadIdx.x;
+  const uint32_t b0 = batch * kS;
+  const uint32_t S = min(kS, a.n_rows - b0);
+  if (i >= N) return;
+  const uint32_t v = a.dev_of[i];
+  const uint4* blk = reinterpret_cast<const uint4*>(a.ms_lvl + (static_cast<size_t>(batch) * N + v) * kS);
+  uint32_t w[kS / 4];
+#pragma unroll
+  for (int q = 0; q < static_cast<int>(kS / 16); ++q) {
+    const uint4 x = blk[q];
+    w[4 * q] = x.x;
+    w[4 * q + 1] = x.y;
+    w[4 * q + 2] = x.z;
+    w[4 * q + 3] = x.w;
+  }
+  const uint32_t w0 = a.w0;
+#pragma unroll
+  for (uint32_t b = 0; b < kS; ++b) {
+    if (b >= S) break;
+    const uint32_t l = (w[b / 4] >> ((b & 3u) * 8u)) & 0xFFu;
+    if (l == kLvlDirect) continue;
+    uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b]);
+    __builtin_nontemporal_store(l == kLvlNone ? kInf : l * w0, &out[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // phase 1b: level-synchronous Dijkstra on a u16 / u32 distance per node
 // ---------------------------------------------------------------------------
 template <class T>
@@ -578,11 +767,32 @@ static hipError_t launch(Kern kernel, const Args& a, uint32_t grid, uint32_t blo
 static size_t align16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
 
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
-                 size_t lds_limit) {
+                 size_t lds_limit, bool multi_source) {
   SpfPlan p{};
   p.ell_k = ell_k;
   if (ell_k != 4 && ell_k != 8) return p;
   const size_t nb = (n_nodes + 31) / 32;
+  if (multi_source && uniform && path_bound < 0xFFFFFFFFull) {
+    // a thread owns J <= 32 nodes (registers); the frontier arrays hold
+    // N + 1 entries (the last is the always-zero target of dead slots)
+    const uint32_t block = n_nodes <= 4096 ? 256 : 512;
+    const uint32_t j = (n_nodes + block - 1) / block;
+    const uint32_t pitch = (n_nodes + 1 + 15) & ~15u;
+    if (j <= 32) {
+      for (uint32_t mb = 4; mb >= 2; mb /= 2) {
+        const size_t bytes = 2 * static_cast<size_t>(mb) * pitch;
+        if (bytes <= lds_limit) {
+          p.variant = SpfVariant::kMsBfs;
+          p.mask_bytes = mb;
+          p.ms_j = (j + 3) & ~3u;
+          p.ms_pitch = pitch;
+          p.lds_bytes = bytes;
+          p.block = block;
+          return p;
+        }
+      }
+    }
+  }
   if (uniform && path_bound < 0xFFFFFFFFull) {
     // levels are < N; the level type's all-ones marks "unvisited"
     p.variant = n_nodes < 0xFFu ? SpfVariant::kBfs8
@@ -610,9 +820,52 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   return p;
 }
 
+template <int K, class M, int J>
+static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
+  constexpr uint32_t kS = MsMask<M>::kS;
+  const uint32_t batches = (n_rows + kS - 1) / kS;
+  hipError_t e = launch(spf_msbfs_kernel<K, M, J>, a, batches, plan.block, plan.lds_bytes, s);
+  if (e != hipSuccess) return e;
+  const uint32_t tiles = (a.n_nodes + 255) / 256;
+  hipLaunchKernelGGL(ms_finalize_kernel<M>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
+  return hipGetLastError();
+}
+
+template <int K, class M>
+static hipError_t launch_ms_m(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
+  switch (plan.ms_j) {
+    case 4: return launch_ms_j<K, M, 4>(plan, a, n_rows, s);
+    case 8: return launch_ms_j<K, M, 8>(plan, a, n_rows, s);
+    case 12: return launch_ms_j<K, M, 12>(plan, a, n_rows, s);
+    case 16: return launch_ms_j<K, M, 16>(plan, a, n_rows, s);
+    case 20: return launch_ms_j<K, M, 20>(plan, a, n_rows, s);
+    case 24: return launch_ms_j<K, M, 24>(plan, a, n_rows, s);
+    case 28: return launch_ms_j<K, M, 28>(plan, a, n_rows, s);
+    case 32: return launch_ms_j<K, M, 32>(plan, a, n_rows, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int K>
+static hipError_t launch_ms(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
+  switch (plan.mask_bytes) {
+    case 2: return launch_ms_m<K, uint16_t>(plan, a, n_rows, s);
+    case 4: return launch_ms_m<K, uint32_t>(plan, a, n_rows, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows) {
+  if (plan.variant != SpfVariant::kMsBfs) return 0;
+  const uint32_t s = plan.mask_bytes * 8;
+  return static_cast<size_t>((n_rows + s - 1) / s) * n_nodes * s;
+}
+
 template <int K>
 static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   switch (plan.variant) {
+    case SpfVariant::kMsBfs:
+      return launch_ms<K>(plan, a, n_rows, s);
     case SpfVariant::kBfs8:
       return launch(spf_bfs_kernel<K, uint8_t>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kBfs16:
@@ -631,6 +884,9 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
   a.lds_pend_off = static_cast<uint32_t>(plan.pend_off);
+  a.n_rows = n_rows;
+  a.ms_pitch = plan.ms_pitch;
+  a.ms_zero = a.n_nodes;
   return plan.ell_k == 8 ? launch_k<8>(plan, a, n_rows, s) : launch_k<4>(plan, a, n_rows, s);
 }
 

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -20,6 +21,7 @@ struct orh_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;  // around phase 1 | phase 2
   size_t lds_limit = 160 * 1024;
+  bool no_multi = false;  // ORH_NO_MULTI_SOURCE=1: per-source distance kernels only (A/B)
   std::string err;
   orh_counters counters{};
   // reusable device staging for request arrays, keyed by the request that
@@ -30,6 +32,9 @@ struct orh_ctx {
   // distance rows of neighbours that are not themselves requested sources
   uint32_t* d_scratch = nullptr;
   size_t d_scratch_cap = 0;  // in u32
+  // multi-source BFS: node-major level bytes
+  uint8_t* d_ms_lvl = nullptr;
+  size_t d_ms_lvl_cap = 0;
 };
 
 struct orh_graph {
@@ -53,6 +58,15 @@ struct orh_graph {
   uint32_t* d_link = nullptr;
   uint16_t* d_rank_out = nullptr;
   uint8_t* d_ovl = nullptr;
+  // multi-source BFS layout: the same ELL records in a Cuthill-McKee node
+  // order (neighbours get nearby ids, so a batch of consecutive sources is a
+  // compact region and a wave's 64 nodes progress together). Rebuilt lazily
+  // after attribute patches. Rows in HBM are always indexed by host id.
+  std::vector<uint32_t> ms_dev_of, ms_host_of;  // host -> CM id, CM id -> host
+  bool ms_dirty = true;
+  uint2* d_ms_recs = nullptr;
+  uint32_t* d_ms_dev_of = nullptr;
+  uint32_t* d_ms_host_of = nullptr;
   std::vector<int32_t> row_of;  // scratch for orh_spf_run (all -1 between calls)
 };
 
@@ -78,6 +92,13 @@ void free_graph_device(orh_graph* g) {
   (void)hipFree(g->d_link);
   (void)hipFree(g->d_rank_out);
   (void)hipFree(g->d_ovl);
+  (void)hipFree(g->d_ms_recs);
+  (void)hipFree(g->d_ms_dev_of);
+  (void)hipFree(g->d_ms_host_of);
+  g->d_ms_recs = nullptr;
+  g->d_ms_dev_of = nullptr;
+  g->d_ms_host_of = nullptr;
+  g->ms_dirty = true;
   g->d_recs = nullptr;
   g->d_link = nullptr;
   g->d_rank_out = nullptr;
@@ -115,8 +136,43 @@ uint32_t choose_ell_k(const orh_graph* g) {
   return deg[deg.size() * 9 / 10] > 4 ? 8 : 4;
 }
 
-uint2 device_record(const orh_graph* g, uint32_t v, uint32_t e) {
-  uint32_t x = g->col[e];
+// Cuthill-McKee: BFS from a low-degree node of each component, neighbours
+// visited in ascending degree (then host id) order
+void order_nodes(orh_graph* g) {
+  const uint32_t N = g->n_nodes;
+  auto& host_of = g->ms_host_of;
+  auto& dev_of = g->ms_dev_of;
+  host_of.clear();
+  host_of.reserve(N);
+  dev_of.assign(N, 0xFFFFFFFFu);
+  std::vector<uint32_t> deg(N), by_deg(N), nb;
+  for (uint32_t v = 0; v < N; ++v) {
+    deg[v] = g->dn_ptr[v + 1] - g->dn_ptr[v];
+    by_deg[v] = v;
+  }
+  std::stable_sort(by_deg.begin(), by_deg.end(),
+                   [&](uint32_t a, uint32_t b) { return deg[a] < deg[b]; });
+  for (uint32_t root : by_deg) {
+    if (dev_of[root] != 0xFFFFFFFFu) continue;
+    size_t head = host_of.size();
+    dev_of[root] = static_cast<uint32_t>(host_of.size());
+    host_of.push_back(root);
+    while (head < host_of.size()) {
+      const uint32_t v = host_of[head++];
+      nb.clear();
+      for (uint32_t k = g->dn_ptr[v]; k < g->dn_ptr[v + 1]; ++k)
+        if (dev_of[g->dn[k]] == 0xFFFFFFFFu) nb.push_back(g->dn[k]);
+      std::stable_sort(nb.begin(), nb.end(), [&](uint32_t a, uint32_t b) { return deg[a] < deg[b]; });
+      for (uint32_t u : nb) {
+        dev_of[u] = static_cast<uint32_t>(host_of.size());
+        host_of.push_back(u);
+      }
+    }
+  }
+}
+
+uint2 device_record(const orh_graph* g, uint32_t v, uint32_t e, const uint32_t* dev_of = nullptr) {
+  uint32_t x = dev_of ? dev_of[g->col[e]] : g->col[e];
   if (g->meta[e] & ORH_META_DOWN) x |= ORH_REC_SKIP;
   if (g->overloaded[v]) x |= ORH_REC_ROW_OVL;
   return make_uint2(x, g->w_out[e]);
@@ -153,11 +209,52 @@ void build_layout(orh_graph* g, std::vector<uint2>& recs, std::vector<uint32_t>&
   g->n_recs = static_cast<uint32_t>(recs.size());
 }
 
+// the ELL records again, rows and columns in Cuthill-McKee ids
+void build_ms_layout(const orh_graph* g, std::vector<uint2>& recs) {
+  const uint32_t K = g->ell_k, N = g->n_nodes;
+  recs.assign(g->n_recs, make_uint2(ORH_REC_SKIP, 1));
+  uint32_t ovf = N * K;
+  for (uint32_t dv = 0; dv < N; ++dv) {
+    const uint32_t v = g->ms_host_of[dv];
+    const uint32_t e0 = g->row_ptr[v], d = g->row_ptr[v + 1] - e0, base = dv * K;
+    const uint32_t inl = d <= K ? d : K - 1;
+    for (uint32_t j = 0; j < inl; ++j) recs[base + j] = device_record(g, v, e0 + j, g->ms_dev_of.data());
+    if (d > K) {
+      recs[base + K - 1] = make_uint2(ovf | ORH_REC_CONT, d - inl);
+      for (uint32_t j = inl; j < d; ++j) recs[ovf++] = device_record(g, v, e0 + j, g->ms_dev_of.data());
+    }
+  }
+}
+
+int sync_ms_layout(orh_graph* g) {
+  if (!g->ms_dirty) return ORH_OK;
+  orh_ctx* ctx = g->ctx;
+  std::vector<uint2> recs;
+  build_ms_layout(g, recs);
+  if (!g->d_ms_recs) {
+    const size_t nn = std::max<uint32_t>(g->n_nodes, 1);
+    if (hipMalloc(&g->d_ms_recs, recs.size() * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&g->d_ms_dev_of, nn * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&g->d_ms_host_of, nn * sizeof(uint32_t)) != hipSuccess)
+      return fail(ctx, ORH_E_NOMEM, "multi-source layout: device allocation failed");
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ms_dev_of, g->ms_dev_of.data(), g->n_nodes * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ms_host_of, g->ms_host_of.data(), g->n_nodes * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, ctx->stream));
+  }
+  ORH_HIP(ctx, hipMemcpyAsync(g->d_ms_recs, recs.data(), recs.size() * sizeof(uint2),
+                              hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // recs is a local
+  g->ms_dirty = false;
+  return ORH_OK;
+}
+
 int upload_record(orh_graph* g, uint32_t v, uint32_t e) {
   const uint2 r = device_record(g, v, e);
   ORH_HIP(g->ctx, hipMemcpyAsync(g->d_recs + g->pos[e], &r, sizeof(uint2),
                                  hipMemcpyHostToDevice, g->ctx->stream));
   ORH_HIP(g->ctx, hipStreamSynchronize(g->ctx->stream));  // r lives on this stack frame
+  g->ms_dirty = true;
   return ORH_OK;
 }
 
@@ -203,6 +300,16 @@ int ensure_scratch(orh_ctx* ctx, size_t words) {
   return ORH_OK;
 }
 
+int ensure_ms_lvl(orh_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->d_ms_lvl_cap) return ORH_OK;
+  hipFree(ctx->d_ms_lvl);
+  ctx->d_ms_lvl = nullptr;
+  ctx->d_ms_lvl_cap = 0;
+  ORH_HIP(ctx, hipMalloc(&ctx->d_ms_lvl, bytes));
+  ctx->d_ms_lvl_cap = bytes;
+  return ORH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -232,6 +339,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
     delete ctx;
     return ORH_E_DEVICE;
   }
+  if (const char* e = getenv("ORH_NO_MULTI_SOURCE")) ctx->no_multi = e[0] == '1';
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
@@ -246,6 +354,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   hipFree(ctx->d_req);
   hipFree(ctx->d_scratch);
+  hipFree(ctx->d_ms_lvl);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -353,6 +462,7 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
     if (n_distinct(g, v) > 0xFFFFu)
       return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_load: more than 65535 neighbours");
   g->ell_k = choose_ell_k(g);
+  order_nodes(g);
   std::vector<uint2> recs;
   std::vector<uint32_t> link;
   std::vector<uint16_t> rank;
@@ -372,8 +482,8 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   ORH_HIP(ctx, hipMemcpyAsync(g->d_rank_out, rank.data(), rank.size() * sizeof(uint16_t),
                               hipMemcpyHostToDevice, ctx->stream));
   if (g->n_nodes)
-    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl, g->overloaded.data(), g->n_nodes,
-                                hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl, g->overloaded.data(), g->n_nodes, hipMemcpyHostToDevice,
+                                ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
@@ -478,7 +588,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   const uint64_t bound = uniform ? static_cast<uint64_t>(N) * w0
       : req->use_link_metric ? g->sum_max_metric / 2 + g->max_metric
                              : static_cast<uint64_t>(g->n_links) + 1;
-  const orh::SpfPlan plan = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit);
+  const bool has_ign = req->h_ignore_ptr != nullptr;
+  const orh::SpfPlan plan =
+      orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, !has_ign && !ctx->no_multi);
   if (plan.variant == orh::SpfVariant::kUnsupported)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: graph exceeds the LDS-resident kernels (N=" +
                                             std::to_string(N) + ")");
@@ -486,7 +598,6 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: too many neighbours for the first-hop phase");
   hipSetDevice(ctx->device);
 
-  const bool has_ign = req->h_ignore_ptr != nullptr;
   const uint32_t n_ign = has_ign ? req->h_ignore_ptr[n_src] : 0u;
   // request key: graph generation + sources + ignore sets
   std::vector<uint32_t> key;
@@ -502,7 +613,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   }
   // staged layout: srcs[n_rows] | ign_ptr[n_rows+1] ign[..] | nbr_ptr[n_src+1] nbr_row[..]
   uint32_t n_rows = n_src;
-  size_t off_ign_ptr = 0, off_ign = 0, off_nbr_ptr = 0, off_nbr_row = 0;
+  size_t off_ign_ptr = 0, off_ign = 0, off_nbr_ptr = 0, off_nbr_row = 0, off_order = 0;
   if (key != ctx->req_key) {
     std::vector<uint32_t> srcs(req->h_srcs, req->h_srcs + n_src), nbr_ptr(n_src + 1, 0), nbr_row;
     std::vector<uint32_t> ign_ptr, ign;
@@ -557,6 +668,17 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     staging.insert(staging.end(), nbr_ptr.begin(), nbr_ptr.end());
     off_nbr_row = staging.size();
     staging.insert(staging.end(), nbr_row.begin(), nbr_row.end());
+    // multi-source batches: rows in ascending device id of their source, so
+    // a batch's sources are neighbours in the Cuthill-McKee order
+    off_order = staging.size();
+    {
+      std::vector<uint32_t> order(n_rows);
+      for (uint32_t r = 0; r < n_rows; ++r) order[r] = r;
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        return g->ms_dev_of[srcs[x]] < g->ms_dev_of[srcs[y]];
+      });
+      staging.insert(staging.end(), order.begin(), order.end());
+    }
     int rc = ensure_req(ctx, staging.size());
     if (rc) return rc;
     ORH_HIP(ctx, hipMemcpyAsync(ctx->d_req, staging.data(), staging.size() * 4,
@@ -566,16 +688,18 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     key.push_back(static_cast<uint32_t>(off_ign));
     key.push_back(static_cast<uint32_t>(off_nbr_ptr));
     key.push_back(static_cast<uint32_t>(off_nbr_row));
+    key.push_back(static_cast<uint32_t>(off_order));
     key.push_back(n_rows);
     ctx->req_key = std::move(key);
   }
   {
     const auto& k = ctx->req_key;
     const size_t t = k.size();
-    off_ign_ptr = k[t - 5];
-    off_ign = k[t - 4];
-    off_nbr_ptr = k[t - 3];
-    off_nbr_row = k[t - 2];
+    off_order = k[t - 2];
+    off_ign_ptr = k[t - 6];
+    off_ign = k[t - 5];
+    off_nbr_ptr = k[t - 4];
+    off_nbr_row = k[t - 3];
     n_rows = k[t - 1];
   }
   const size_t n_extra = n_rows - n_src;
@@ -589,6 +713,17 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.n_out = n_src;
   a.recs = g->d_recs;
   a.link = g->d_link;
+  if (plan.variant == orh::SpfVariant::kMsBfs) {
+    int rc = sync_ms_layout(g);
+    if (rc) return rc;
+    rc = ensure_ms_lvl(ctx, orh::ms_scratch_bytes(plan, N, n_rows));
+    if (rc) return rc;
+    a.recs = g->d_ms_recs;
+    a.dev_of = g->d_ms_dev_of;
+    a.host_of = g->d_ms_host_of;
+    a.ms_lvl = ctx->d_ms_lvl;
+  }
+  a.order = ctx->d_req + off_order;
   a.srcs = ctx->d_req + 1;
   a.ignore_ptr = has_ign ? ctx->d_req + off_ign_ptr : nullptr;
   a.ignore_links = has_ign ? ctx->d_req + off_ign : nullptr;
@@ -617,8 +752,25 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   h.out_nh = d_nh;
 
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+#ifdef ORH_DIAG_STAMPS
+  static uint64_t* d_diag = nullptr;
+  if (!d_diag) hipMalloc(&d_diag, 64);
+  hipMemsetAsync(d_diag, 0, 64, ctx->stream);
+  a.diag = d_diag;
+#endif
   hipError_t e = orh::launch_spf(plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "spf kernel launch");
+#ifdef ORH_DIAG_STAMPS
+  {
+    uint64_t h[8] = {};
+    hipMemcpyAsync(h, d_diag, 64, hipMemcpyDeviceToHost, ctx->stream);
+    hipStreamSynchronize(ctx->stream);
+    if (h[4])
+      fprintf(stderr, "diag: waves %llu avg cycles %.0f barrier %.0f pulls/wave %.1f levels %.1f\n",
+              (unsigned long long)h[4], double(h[0]) / h[4], double(h[1]) / h[4],
+              double(h[2]) / h[4], double(h[3]) / h[4]);
+  }
+#endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
   e = orh::launch_first_hop(h, max_nbr, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
