@@ -44,6 +44,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #include "spf_kernels.h"
 
@@ -261,21 +263,26 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
 // bit per source (multi-source BFS, Then et al., VLDB 2015), as a pull over
 // the nodes:
 //   nx(v) = (OR over live records v -> u of F(u)) & ~visited(v)
-// Thread t owns the device nodes t, t + B, ..., t + (J-1)B and keeps their
-// ELL columns (packed 16-bit; a dead or down slot points at an always-zero
-// LDS entry) and their visited masks in registers, so LDS holds only the two
-// frontier arrays (this level's and the next): 8 bytes per node at S = 32,
-// two workgroups per CU at N = 10,000. A node whose visited mask is full is
-// skipped (its stale frontier entry only repeats bits every neighbour
-// already holds). A node's bits reach its neighbours only if it is a
-// transit node (not overloaded; a source always transits its own bit at
-// level 0).
+// Thread t owns the Cuthill-McKee nodes t, t + B, ..., t + (J-1)B and keeps
+// their ELL columns (packed 16-bit; a dead or down slot points at an
+// always-zero LDS entry) and their visited masks in registers, so LDS holds
+// only the two frontier arrays (this level's and the next): 8 bytes per node
+// at S = 32, two workgroups per CU at N = 10,000. Groups of owned nodes whose
+// masks are full on every lane are skipped (a full node's stale frontier
+// entry only repeats bits every neighbour already holds). A node's bits
+// reach its neighbours only if it is a transit node (not overloaded; a
+// source always transits its own bit at level 0).
 //
 // Levels leave the CU as they are found, as bytes in a node-major scratch
-// lvl[(batch * N + v) * S + b] (one 32-byte block per node, written only by
-// the node's owner thread), and ms_finalize_kernel turns the scratch into
-// host-order u32 rows with coalesced stores. Levels >= 254 are written to the
-// output row directly (marker 254), so any depth is exact; 255 = unreached.
+// lvl[(batch * N + v) * S + b] (one S-byte block per node, written only by
+// the node's owner thread, so a store instruction's 64 lanes land in one
+// 2 KB span), and ms_finalize_kernel turns the scratch into host-order u32
+// rows with coalesced stores. (Measured alternatives: a row-major scratch
+// written per source bit issues ~5x more store instructions on the grid, where
+// a node's bits arrive a few at a time but different lanes get different bits;
+// dword stores for whole nibbles cost more than the stores they save.) Levels
+// >= 254 are written to the output row directly (marker 254), so any depth is
+// exact; 255 = unreached.
 constexpr uint32_t kLvlDirect = 254u, kLvlNone = 255u;
 
 template <class M>
@@ -293,6 +300,12 @@ __device__ inline uint32_t ms_col(const uint2& r, uint32_t zero) {
   return (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) ? zero : (r.x & ORH_REC_COL_MASK);
 }
 
+// workgroup barrier that orders LDS only (s_waitcnt lgkmcnt(0) + s_barrier);
+// the "memory" clobber keeps the compiler from moving LDS accesses across it
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int K, class M, int J>
 __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -304,17 +317,24 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
   const uint32_t b0 = blockIdx.x * kS;
   const uint32_t S = min(kS, a.n_rows - b0);
   const uint32_t full = S == 32u ? 0xFFFFFFFFu : (1u << S) - 1u;
+  __shared__ uint32_t s_prog[3];
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
-  uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;
+  uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
 
   for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
+  if (tid < 3) s_prog[tid] = 0u;
+  {  // every level byte starts as "unreached"
+    uint4* l4 = reinterpret_cast<uint4*>(lvl);
+    for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
   __syncthreads();
   if (tid < S) {  // sources may repeat: OR the bits in
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
     uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f_cur + src) & ~uintptr_t(3));
     const uint32_t sh = (reinterpret_cast<uintptr_t>(f_cur + src) & 3u) * 8u;
     atomicOr(w, (1u << tid) << sh);
+    lvl[static_cast<size_t>(src) * kS + tid] = 0;
   }
 
   uint32_t col[J][KH];
@@ -336,22 +356,13 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
         col[j][h] = ms_col(r[2 * h], NZ) | ((2 * h + 1 < K ? ms_col(r[2 * h + 1], NZ) : NZ) << 16);
       if (r[0].x & ORH_REC_ROW_OVL) ovlm |= 1u << j;
       if (r[K - 1].x & ORH_REC_CONT) ovfm |= 1u << j;
-      // every byte of the node's block starts as "unreached"
-      uint4* blk = reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS);
-#pragma unroll
-      for (int q = 0; q < static_cast<int>(kS / 16); ++q) blk[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
   }
   __syncthreads();
-  // level 0: the sources
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const uint32_t v = j * B + tid;
-    if (v < N) {
-      const uint32_t f = f_cur[v];
-      vis[j] = f;
-      for (uint32_t q = f; q; q &= q - 1) lvl[static_cast<size_t>(v) * kS + __builtin_ctz(q)] = 0;
-    }
+    if (v < N) vis[j] = f_cur[v];  // level 0: the sources
   }
 
   const uint32_t w0 = a.w0;
@@ -362,51 +373,80 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
     // two 512-thread workgroups per CU need <= 128)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
+    // groups of G owned nodes: a group is skipped when every lane holds all
+    // bits for all G nodes (wave-uniform branch); otherwise all G * K
+    // frontier reads go out back to back before any is consumed
+    constexpr int G = 4;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      if (vis[j] == full) continue;  // also every v >= N
+    for (int j0 = 0; j0 < J; j0 += G) {
+      bool open = false;
 #pragma unroll
-      for (int h = 0; h < KH; ++h) asm volatile("" : "+v"(col[j][h]));
-      const uint32_t v = j * B + me;
-      uint32_t acc = 0u;
+      for (int g = 0; g < G; ++g) open |= vis[j0 + g] != full;
+      if (!__builtin_amdgcn_ballot_w64(open)) continue;
+      uint32_t acc[G];
 #pragma unroll
-      for (int h = 0; h < KH; ++h) {
-        acc |= f_cur[col[j][h] & 0xFFFFu];
-        if (2 * h + 1 < K) acc |= f_cur[col[j][h] >> 16];
-      }
-      if ((ovfm >> j) & 1u) {
-        const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
-        const uint2* ov = a.recs + (last.x & ORH_REC_COL_MASK);
-        for (uint32_t q = 0; q < last.y; ++q) {
-          const uint32_t r = ov[q].x;
-          if (!(r & ORH_REC_SKIP)) acc |= f_cur[r & ORH_REC_COL_MASK];
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int h = 0; h < KH; ++h) asm volatile("" : "+v"(col[j0 + g][h]));
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        acc[g] = 0u;
+#pragma unroll
+        for (int h = 0; h < KH; ++h) {
+          acc[g] |= f_cur[col[j0 + g][h] & 0xFFFFu];
+          if (2 * h + 1 < K) acc[g] |= f_cur[col[j0 + g][h] >> 16];
         }
       }
-      uint32_t nx = acc & ~vis[j];
-      if (nx) {
-        vis[j] |= nx;
-        prog = 1;
-        uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
-        if (level < kLvlDirect) {
-          for (uint32_t q = nx; q; q &= q - 1) lb[__builtin_ctz(q)] = static_cast<uint8_t>(level);
-        } else {
-          const uint32_t vh = a.host_of[v];
-          for (uint32_t q = nx; q; q &= q - 1) {
-            const uint32_t b = __builtin_ctz(q);
-            lb[b] = kLvlDirect;
-            dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int j = j0 + g;
+        const uint32_t v = j * B + me;
+        uint32_t nx = 0u;
+        if (vis[j] != full) {  // also every v >= N
+          if ((ovfm >> j) & 1u) {
+            const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
+            const uint2* ov = a.recs + (last.x & ORH_REC_COL_MASK);
+            for (uint32_t q = 0; q < last.y; ++q) {
+              const uint32_t r = ov[q].x;
+              if (!(r & ORH_REC_SKIP)) acc[g] |= f_cur[r & ORH_REC_COL_MASK];
+            }
+          }
+          nx = acc[g] & ~vis[j];
+          vis[j] |= nx;
+        }
+        if (nx) {
+          prog = 1;
+          uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
+          if (level < kLvlDirect) {
+            for (uint32_t q = nx; q; q &= q - 1) lb[__builtin_ctz(q)] = static_cast<uint8_t>(level);
+          } else {
+            const uint32_t vh = a.host_of[v];
+            for (uint32_t q = nx; q; q &= q - 1) {
+              const uint32_t b = __builtin_ctz(q);
+              lb[b] = kLvlDirect;
+              dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
+            }
           }
         }
-        if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
+        if (vis[j] != full || nx) {
+          if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
+          f_nxt[v] = static_cast<M>(nx);
+        }
       }
-      f_nxt[v] = static_cast<M>(nx);
     }
-    // every level that makes progress adds >= 1 visited bit: at most S * N levels
-    if (!__syncthreads_or(prog)) break;
+    // every level that makes progress adds >= 1 visited bit: at most S * N
+    // levels. The barrier waits for LDS traffic only: the level bytes on
+    // their way to memory are read by the next kernel, and waiting for their
+    // write acknowledgements every level (what __syncthreads does) is wasted.
+    if (prog) s_prog[level % 3u] = 1u;
+    lds_barrier();
+    if (!s_prog[level % 3u]) break;
+    if (tid == 0) s_prog[(level + 2u) % 3u] = 0u;  // the previous level's flag, read before this barrier
     M* t = f_cur;
     f_cur = f_nxt;
     f_nxt = t;
   }
+
 }
 
 // node-major level bytes -> host-order u32 distance rows, one workgroup per
@@ -415,11 +455,14 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
 template <class M>
 __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t tiles) {
   constexpr uint32_t kS = MsMask<M>::kS;
+  __shared__ uint32_t* s_out[kS];
   const uint32_t N = a.n_nodes;
   const uint32_t batch = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const uint32_t i = tile * 256 + threadIdx.x;
   const uint32_t b0 = batch * kS;
   const uint32_t S = min(kS, a.n_rows - b0);
+  if (threadIdx.x < S) s_out[threadIdx.x] = dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + threadIdx.x]);
+  __syncthreads();
   if (i >= N) return;
   const uint32_t v = a.dev_of[i];
   const uint4* blk = reinterpret_cast<const uint4*>(a.ms_lvl + (static_cast<size_t>(batch) * N + v) * kS);
@@ -438,8 +481,7 @@ __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t ti
     if (b >= S) break;
     const uint32_t l = (w[b / 4] >> ((b & 3u) * 8u)) & 0xFFu;
     if (l == kLvlDirect) continue;
-    uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b]);
-    __builtin_nontemporal_store(l == kLvlNone ? kInf : l * w0, &out[i]);
+    __builtin_nontemporal_store(l == kLvlNone ? kInf : l * w0, &s_out[b][i]);
   }
 }
 
@@ -753,12 +795,26 @@ __global__ __launch_bounds__(kBlock) void route_select_kernel(RouteSelectArgs a)
 // ---------------------------------------------------------------------------
 // planning and launch
 // ---------------------------------------------------------------------------
+// dynamic-LDS opt-in, raised once per kernel to the largest size launched
+// (hipFuncSetAttribute is a runtime call worth avoiding on every sweep)
+template <typename Kern>
+static hipError_t lds_opt_in(Kern kernel, size_t lds) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> granted;
+  const void* f = reinterpret_cast<const void*>(kernel);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = granted.find(f);
+  if (it != granted.end() && lds <= it->second) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     static_cast<int>(lds));
+  if (e == hipSuccess) granted[f] = lds;
+  return e;
+}
+
 template <typename Kern, typename Args>
 static hipError_t launch(Kern kernel, const Args& a, uint32_t grid, uint32_t block, size_t lds,
                          hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     static_cast<int>(lds));
+  hipError_t e = lds_opt_in(kernel, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, a);
   return hipGetLastError();

@@ -754,21 +754,21 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
 #ifdef ORH_DIAG_STAMPS
   static uint64_t* d_diag = nullptr;
-  if (!d_diag) hipMalloc(&d_diag, 64);
-  hipMemsetAsync(d_diag, 0, 64, ctx->stream);
+  if (!d_diag) hipMalloc(&d_diag, 128);
+  hipMemsetAsync(d_diag, 0, 128, ctx->stream);
   a.diag = d_diag;
 #endif
   hipError_t e = orh::launch_spf(plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "spf kernel launch");
 #ifdef ORH_DIAG_STAMPS
   {
-    uint64_t h[8] = {};
-    hipMemcpyAsync(h, d_diag, 64, hipMemcpyDeviceToHost, ctx->stream);
+    uint64_t h[16] = {};
+    hipMemcpyAsync(h, d_diag, 128, hipMemcpyDeviceToHost, ctx->stream);
     hipStreamSynchronize(ctx->stream);
     if (h[4])
-      fprintf(stderr, "diag: waves %llu avg cycles %.0f barrier %.0f pulls/wave %.1f levels %.1f\n",
+      fprintf(stderr, "diag: waves %llu avg cycles %.0f barrier %.0f groups/wave %.1f levels %.1f max cycles %llu max levels %llu read %.0f proc %.0f\n",
               (unsigned long long)h[4], double(h[0]) / h[4], double(h[1]) / h[4],
-              double(h[2]) / h[4], double(h[3]) / h[4]);
+              double(h[2]) / h[4], double(h[3]) / h[4], (unsigned long long)h[5], (unsigned long long)h[6], double(h[7]) / h[4], double(h[8]) / h[4]);
   }
 #endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
