@@ -106,6 +106,18 @@ const char* orh_last_error(const orh_ctx* ctx);
 int orh_sync(orh_ctx* ctx);
 int orh_get_counters(const orh_ctx* ctx, orh_counters* out);
 int orh_reset_counters(orh_ctx* ctx);
+/* distance-kernel selection for later orh_spf_run calls on this context:
+ *   ORH_SPF_AUTO (default)  multi-source BFS when every live link has one
+ *                           metric and the batch has no ignore sets, else the
+ *                           LDS-resident per-source kernels, else the HBM
+ *                           frontier kernel (graphs beyond LDS, e.g. 50k nodes)
+ *   ORH_SPF_PER_SOURCE      per-source kernels only (LDS, HBM when too large)
+ *   ORH_SPF_GLOBAL          the HBM frontier kernel for every graph
+ * All modes produce identical results; the choice is performance only. */
+#define ORH_SPF_AUTO 0
+#define ORH_SPF_PER_SOURCE 1
+#define ORH_SPF_GLOBAL 2
+int orh_set_spf_mode(orh_ctx* ctx, int mode);
 /* device time (HIP events on the context stream) of the last orh_spf_run;
  * waits for that launch to finish */
 int orh_last_spf_ms(orh_ctx* ctx, double* ms_out);

@@ -461,4 +461,10 @@ PYBIND11_MODULE(_openr_host, m) {
     orh_device_count(&n);
     return n;
   });
+  // distance-kernel selection on the default context (ORH_SPF_AUTO /
+  // ORH_SPF_PER_SOURCE / ORH_SPF_GLOBAL); results are identical in every mode
+  m.def("set_spf_mode", [](int mode) {
+    if (orh_set_spf_mode(defaultContext(), mode) != ORH_OK)
+      throw std::invalid_argument("set_spf_mode: mode must be 0, 1 or 2");
+  });
 }

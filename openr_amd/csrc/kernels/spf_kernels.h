@@ -34,6 +34,7 @@ struct SpfArgs {
   int32_t use_link_metric;
   uint32_t w0;  // the uniform metric (BFS variant)
   uint32_t lds_pend_off;
+  uint32_t delta;  // HBM frontier kernel: near/far bucket width
   uint32_t* out_dist;
   uint32_t* scratch;
   uint64_t* diag;  // ORH_DIAG_STAMPS builds only
@@ -62,7 +63,12 @@ struct HopArgs {
   uint32_t* out_nh;
 };
 
-enum class SpfVariant { kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32 };
+enum class SpfVariant { kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal };
+
+// distance-kernel selection (orh_set_spf_mode): automatic (multi-source BFS
+// when eligible, else the LDS-resident per-source kernels, else the HBM
+// frontier kernel), per-source LDS kernels only, or the HBM kernel always
+enum class SpfMode { kAuto = 0, kPerSource = 1, kGlobal = 2 };
 
 struct SpfPlan {
   SpfVariant variant;
@@ -79,7 +85,7 @@ struct SpfPlan {
 // path_bound: upper bound on any tentative distance
 // multi_source: the batch has no ignore sets, so rows may share one search
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
-                 size_t lds_limit, bool multi_source);
+                 size_t lds_limit, bool multi_source, SpfMode mode);
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
 // bytes of node-major level scratch a multi-source plan needs for n_rows rows
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);

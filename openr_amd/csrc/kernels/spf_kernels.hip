@@ -682,6 +682,126 @@ __global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// phase 1c: frontier relaxation with the distances in HBM (graphs whose
+// per-source state does not fit LDS, e.g. the 50k-node WAN of C4)
+// ---------------------------------------------------------------------------
+// One workgroup per source row. The row itself (u32, in the output or the
+// scratch) holds the tentative distances; LDS holds only frontier bitmaps,
+// so any N up to ~400k fits. Label-correcting with a near/far split
+// (delta-stepping): a node lowered to d < T joins the next near frontier,
+// one lowered to d >= T the far set; when the near frontier empties, T
+// advances to (smallest far distance) + delta and the far nodes below it
+// become the frontier. Exact for positive integer metrics: every lowering is
+// re-expanded, so the fixpoint is the shortest-path distance. Relaxation is
+// an atomicMin on the row (L2 atomics); the row is L2-resident while its
+// source is searched.
+template <int K>
+__global__ __launch_bounds__(256) void spf_global_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_flag[3];
+  __shared__ uint32_t s_min;
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  uint32_t* near0 = lds;
+  uint32_t* near1 = lds + NB;
+  uint32_t* far = lds + 2 * NB;
+  const Src s(a, row);
+  uint32_t* dist = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+
+  for (uint32_t i = tid; i < 3 * NB; i += nthr) lds[i] = 0u;
+  for (uint32_t i = tid; i < N; i += nthr) dist[i] = kInf;
+  if (tid < 3) s_flag[tid] = 0u;
+  __syncthreads();  // also orders the row initialisation before the search
+  if (tid == 0) {
+    dist[s.node] = 0u;
+    near0[s.node >> 5] = 1u << (s.node & 31u);
+  }
+  __syncthreads();
+
+  const uint32_t delta = a.delta;
+  uint32_t T = delta;  // near/far threshold
+  uint32_t* cur = near0;
+  uint32_t* nxt = near1;
+  for (uint32_t it = 0;; ++it) {
+    // expand the near frontier
+    bool pushed_near = false;
+    for (uint32_t w = tid; w < NB; w += nthr) {
+      uint32_t bits = cur[w];
+      if (!bits) continue;
+      cur[w] = 0u;
+      while (bits) {
+        const uint32_t v = w * 32 + __builtin_ctz(bits);
+        bits &= bits - 1;
+        uint2 rec[K];
+        load_recs<K>(a, v, rec);
+        if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) continue;  // no transit
+        const uint32_t dv = __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        auto relax = [&](const uint2& r, uint32_t q) {
+          if (!live(a, s, r, q)) return;
+          const uint32_t u = r.x & ORH_REC_COL_MASK;
+          const uint32_t nd = dv + (a.use_link_metric ? r.y : 1u);
+          if (nd >= __hip_atomic_load(&dist[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+          const uint32_t old = atomicMin(&dist[u], nd);
+          if (nd >= old) return;
+          if (nd < T) {
+            atomicOr(&nxt[u >> 5], 1u << (u & 31u));
+            pushed_near = true;
+          } else {
+            atomicOr(&far[u >> 5], 1u << (u & 31u));
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < K; ++j) relax(rec[j], v * K + j);
+        const uint2 last = rec[K - 1];
+        if (last.x & ORH_REC_CONT) {
+          const uint32_t start = last.x & ORH_REC_COL_MASK;
+          for (uint32_t q = 0; q < last.y; ++q) relax(a.recs[start + q], start + q);
+        }
+      }
+    }
+    const uint32_t par = it % 3u;
+    if (pushed_near) s_flag[par] = 1u;
+    if (tid == 0) s_min = kInf;
+    __syncthreads();  // relaxations (global atomics) and bitmaps settled
+    const bool more_near = s_flag[par] != 0u;
+    if (tid == 0) s_flag[(par + 2u) % 3u] = 0u;  // the previous iteration's flag
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    if (more_near) continue;
+    // near frontier empty: smallest far distance, then promote far nodes below
+    // the new threshold
+    uint32_t local_min = kInf;
+    for (uint32_t w = tid; w < NB; w += nthr) {
+      for (uint32_t bits = far[w]; bits; bits &= bits - 1) {
+        const uint32_t v = w * 32 + __builtin_ctz(bits);
+        local_min = min(local_min, __hip_atomic_load(&dist[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+    }
+    const uint32_t wm = wave_min(local_min);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min, wm);
+    __syncthreads();
+    const uint32_t m = s_min;
+    if (m == kInf) break;  // far set empty: done (every wave sees the same value)
+    T = m + delta;
+    for (uint32_t w = tid; w < NB; w += nthr) {
+      uint32_t bits = far[w], promote = 0u;
+      for (uint32_t q = bits; q; q &= q - 1) {
+        const uint32_t b = __builtin_ctz(q);
+        if (__hip_atomic_load(&dist[w * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < T)
+          promote |= 1u << b;
+      }
+      if (promote) {
+        far[w] = bits & ~promote;
+        cur[w] |= promote;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // phase 2: first-hop masks
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
@@ -822,13 +942,26 @@ static hipError_t launch(Kern kernel, const Args& a, uint32_t grid, uint32_t blo
 
 static size_t align16(size_t x) { return (x + 15) & ~static_cast<size_t>(15); }
 
+static SpfPlan plan_global(SpfPlan p, uint32_t n_nodes, uint64_t path_bound, size_t lds_limit) {
+  const size_t bytes = 3 * static_cast<size_t>((n_nodes + 31) / 32) * 4;
+  if (path_bound >= 0xFFFFFFFFull || bytes > lds_limit) {
+    p.variant = SpfVariant::kUnsupported;
+    return p;
+  }
+  p.variant = SpfVariant::kGlobal;
+  p.lds_bytes = std::max<size_t>(bytes, 16);
+  p.block = 256;
+  return p;
+}
+
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
-                 size_t lds_limit, bool multi_source) {
+                 size_t lds_limit, bool multi_source, SpfMode mode) {
   SpfPlan p{};
   p.ell_k = ell_k;
   if (ell_k != 4 && ell_k != 8) return p;
+  if (mode == SpfMode::kGlobal) return plan_global(p, n_nodes, path_bound, lds_limit);
   const size_t nb = (n_nodes + 31) / 32;
-  if (multi_source && uniform && path_bound < 0xFFFFFFFFull) {
+  if (mode == SpfMode::kAuto && multi_source && uniform && path_bound < 0xFFFFFFFFull) {
     // a thread owns J <= 32 nodes (registers); the frontier arrays hold
     // N + 1 entries (the last is the always-zero target of dead slots)
     const uint32_t block = n_nodes <= 4096 ? 256 : 512;
@@ -872,7 +1005,7 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   // in one pass and leave room for 8 workgroups per CU
   const uint32_t half = static_cast<uint32_t>((nb + 1) / 2);
   p.block = std::min<uint32_t>(kMaxBlock, std::max<uint32_t>(256, (half + 63) / 64 * 64));
-  if (p.lds_bytes > lds_limit) p.variant = SpfVariant::kUnsupported;
+  if (p.lds_bytes > lds_limit) return plan_global(p, n_nodes, path_bound, lds_limit);
   return p;
 }
 
@@ -932,6 +1065,8 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
       return launch(spf_dist_kernel<uint16_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kDist32:
       return launch(spf_dist_kernel<uint32_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kGlobal:
+      return launch(spf_global_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     default:
       return hipErrorInvalidValue;
   }

@@ -21,7 +21,7 @@ struct orh_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;  // around phase 1 | phase 2
   size_t lds_limit = 160 * 1024;
-  bool no_multi = false;  // ORH_NO_MULTI_SOURCE=1: per-source distance kernels only (A/B)
+  orh::SpfMode spf_mode = orh::SpfMode::kAuto;  // orh_set_spf_mode
   std::string err;
   orh_counters counters{};
   // reusable device staging for request arrays, keyed by the request that
@@ -49,6 +49,7 @@ struct orh_graph {
   uint64_t sum_max_metric = 0;       // sum over up CSR entries of max(w_out, w_in)
   uint32_t max_metric = 0;
   uint32_t min_out = 0, max_out = 0;  // w_out range over up CSR entries
+  uint32_t mean_out = 1;               // mean w_out over up CSR entries
   // device layout: ELL slots v*K .. v*K+K-1, the last one a continuation
   // record into the overflow area when deg(v) > K
   uint32_t ell_k = 4;
@@ -277,6 +278,13 @@ void recompute_bounds(orh_graph* g) {
     g->max_out = std::max(g->max_out, g->w_out[e]);
   }
   if (g->max_out == 0) g->min_out = g->max_out = 1;  // no up link
+  uint64_t sum_out = 0, n_up = 0;
+  for (uint32_t e = 0; e < g->n_edges; ++e)
+    if (!(g->meta[e] & ORH_META_DOWN)) {
+      sum_out += g->w_out[e];
+      ++n_up;
+    }
+  g->mean_out = n_up ? static_cast<uint32_t>(sum_out / n_up) : 1u;
 }
 
 int ensure_req(orh_ctx* ctx, size_t words) {
@@ -339,12 +347,18 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
     delete ctx;
     return ORH_E_DEVICE;
   }
-  if (const char* e = getenv("ORH_NO_MULTI_SOURCE")) ctx->no_multi = e[0] == '1';
+  if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % 3);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
   }
   *out = ctx;
+  return ORH_OK;
+}
+
+int orh_set_spf_mode(orh_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return ORH_E_INVALID;
+  ctx->spf_mode = static_cast<orh::SpfMode>(mode);
   return ORH_OK;
 }
 
@@ -590,10 +604,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
                              : static_cast<uint64_t>(g->n_links) + 1;
   const bool has_ign = req->h_ignore_ptr != nullptr;
   const orh::SpfPlan plan =
-      orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, !has_ign && !ctx->no_multi);
+      orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, !has_ign, ctx->spf_mode);
   if (plan.variant == orh::SpfVariant::kUnsupported)
-    return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: graph exceeds the LDS-resident kernels (N=" +
-                                            std::to_string(N) + ")");
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: no distance kernel for this graph (N=" +
+                                            std::to_string(N) + ", path bound " +
+                                            std::to_string(bound) + ")");
   if (orh::hop_lds_bytes(max_nbr) > ctx->lds_limit)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: too many neighbours for the first-hop phase");
   hipSetDevice(ctx->device);
@@ -729,6 +744,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.ignore_links = has_ign ? ctx->d_req + off_ign : nullptr;
   a.use_link_metric = req->use_link_metric;
   a.w0 = w0;
+  // near/far width of the HBM kernel: the mean live metric (one BFS level
+  // when metrics are uniform)
+  a.delta = uniform ? w0 : std::max<uint32_t>(1u, g->mean_out);
   a.out_dist = d_dist;
   a.scratch = ctx->d_scratch;
 

@@ -1,0 +1,111 @@
+"""Every distance kernel against the oracle (``-m gpu``).
+
+libopenr_hip picks among three distance kernels (orh_set_spf_mode): the
+multi-source BFS (uniform metrics, no ignore sets), the LDS-resident
+per-source kernels, and the HBM frontier kernel (graphs beyond LDS, such as
+the 50k-node WAN of config C4). Results must be identical in every mode, so
+the parity cases run once per mode.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from openr_amd import host_module
+from openr_amd.facade import load_topology
+from openr_amd.topology import bench_grid, fabric, wan
+from openr_amd.types import K_TESTING_AREA
+
+from test_gpu_parity import random_topology, spf_view
+
+pytestmark = pytest.mark.gpu
+A = K_TESTING_AREA
+MODES = {"auto": 0, "per_source": 1, "global": 2}
+
+
+@pytest.fixture(params=list(MODES))
+def spf_mode(request, hip):
+    mod = host_module()
+    mod.set_spf_mode(MODES[request.param])
+    yield request.param
+    mod.set_spf_mode(0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_modes_random_graphs(hip, oracle, spf_mode, seed):
+    dbs = random_topology(500 + seed, n=40, extra=60)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    for db in dbs:
+        for metric in (True, False):
+            assert spf_view(als_h[A], db.thisNodeName, metric) == \
+                spf_view(als_o[A], db.thisNodeName, metric), (spf_mode, seed, db.thisNodeName)
+
+
+def test_modes_ignore_sets(hip, oracle, spf_mode):
+    dbs = random_topology(600, n=30, extra=40)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    rng = random.Random(3)
+    for db in dbs[:10]:
+        links = als_o[A].links_from_node(db.thisNodeName)
+        ignore = [tuple(l) for l in rng.sample(links, min(2, len(links)))]
+        assert als_h[A]._impl.run_spf_ignoring(db.thisNodeName, ignore) == \
+            als_o[A]._impl.run_spf_ignoring(db.thisNodeName, ignore)
+
+
+def test_modes_sweep_fabric(hip, oracle, spf_mode):
+    """Clos fabric (uniform metrics, high-degree spines with ELL overflow
+    records): an all-sources sweep in each mode, compared with the oracle on
+    every 7th source."""
+    adj_dbs, _ = fabric(600, bug_compatible=False)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    names = [db.thisNodeName for db in adj_dbs]
+    sweep = als_h[A]._impl.sweep(names, True)
+    sweep.run()
+    sweep.sync()
+    node_names = als_h[A]._impl.node_names()
+    for i in range(0, len(names), 7):
+        dist, _ = sweep.fetch(i)
+        ref = als_o[A].get_spf_result(names[i])
+        got = {node_names[v]: int(d) for v, d in enumerate(dist) if d != 0xFFFFFFFF}
+        assert got == {k: v.metric for k, v in ref.items()}, (spf_mode, names[i])
+        hv = {k: (v.metric, v.nextHops) for k, v in als_h[A].get_spf_result(names[i]).items()}
+        assert hv == {k: (v.metric, v.nextHops) for k, v in ref.items()}
+
+
+def test_modes_grid_sweep_properties(hip, spf_mode):
+    """40x40 grid, all sources: dist = Manhattan distance in every mode."""
+    n = 40
+    adj_dbs, _ = bench_grid(n)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    ls = als_h[A]
+    sweep = ls._impl.sweep([str(i) for i in range(n * n)], True)
+    sweep.run()
+    sweep.sync()
+    node_ids = {name: i for i, name in enumerate(ls._impl.node_names())}
+    ids = np.array([node_ids[str(v)] for v in range(n * n)])
+    rr, cc = np.divmod(np.arange(n * n), n)
+    for s in range(0, n * n, 13):
+        dist, nh = sweep.fetch(s)
+        assert np.array_equal(dist[ids], np.abs(rr - rr[s]) + np.abs(cc - cc[s])), (spf_mode, s)
+
+
+def test_wan_50k_hbm_kernel(hip, oracle):
+    """Config C4's 50k-node WAN (log-normal metrics): too large for the
+    LDS-resident kernels, so AUTO selects the HBM frontier kernel. Exact
+    comparison with the oracle on sampled sources, including first hops and
+    an ignore-set (what-if) SPF."""
+    adj_dbs, _ = wan(50000, seed=4)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    for src in ("w0", "w49999"):
+        h = als_h[A].get_spf_result(src)
+        o = als_o[A].get_spf_result(src)
+        assert {k: (v.metric, v.nextHops) for k, v in h.items()} == \
+            {k: (v.metric, v.nextHops) for k, v in o.items()}, src
+    links = als_o[A].links_from_node("w777")
+    ignore = [tuple(links[0])]
+    assert als_h[A]._impl.run_spf_ignoring("w777", ignore) == \
+        als_o[A]._impl.run_spf_ignoring("w777", ignore)
