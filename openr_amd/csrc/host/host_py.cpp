@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 
+#include "rib_policy.h"
 #include "spf_solver.h"
 
 namespace py = pybind11;
@@ -71,6 +72,8 @@ PrefixEntry entryFromWire(const py::tuple& t) {
     e.mv = std::move(mv);
   }
   if (!t[9].is_none()) e.data = str(t[9]);
+  if (t.size() > 10 && !t[10].is_none())
+    for (auto tag : t[10]) e.tags.insert(tag.cast<std::string>());
   return e;
 }
 
@@ -86,7 +89,8 @@ py::object entryToWire(const PrefixEntry& e) {
   return py::make_tuple(py::bytes(e.addr), e.len, e.type, e.forwardingType, e.forwardingAlgorithm,
                         py::cast(e.minNexthop), py::cast(e.prependLabel),
                         py::make_tuple(e.pathPreference, e.sourcePreference, e.distance), mv,
-                        e.data ? py::object(py::bytes(*e.data)) : py::none());
+                        e.data ? py::object(py::bytes(*e.data)) : py::none(),
+                        py::tuple(py::cast(std::vector<std::string>(e.tags.begin(), e.tags.end()))));
 }
 
 NextHopThrift nhFromWire(const py::tuple& t) {
@@ -130,6 +134,39 @@ py::tuple unicastToWire(const RibUnicastEntry& e) {
   return py::make_tuple(py::bytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
                         e.doNotInstall, e.bestArea,
                         e.bestPrefixEntry ? entryToWire(*e.bestPrefixEntry) : py::none());
+}
+
+RibUnicastEntry unicastFromWire(const py::tuple& t) {
+  RibUnicastEntry e;
+  e.prefix = {str(t[0]), t[1].cast<int32_t>()};
+  for (auto nh : t[2]) e.nexthops.insert(nhFromWire(nh.cast<py::tuple>()));
+  e.doNotInstall = t[3].cast<bool>();
+  e.bestArea = str(t[4]);
+  if (!t[5].is_none()) e.bestPrefixEntry = entryFromWire(t[5].cast<py::tuple>());
+  return e;
+}
+
+RibPolicyStatementSpec statementFromWire(const py::tuple& t) {
+  // (name, prefixes | None, tags | None, (default, {area: w}, {nbr: w}) | None)
+  RibPolicyStatementSpec s;
+  s.name = str(t[0]);
+  if (!t[1].is_none()) {
+    s.prefixes.emplace();
+    for (auto p : t[1]) {
+      auto pt = p.cast<py::tuple>();
+      s.prefixes->emplace_back(str(pt[0]), pt[1].cast<int32_t>());
+    }
+  }
+  if (!t[2].is_none()) s.tags = t[2].cast<std::vector<std::string>>();
+  if (!t[3].is_none()) {
+    auto w = t[3].cast<py::tuple>();
+    RibRouteActionWeight a;
+    a.defaultWeight = w[0].cast<int32_t>();
+    a.areaToWeight = w[1].cast<std::map<std::string, int32_t>>();
+    a.neighborToWeight = w[2].cast<std::map<std::string, int32_t>>();
+    s.setWeight = std::move(a);
+  }
+  return s;
 }
 
 py::tuple routeDbToWire(const DecisionRouteDb& db) {
@@ -185,8 +222,18 @@ struct AreaMap {
 // device-resident dist + first-hop rows for a fixed source list
 class SpfSweep {
  public:
-  SpfSweep(const LinkState& ls, const std::vector<std::string>& srcs, bool useLinkMetric)
+  SpfSweep(const LinkState& ls, const std::vector<std::string>& srcs, bool useLinkMetric,
+           const std::vector<std::vector<uint32_t>>* ignore = nullptr)
       : ls_(ls), useLinkMetric_(useLinkMetric) {
+    if (ignore) {
+      if (ignore->size() != srcs.size())
+        throw std::invalid_argument("SpfSweep: one ignore set per source");
+      ignPtr_.push_back(0);
+      for (const auto& set : *ignore) {
+        ignLinks_.insert(ignLinks_.end(), set.begin(), set.end());
+        ignPtr_.push_back(static_cast<uint32_t>(ignLinks_.size()));
+      }
+    }
     for (const auto& s : srcs) {
       auto id = ls.nodeId(s);
       if (!id) throw std::invalid_argument("SpfSweep: unknown source " + s);
@@ -214,6 +261,10 @@ class SpfSweep {
     req.h_srcs = srcs_.data();
     req.n_src = static_cast<uint32_t>(srcs_.size());
     req.use_link_metric = useLinkMetric_ ? 1 : 0;
+    if (!ignPtr_.empty()) {
+      req.h_ignore_ptr = ignPtr_.data();
+      req.h_ignore_links = ignLinks_.empty() ? ignPtr_.data() : ignLinks_.data();
+    }
     if (orh_spf_run(graph_, &req, words_, dDist_, dNh_) != ORH_OK)
       throw std::runtime_error(std::string("orh_spf_run: ") + orh_last_error(ctx_));
   }
@@ -248,11 +299,16 @@ class SpfSweep {
   const LinkState& ls_;
   bool useLinkMetric_;
   std::vector<uint32_t> srcs_;
+  std::vector<uint32_t> ignPtr_, ignLinks_;  // per-source ignore sets (CSR), empty for none
   orh_graph* graph_{nullptr};
   orh_ctx* ctx_{nullptr};
   uint32_t n_{0}, edges_{0}, words_{1};
   uint32_t* dDist_{nullptr};
   uint32_t* dNh_{nullptr};
+};
+
+struct RibStatementProbe {  // a lone RibPolicyStatement (RibPolicyTest.cpp statement tests)
+  RibPolicyStatement st;
 };
 
 }  // namespace
@@ -340,6 +396,42 @@ PYBIND11_MODULE(_openr_host, m) {
              for (uint32_t i = 0; i < s.numNodeIds(); ++i) v.push_back(s.nodeName(i));
              return v;
            })
+      .def("link_ids",
+           [](const LinkState& s) {  // every link id, with its (n1, if1, n2, if2)
+             py::list out;
+             for (uint32_t lid = 0; lid < s.numLinkSlots(); ++lid)
+               if (s.linkAlive(lid)) out.append(py::make_tuple(lid, linkDesc(s.link(lid))));
+             return out;
+           })
+      .def("what_if_sweep",  // runSpf(src, true, {links}) for many (src, ignore set) pairs
+           [](const LinkState& s, const std::vector<std::string>& srcs,
+              const std::vector<std::vector<uint32_t>>& ignore) {
+             return new SpfSweep(s, srcs, true, &ignore);
+           },
+           py::keep_alive<0, 1>())
+      .def("run_spf_batch",
+           [](const LinkState& s, const std::vector<std::string>& srcs,
+              const std::vector<std::vector<uint32_t>>& ignore) {
+             std::vector<uint32_t> ids;
+             for (const auto& n : srcs) {
+               auto id = s.nodeId(n);
+               if (!id) throw std::invalid_argument("run_spf_batch: unknown source " + n);
+               ids.push_back(*id);
+             }
+             py::list out;
+             for (const auto& row : s.runSpfBatch(ids, true, ignore.empty() ? nullptr : &ignore)) {
+               py::dict d;
+               for (auto item : rowToDict(s, row, false)) {
+                 auto v = item.second.cast<py::tuple>();
+                 d[item.first] = py::make_tuple(v[0], v[1]);
+               }
+               out.append(d);
+             }
+             return out;
+           })
+      .def("prefetch_spf_results", &LinkState::prefetchSpfResults, py::arg("nodes"),
+           py::arg("use_link_metric") = true)
+      .def("prefetch_kth_paths", &LinkState::prefetchKthPaths)
       .def("sweep", [](const LinkState& s, const std::vector<std::string>& srcs, bool useLinkMetric) {
              return new SpfSweep(s, srcs, useLinkMetric);
            },
@@ -455,6 +547,57 @@ PYBIND11_MODULE(_openr_host, m) {
              s.updateStaticMplsRoutes(u, del);
            })
       .def_property_readonly("route_build_runs", &SpfSolver::routeBuildRuns);
+
+  py::class_<RibPolicy>(m, "RibPolicy")
+      .def(py::init([](py::list statements, int64_t ttlSecs) {
+             std::vector<RibPolicyStatementSpec> specs;
+             for (auto st : statements) specs.push_back(statementFromWire(st.cast<py::tuple>()));
+             try {
+               return new RibPolicy(specs, ttlSecs);
+             } catch (const std::invalid_argument& e) {
+               throw py::value_error(e.what());
+             }
+           }),
+           py::arg("statements"), py::arg("ttl_secs"))
+      .def("is_active", &RibPolicy::isActive)
+      .def("ttl_ms", [](const RibPolicy& p) { return p.getTtlDuration().count(); })
+      .def("match", [](const RibPolicy& p, py::tuple r) { return p.match(unicastFromWire(r)); })
+      .def("apply_action",
+           [](RibPolicy& p, py::tuple r) {
+             RibUnicastEntry e = unicastFromWire(r);
+             const bool changed = p.applyAction(e);
+             return py::make_tuple(changed, unicastToWire(e));
+           })
+      .def("apply_policy",  // (updated prefixes, deleted prefixes, transformed unicast routes)
+           [](RibPolicy& p, py::list routes) {
+             std::unordered_map<Cidr, RibUnicastEntry, CidrHash> m;
+             for (auto r : routes) {
+               RibUnicastEntry e = unicastFromWire(r.cast<py::tuple>());
+               Cidr k = e.prefix;
+               m.emplace(std::move(k), std::move(e));
+             }
+             auto ch = p.applyPolicy(m);
+             py::list up, del, out;
+             for (const auto& c : ch.updatedRoutes) up.append(py::make_tuple(py::bytes(c.first), c.second));
+             for (const auto& c : ch.deletedRoutes) del.append(py::make_tuple(py::bytes(c.first), c.second));
+             for (const auto& [_, e] : m) out.append(unicastToWire(e));
+             return py::make_tuple(up, del, out);
+           })
+      .def_property_readonly("invalidated_routes", &RibPolicy::invalidatedRoutes);
+  py::class_<RibStatementProbe>(m, "RibPolicyStatement")
+      .def(py::init([](py::tuple st) {
+        try {
+          return new RibStatementProbe{RibPolicyStatement(statementFromWire(st))};
+        } catch (const std::invalid_argument& e) {
+          throw py::value_error(e.what());
+        }
+      }))
+      .def("match", [](const RibStatementProbe& s, py::tuple r) { return s.st.match(unicastFromWire(r)); })
+      .def("apply_action", [](const RibStatementProbe& s, py::tuple r) {
+        RibUnicastEntry e = unicastFromWire(r);
+        const bool changed = s.st.applyAction(e);
+        return py::make_tuple(changed, unicastToWire(e));
+      });
 
   m.def("device_count", [] {
     int n = 0;

@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <optional>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -82,12 +83,13 @@ struct PrefixEntry {
   int32_t pathPreference{0}, sourcePreference{0}, distance{0};
   std::optional<MetricVector> mv;
   std::optional<std::string> data;
+  std::set<std::string> tags;  // Types.thrift PrefixEntry.tags (RibPolicy tag matcher)
   bool operator==(const PrefixEntry& o) const {
     return addr == o.addr && len == o.len && type == o.type &&
         forwardingType == o.forwardingType && forwardingAlgorithm == o.forwardingAlgorithm &&
         minNexthop == o.minNexthop && prependLabel == o.prependLabel &&
         pathPreference == o.pathPreference && sourcePreference == o.sourcePreference &&
-        distance == o.distance && mv == o.mv && data == o.data;
+        distance == o.distance && mv == o.mv && data == o.data && tags == o.tags;
   }
 };
 

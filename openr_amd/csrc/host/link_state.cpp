@@ -1,6 +1,8 @@
 // Drop-in LinkState over libopenr_hip (see link_state.h).
 #include "link_state.h"
 
+#include <set>
+
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
@@ -162,6 +164,8 @@ std::optional<Link> LinkState::maybeMakeLink(const std::string& node, const Adja
   }
   return std::nullopt;
 }
+
+bool LinkState::linkAlive(uint32_t id) const { return id < links_.size() && links_[id].alive; }
 
 uint32_t LinkState::addLink(Link&& l) {  // LinkState.cpp:421-426
   uint32_t id;
@@ -469,6 +473,106 @@ SpfRow LinkState::spfOnDevice(uint32_t src, bool useLinkMetric,
   return row;
 }
 
+std::vector<SpfRow> LinkState::runSpfBatch(
+    const std::vector<uint32_t>& srcIds, bool useLinkMetric,
+    const std::vector<std::vector<uint32_t>>* ignoreSets) const {
+  std::vector<SpfRow> rows(srcIds.size());
+  if (srcIds.empty()) return rows;
+  flushMirror();
+  const uint32_t N = static_cast<uint32_t>(names_.size());
+  const uint32_t n = static_cast<uint32_t>(srcIds.size());
+  uint32_t words = 1;
+  check(ctx_, orh_spf_words(graph_, srcIds.data(), n, &words), "orh_spf_words");
+  std::vector<uint32_t> ptr, flat;
+  orh_spf_request req{};
+  req.h_srcs = srcIds.data();
+  req.n_src = n;
+  req.use_link_metric = useLinkMetric ? 1 : 0;
+  if (ignoreSets) {
+    if (ignoreSets->size() != srcIds.size())
+      throw std::invalid_argument("runSpfBatch: one ignore set per source");
+    ptr.push_back(0);
+    for (const auto& ign : *ignoreSets) {
+      flat.insert(flat.end(), ign.begin(), ign.end());
+      ptr.push_back(static_cast<uint32_t>(flat.size()));
+    }
+    req.h_ignore_ptr = ptr.data();
+    req.h_ignore_links = flat.empty() ? ptr.data() : flat.data();
+  }
+  std::vector<uint32_t> dist(static_cast<size_t>(n) * N), nh(static_cast<size_t>(n) * N * words);
+  check(ctx_, orh_spf_batch(graph_, &req, words, dist.data(), nh.data()), "orh_spf_batch");
+  for (uint32_t i = 0; i < n; ++i) {
+    SpfRow& row = rows[i];
+    const uint32_t src = srcIds[i];
+    row.srcName = names_[src];
+    row.src = src;
+    row.known = true;
+    row.useLinkMetric = useLinkMetric;
+    row.words = words;
+    row.dist.assign(dist.begin() + static_cast<size_t>(i) * N,
+                    dist.begin() + static_cast<size_t>(i + 1) * N);
+    row.nh.assign(nh.begin() + static_cast<size_t>(i) * N * words,
+                  nh.begin() + static_cast<size_t>(i + 1) * N * words);
+    uint32_t nn = 0;
+    check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &nn), "orh_graph_neighbors");
+    row.nbrs.resize(nn);
+    check(ctx_, orh_graph_neighbors(graph_, src, row.nbrs.data(), nn, &nn), "orh_graph_neighbors");
+  }
+  spfRuns_ += n;
+  return rows;
+}
+
+void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes,
+                                   bool useLinkMetric) const {
+  std::vector<uint32_t> ids;
+  std::unordered_set<uint32_t> seen;
+  for (const auto& nm : nodes) {
+    if (spfResults_.count({nm, useLinkMetric})) continue;
+    auto id = nodeId(nm);
+    if (id && seen.insert(*id).second) ids.push_back(*id);
+  }
+  auto rows = runSpfBatch(ids, useLinkMetric, nullptr);
+  for (auto& r : rows) {
+    std::string name = r.srcName;
+    spfResults_.emplace(std::make_pair(std::move(name), useLinkMetric), std::move(r));
+  }
+}
+
+void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const {
+  // k = 1: traces over the memoized SPF of each source (batched)
+  std::vector<std::string> srcs;
+  for (const auto& pr : pairs) srcs.push_back(pr.first);
+  prefetchSpfResults(srcs, true);
+  for (const auto& [a, b] : pairs) getKthPaths(a, b, 1);
+  // k = 2: one fresh SPF per pair with its k = 1 links ignored, all in one launch
+  std::vector<uint32_t> ids;
+  std::vector<std::vector<uint32_t>> ign;
+  std::vector<const std::pair<std::string, std::string>*> todo;
+  std::set<std::pair<std::string, std::string>> queued;
+  for (const auto& pr : pairs) {
+    if (kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{2}))) continue;
+    if (!queued.insert(pr).second) continue;
+    std::unordered_set<uint32_t> s;
+    for (const auto& p : getKthPaths(pr.first, pr.second, 1))
+      for (uint32_t lid : p) s.insert(lid);
+    auto id = nodeId(pr.first);
+    if (s.empty() || !id) {
+      getKthPaths(pr.first, pr.second, 2);  // no re-run needed (memoized row)
+      continue;
+    }
+    ids.push_back(*id);
+    ign.emplace_back(s.begin(), s.end());
+    todo.push_back(&pr);
+  }
+  auto rows = runSpfBatch(ids, true, &ign);
+  for (size_t i = 0; i < todo.size(); ++i) {
+    const auto& [src, dst] = *todo[i];
+    std::unordered_set<uint32_t> ignore(ign[i].begin(), ign[i].end());
+    kthPaths_.emplace(std::make_tuple(src, dst, size_t{2}),
+                      traceKthPaths(src, dst, rows[i], &ignore));
+  }
+}
+
 const SpfRow& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) const {
   auto key = std::make_pair(node, useLinkMetric);
   auto it = spfResults_.find(key);
@@ -597,19 +701,27 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
     fresh = runSpf(src, true, ign);
     row = &fresh;
   }
+  paths = traceKthPaths(src, dst, *row, ignore.empty() ? nullptr : &ignore);
+  return kthPaths_.emplace(key, std::move(paths)).first->second;
+}
+
+std::vector<Path> LinkState::traceKthPaths(const std::string& src, const std::string& dst,
+                                           const SpfRow& row,
+                                           const std::unordered_set<uint32_t>* ignore) const {
+  // successive greedy traces sharing one visited-link set (LinkState.cpp:778-791)
+  std::vector<Path> paths;
   auto s = nodeId(src);
   auto d = nodeId(dst);
-  const bool hasDst = (src == dst) || (s && d && row->reachable(*d));
+  const bool hasDst = (src == dst) || (s && d && row.reachable(*d));
   if (hasDst && s && d) {
     std::unordered_set<uint32_t> visited;
-    const auto* ign = ignore.empty() ? nullptr : &ignore;
-    auto p = traceOnePath(*s, *d, *row, visited, ign);
+    auto p = traceOnePath(*s, *d, row, visited, ignore);
     while (p && !p->empty()) {
       paths.push_back(std::move(*p));
-      p = traceOnePath(*s, *d, *row, visited, ign);
+      p = traceOnePath(*s, *d, row, visited, ignore);
     }
   }
-  return kthPaths_.emplace(key, std::move(paths)).first->second;
+  return paths;
 }
 
 bool LinkState::pathAInPathB(const Path& a, const Path& b) {  // LinkState.h:395-410

@@ -146,6 +146,17 @@ class LinkState {
                 const std::vector<uint32_t>& ignoreLinks) const;
   const std::vector<Path>& getKthPaths(const std::string& src, const std::string& dst,
                                        size_t k) const;
+
+  // batched forms: one device launch for many SPFs (the reference runs them
+  // one by one). runSpfBatch: sources by node id, optional per-source ignore
+  // sets (what-if SPFs). prefetch*: fill the memos for many queries at once
+  // (getSpfResult for every node; getKthPaths for every (src, dst) pair with
+  // all k = 2 re-runs in one launch); later getSpfResult / getKthPaths calls
+  // are memo hits with identical results.
+  std::vector<SpfRow> runSpfBatch(const std::vector<uint32_t>& srcIds, bool useLinkMetric,
+                                  const std::vector<std::vector<uint32_t>>* ignoreSets) const;
+  void prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
+  void prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const;
   std::optional<Metric> getMetricFromAToB(const std::string& a, const std::string& b,
                                           bool useLinkMetric = true) const;
   Metric getMaxHopsToNode(const std::string& node) const;
@@ -162,6 +173,8 @@ class LinkState {
   uint32_t numNodeIds() const { return static_cast<uint32_t>(names_.size()); }
   std::vector<uint32_t> linksFromNode(const std::string& n) const;  // LinkSet order
   const Link& link(uint32_t id) const { return links_[id]; }
+  uint32_t numLinkSlots() const { return static_cast<uint32_t>(links_.size()); }
+  bool linkAlive(uint32_t id) const;
   size_t numLinks() const { return nLinks_; }
   size_t numNodes() const;
   const std::unordered_map<std::string, AdjacencyDatabase>& getAdjacencyDatabases() const {
@@ -192,6 +205,9 @@ class LinkState {
   void flushMirror() const;
   SpfRow spfOnDevice(uint32_t src, bool useLinkMetric,
                      const std::vector<uint32_t>* ignore) const;
+  std::vector<Path> traceKthPaths(const std::string& src, const std::string& dst,
+                                  const SpfRow& row,
+                                  const std::unordered_set<uint32_t>* ignore) const;
   std::optional<Path> traceOnePath(uint32_t src, uint32_t dst, const SpfRow& row,
                                    std::unordered_set<uint32_t>& visited,
                                    const std::unordered_set<uint32_t>* ignore) const;

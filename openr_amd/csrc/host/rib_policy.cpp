@@ -1,0 +1,96 @@
+// Drop-in RibPolicy (see rib_policy.h).
+#include "rib_policy.h"
+
+#include <stdexcept>
+
+namespace openr_amd {
+
+RibPolicyStatement::RibPolicyStatement(const RibPolicyStatementSpec& spec)
+    : name_(spec.name) {
+  // RibPolicy.cpp:20-36: an action and at least one matcher are mandatory
+  if (!spec.setWeight)
+    throw std::invalid_argument("Missing policy_statement.action.set_weight attribute");
+  if (!spec.prefixes && !spec.tags)
+    throw std::invalid_argument(
+        "Missing policy_statement.matcher.prefixes or policy_statement.matcher.tags attribute");
+  action_ = *spec.setWeight;
+  if (spec.prefixes) prefixSet_.insert(spec.prefixes->begin(), spec.prefixes->end());
+  if (spec.tags) tagSet_.insert(spec.tags->begin(), spec.tags->end());
+}
+
+bool RibPolicyStatement::match(const RibUnicastEntry& route) const {  // RibPolicy.cpp:73-105
+  if (tagSet_.empty() && prefixSet_.empty()) return false;
+  bool tagMatch = tagSet_.empty();
+  if (!tagMatch && route.bestPrefixEntry) {
+    for (const auto& tag : tagSet_) {
+      if (route.bestPrefixEntry->tags.count(tag)) {
+        tagMatch = true;
+        break;
+      }
+    }
+  }
+  const bool prefixMatch = prefixSet_.empty() || prefixSet_.count(route.prefix) > 0;
+  return tagMatch && prefixMatch;
+}
+
+bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidated) const {
+  if (!match(route)) return false;  // RibPolicy.cpp:108-161
+  NextHopSet out;
+  for (const auto& nh : route.nexthops) {
+    // precedence: neighbour weight, then area weight, then default weight
+    int32_t w = action_.defaultWeight;
+    if (nh.area) {
+      auto it = action_.areaToWeight.find(*nh.area);
+      if (it != action_.areaToWeight.end()) w = it->second;
+    }
+    if (nh.neighborNodeName) {
+      auto it = action_.neighborToWeight.find(*nh.neighborNodeName);
+      if (it != action_.neighborToWeight.end()) w = it->second;
+    }
+    if (w > 0) {
+      NextHopThrift n = nh;
+      n.weight = w;
+      out.insert(std::move(n));
+    }
+  }
+  if (out.empty()) {  // every nexthop dropped: keep the route as it was
+    if (invalidated) ++*invalidated;
+    return false;
+  }
+  route.nexthops = std::move(out);
+  return true;
+}
+
+RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& statements, int64_t ttlSecs)
+    : validUntil_(std::chrono::steady_clock::now() + std::chrono::seconds(ttlSecs)) {
+  if (statements.empty()) throw std::invalid_argument("Missing policy.statements attribute");
+  for (const auto& s : statements) statements_.emplace_back(s);
+}
+
+std::chrono::milliseconds RibPolicy::getTtlDuration() const {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(validUntil_ -
+                                                               std::chrono::steady_clock::now());
+}
+
+bool RibPolicy::match(const RibUnicastEntry& route) const {
+  for (const auto& s : statements_)
+    if (s.match(route)) return true;
+  return false;
+}
+
+bool RibPolicy::applyAction(RibUnicastEntry& route) {
+  for (const auto& s : statements_)
+    if (s.applyAction(route, &invalidated_)) return true;
+  return false;
+}
+
+RibPolicy::PolicyChange RibPolicy::applyPolicy(
+    std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes) {
+  PolicyChange change;  // RibPolicy.cpp:229-247
+  if (!isActive()) return change;
+  for (auto& [prefix, route] : routes)
+    if (applyAction(route)) change.updatedRoutes.push_back(route.prefix);
+  return change;
+}
+
+}  // namespace openr_amd

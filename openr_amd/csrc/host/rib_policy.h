@@ -1,0 +1,73 @@
+// Drop-in RibPolicy (openr/decision/RibPolicy.{h,cpp}): UCMP weights applied
+// to the unicast routes of a built DecisionRouteDb.
+//
+// A statement matches a route when every populated matcher matches (prefix
+// set: the route's prefix; tag set: any tag of the route's best prefix
+// entry) and at least one matcher is populated (RibPolicy.cpp:73-105). Its
+// set_weight action gives each nexthop the neighbour weight, else the area
+// weight, else the default weight; weight 0 drops the nexthop, and a route
+// whose nexthops would all be dropped is kept unchanged
+// (RibPolicy.cpp:108-161). A policy applies the first matching statement per
+// route and only while its TTL has not expired (RibPolicy.cpp:215-247).
+#pragma once
+
+#include <chrono>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "host_types.h"
+
+namespace openr_amd {
+
+struct RibRouteActionWeight {  // OpenrCtrl.thrift RibRouteActionWeight
+  int32_t defaultWeight{0};
+  std::map<std::string, int32_t> areaToWeight;
+  std::map<std::string, int32_t> neighborToWeight;
+};
+
+struct RibPolicyStatementSpec {  // thrift::RibPolicyStatement
+  std::string name;
+  std::optional<std::vector<Cidr>> prefixes;      // matcher.prefixes
+  std::optional<std::vector<std::string>> tags;   // matcher.tags
+  std::optional<RibRouteActionWeight> setWeight;  // action.set_weight
+};
+
+class RibPolicyStatement {
+ public:
+  explicit RibPolicyStatement(const RibPolicyStatementSpec& spec);  // throws std::invalid_argument
+  bool match(const RibUnicastEntry& route) const;
+  bool applyAction(RibUnicastEntry& route, uint64_t* invalidated = nullptr) const;
+  const std::string& name() const { return name_; }
+
+ private:
+  std::string name_;
+  RibRouteActionWeight action_;
+  std::set<Cidr> prefixSet_;
+  std::set<std::string> tagSet_;
+};
+
+class RibPolicy {
+ public:
+  struct PolicyChange {
+    std::vector<Cidr> updatedRoutes;
+    std::vector<Cidr> deletedRoutes;
+  };
+
+  RibPolicy(const std::vector<RibPolicyStatementSpec>& statements, int64_t ttlSecs);
+  bool isActive() const { return getTtlDuration().count() > 0; }
+  std::chrono::milliseconds getTtlDuration() const;
+  bool match(const RibUnicastEntry& route) const;
+  bool applyAction(RibUnicastEntry& route);
+  PolicyChange applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes);
+  // decision.rib_policy.invalidated_routes (RibPolicy.cpp:150-153)
+  uint64_t invalidatedRoutes() const { return invalidated_; }
+
+ private:
+  std::chrono::steady_clock::time_point validUntil_;
+  std::vector<RibPolicyStatement> statements_;
+  uint64_t invalidated_{0};
+};
+
+}  // namespace openr_amd

@@ -222,6 +222,15 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
     fa = std::min(fa, e.forwardingAlgorithm);
     if (ft == kFwdIp && fa == kAlgoSpEcmp) break;
   }
+  if (kspPlan_) {
+    // planning pass of buildRouteDb: record the (me, node) pairs whose
+    // k = 2 paths selectBestPathsKsp2 will ask for, build nothing
+    if (fa == kAlgoKsp2EdEcmp && ft == kFwdSrMpls)
+      for (const auto& [area, ls] : als)
+        for (const auto& [node, bestArea] : best.allNodeAreas)
+          if (area == bestArea) (*kspPlan_)[&ls].emplace_back(me, node);
+    return std::nullopt;
+  }
   if (fa == kAlgoSpEcmp) return selectBestPathsSpf(me, prefix, best, entries, hasBgp, ft, als);
   if (fa == kAlgoKsp2EdEcmp) return selectBestPathsKsp2(me, prefix, best, entries, hasBgp, ft, als);
   return std::nullopt;
@@ -561,6 +570,26 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   for (const auto& [_, ls] : als) exists |= ls.hasNode(me);
   if (!exists) return std::nullopt;
   ++routeBuildRuns_;
+
+  // KSP2 prefixes need one fresh SPF per best node (getKthPaths k = 2): plan
+  // them first and run them as one device batch (the memo then serves the
+  // route build with the same paths and the same spf_runs count)
+  {
+    std::unordered_map<const LinkState*, std::vector<std::pair<std::string, std::string>>> plan;
+    kspPlan_ = &plan;
+    try {
+      for (const auto& [prefix, entries] : ps.prefixes()) {
+        bool ksp = false;
+        for (const auto& [na, e] : entries) ksp |= e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+        if (ksp) createRouteForPrefix(me, als, ps, prefix);
+      }
+    } catch (...) {
+      kspPlan_ = nullptr;
+      throw;
+    }
+    kspPlan_ = nullptr;
+    for (auto& [ls, pairs] : plan) ls->prefetchKthPaths(pairs);
+  }
 
   DecisionRouteDb db;
   db.unicastRoutes.reserve(ps.prefixes().size());

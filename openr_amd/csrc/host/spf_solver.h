@@ -108,6 +108,9 @@ class SpfSolver {
   std::string myNodeName_;
   bool enableV4_, enableOrderedFib_, bgpDryRun_, enableBestRouteSelection_;
   uint64_t routeBuildRuns_{0};
+  // set during buildRouteDb's KSP2 planning pass (see buildRouteDb)
+  std::unordered_map<const LinkState*, std::vector<std::pair<std::string, std::string>>>* kspPlan_{
+      nullptr};
 };
 
 }  // namespace openr_amd

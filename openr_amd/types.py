@@ -173,6 +173,7 @@ class PrefixEntry:
     minNexthop: Optional[int] = None
     prependLabel: Optional[int] = None
     metrics: PrefixMetrics = field(default_factory=PrefixMetrics)
+    tags: tuple = ()  # Types.thrift PrefixEntry.tags (RibPolicy tag matcher)
 
     def to_wire(self):
         m = self.metrics
@@ -181,15 +182,16 @@ class PrefixEntry:
                 int(self.forwardingAlgorithm), self.minNexthop,
                 self.prependLabel,
                 (int(m.path_preference), int(m.source_preference), int(m.distance)),
-                self.mv, self.data)
+                self.mv, self.data, tuple(sorted(self.tags)))
 
 
 def prefix_entry_from_wire(w) -> PrefixEntry:
-    addr, plen, typ, ft, fa, mn, pl, (pp, sp, d), mv, data = w
+    addr, plen, typ, ft, fa, mn, pl, (pp, sp, d), mv, data = w[:10]
+    tags = tuple(w[10]) if len(w) > 10 and w[10] is not None else ()
     if mv is not None:
         mv = (mv[0], tuple((t, p, o, tb, tuple(m)) for t, p, o, tb, m in mv[1]))
     return PrefixEntry(IpPrefix(BinaryAddress(addr), plen), typ, data, ft, fa,
-                       mv, mn, pl, PrefixMetrics(1, pp, sp, d))
+                       mv, mn, pl, PrefixMetrics(1, pp, sp, d), tags)
 
 
 def nexthop_from_wire(w) -> NextHopThrift:

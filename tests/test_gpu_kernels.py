@@ -109,3 +109,58 @@ def test_wan_50k_hbm_kernel(hip, oracle):
     ignore = [tuple(links[0])]
     assert als_h[A]._impl.run_spf_ignoring("w777", ignore) == \
         als_o[A]._impl.run_spf_ignoring("w777", ignore)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_what_if_batch(hip, oracle, seed):
+    """Batched single-link what-if SPFs (runSpf(src, true, {link}) for many
+    (src, link) pairs in one launch) against the oracle, pair by pair."""
+    dbs = random_topology(700 + seed, n=30, extra=40)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    links = als_h[A]._impl.link_ids()
+    rng = random.Random(seed)
+    srcs, ign, descs = [], [], []
+    for _ in range(40):
+        lid, desc = links[rng.randrange(len(links))]
+        srcs.append(dbs[rng.randrange(len(dbs))].thisNodeName)
+        ign.append([lid])
+        descs.append(desc)
+    got = als_h[A]._impl.run_spf_batch(srcs, ign)
+    for src, desc, g in zip(srcs, descs, got):
+        assert g == als_o[A]._impl.run_spf_ignoring(src, [(desc[0], desc[1], desc[2])]), (src, desc)
+
+
+def test_what_if_sweep_device_rows(hip, oracle):
+    """Device-resident what-if sweep (the bench path) row by row."""
+    dbs = random_topology(800, n=30, extra=40)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    links = als_h[A]._impl.link_ids()
+    names = als_h[A]._impl.node_names()
+    srcs = [dbs[i % len(dbs)].thisNodeName for i in range(24)]
+    picks = [links[(7 * i) % len(links)] for i in range(24)]
+    sweep = als_h[A]._impl.what_if_sweep(srcs, [[lid] for lid, _ in picks])
+    sweep.run()
+    sweep.sync()
+    for i, (src, (lid, desc)) in enumerate(zip(srcs, picks)):
+        dist, _ = sweep.fetch(i)
+        ref = als_o[A]._impl.run_spf_ignoring(src, [(desc[0], desc[1], desc[2])])
+        got = {names[v]: int(d) for v, d in enumerate(dist) if d != 0xFFFFFFFF}
+        assert got == {k: v[0] for k, v in ref.items()}, (src, desc)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_ksp2_batch_prefetch(hip, oracle, seed):
+    """All k = 2 re-runs of many (src, dst) pairs in one launch: the memo then
+    returns exactly the oracle's paths."""
+    dbs = random_topology(900 + seed, n=16, extra=24, max_metric=3, parallel=0.4, overload=0.0,
+                          link_overload=0.0)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    pairs = [(s, d) for s in names[:4] for d in names]
+    als_h[A]._impl.prefetch_kth_paths(pairs)
+    for s, d in pairs:
+        for k in (1, 2):
+            assert als_h[A].get_kth_paths(s, d, k) == als_o[A].get_kth_paths(s, d, k), (s, d, k)
