@@ -1,7 +1,12 @@
 // Drop-in SpfSolver / PrefixState over device SPF rows (see spf_solver.h).
 #include "spf_solver.h"
 
+#include "parallel.h"
+
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <list>
 #include <stdexcept>
@@ -10,6 +15,23 @@
 namespace openr_amd {
 
 namespace {
+
+// prefixes / adjacency databases below which the route build stays on the
+// calling thread (the pool's hand-off costs more than it saves)
+constexpr size_t kParallelMin = 2048;
+
+// ORH_ROUTE_PROF=1: phase times of buildRouteDb on stderr
+struct RouteProf {
+  bool on = std::getenv("ORH_ROUTE_PROF") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "route-prof %-16s %8.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
 
 MplsAction mpls(int32_t code, std::optional<int32_t> swap = std::nullopt,
                 std::optional<std::vector<int32_t>> push = std::nullopt) {
@@ -574,6 +596,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // KSP2 prefixes need one fresh SPF per best node (getKthPaths k = 2): plan
   // them first and run them as one device batch (the memo then serves the
   // route build with the same paths and the same spf_runs count)
+  RouteProf prof;
+  bool hasKsp = false;
   {
     std::unordered_map<const LinkState*, std::vector<std::pair<std::string, std::string>>> plan;
     kspPlan_ = &plan;
@@ -589,14 +613,42 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     }
     kspPlan_ = nullptr;
     for (auto& [ls, pairs] : plan) ls->prefetchKthPaths(pairs);
+    hasKsp = !plan.empty();
   }
 
+  // Every SPF row the prefixes read is memoized from here on (me's row per
+  // area; KSP2 paths were prefetched above), so the per-prefix work reads
+  // shared state only and runs on the host worker pool. KSP2 prefixes that
+  // found paths in other areas may still trace lazily, so their presence
+  // keeps the loop sequential.
+  prof.mark("ksp2 plan");
+  for (const auto& [_, ls] : als) ls.getSpfResult(me);
+  prof.mark("spf(me)");
   DecisionRouteDb db;
   db.unicastRoutes.reserve(ps.prefixes().size());
-  for (const auto& [prefix, _] : ps.prefixes()) {
-    if (auto r = createRouteForPrefix(me, als, ps, prefix)) {
-      if (!db.unicastRoutes.emplace(prefix, std::move(*r)).second)
-        throw std::logic_error("duplicate unicast route");
+  std::vector<const Cidr*> keys;
+  keys.reserve(ps.prefixes().size());
+  for (const auto& [prefix, _] : ps.prefixes()) keys.push_back(&prefix);
+  auto& pool = WorkerPool::instance();
+  if (!hasKsp && keys.size() >= kParallelMin && pool.size() > 1) {
+    std::vector<std::vector<RibUnicastEntry>> parts(pool.size());
+    pool.parallelFor(keys.size(), [&](size_t w, size_t b, size_t e) {
+      for (size_t i = b; i < e; ++i)
+        if (auto r = createRouteForPrefix(me, als, ps, *keys[i])) parts[w].push_back(std::move(*r));
+    });
+    prof.mark("unicast (pool)");
+    for (auto& part : parts)
+      for (auto& r : part) {
+        Cidr k = r.prefix;
+        if (!db.unicastRoutes.emplace(std::move(k), std::move(r)).second)
+          throw std::logic_error("duplicate unicast route");
+      }
+  } else {
+    for (const Cidr* prefix : keys) {
+      if (auto r = createRouteForPrefix(me, als, ps, *prefix)) {
+        if (!db.unicastRoutes.emplace(*prefix, std::move(*r)).second)
+          throw std::logic_error("duplicate unicast route");
+      }
     }
   }
   for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
@@ -607,14 +659,20 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     db.unicastRoutes.emplace(prefix, std::move(e));
   }
 
-  // node-label routes; duplicate labels resolve to the smaller node name
+  prof.mark("unicast merge");
+  // node-label routes; duplicate labels resolve to the smaller node name.
+  // The candidate entry of every adjacency database is computed on the
+  // worker pool, then the duplicate resolution walks them in the reference's
+  // iteration order (Decision.cpp:655-744).
   std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
   for (const auto& [area, ls] : als) {
-    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
+    std::vector<const AdjacencyDatabase*> dbs;
+    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
+    std::vector<std::optional<RibMplsEntry>> cand(dbs.size());
+    auto compute = [&, &area = area, &ls = ls](size_t i) {
+      const AdjacencyDatabase& adjDb = *dbs[i];
       const int32_t label = adjDb.nodeLabel;
-      if (label == 0 || !isMplsLabelValid(label)) continue;
-      auto it = labelToNode.find(label);
-      if (it != labelToNode.end() && it->second.first < adjDb.thisNodeName) continue;
+      if (label == 0 || !isMplsLabelValid(label)) return;
       RibMplsEntry entry{label, {}};
       if (adjDb.thisNodeName == me) {
         NextHopThrift nh;
@@ -625,19 +683,45 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       } else {
         const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};
         if (als.size() == 1 && ls.nodeId(me)) {
-          if (!fastSpEcmp(me, ls, area, dst, false, label, entry.nexthops)) continue;
+          if (!fastSpEcmp(me, ls, area, dst, false, label, entry.nexthops)) return;
         } else {
           auto nhm = getNextHopsWithMetric(me, dst, false, als);
-          if (nhm.second.empty()) continue;
+          if (nhm.second.empty()) return;
           entry.nexthops = getNextHopsThrift(me, dst, false, false, nhm.first, nhm.second, label,
                                              als, nullptr);
         }
       }
-      labelToNode.erase(label);
-      labelToNode.emplace(label, std::make_pair(adjDb.thisNodeName, std::move(entry)));
+      cand[i] = std::move(entry);
+    };
+    if (dbs.size() >= kParallelMin && pool.size() > 1) {
+      pool.parallelFor(dbs.size(), [&](size_t, size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) compute(i);
+      });
+    } else {
+      for (size_t i = 0; i < dbs.size(); ++i) compute(i);
     }
+    // winner per label: (node name, candidate index); entries move once
+    std::unordered_map<int32_t, std::pair<const std::string*, size_t>> win;
+    win.reserve(dbs.size());
+    for (size_t i = 0; i < dbs.size(); ++i) {
+      const AdjacencyDatabase& adjDb = *dbs[i];
+      const int32_t label = adjDb.nodeLabel;
+      if (label == 0 || !isMplsLabelValid(label)) continue;
+      auto lt = labelToNode.find(label);  // an earlier area's winner
+      const std::string* held = nullptr;
+      auto it = win.find(label);
+      if (it != win.end()) held = it->second.first;
+      else if (lt != labelToNode.end()) held = &lt->second.first;
+      if (held && *held < adjDb.thisNodeName) continue;
+      if (!cand[i]) continue;
+      if (lt != labelToNode.end()) labelToNode.erase(lt);
+      win[label] = {&adjDb.thisNodeName, i};
+    }
+    for (auto& [label, w] : win)
+      labelToNode.emplace(label, std::make_pair(*w.first, std::move(*cand[w.second])));
   }
   for (auto& [label, ne] : labelToNode) db.mplsRoutes.emplace(label, std::move(ne.second));
+  prof.mark("node labels");
 
   // adjacency-label routes for all my links, up or not (:749-775)
   for (const auto& [_, ls] : als) {
@@ -661,6 +745,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     if (!db.mplsRoutes.emplace(label, std::move(e)).second)
       throw std::logic_error("duplicate mpls route");
   }
+  prof.mark("adj + static mpls");
   return db;
 }
 

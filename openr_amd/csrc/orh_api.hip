@@ -35,6 +35,10 @@ struct orh_ctx {
   // multi-source BFS: node-major level bytes
   uint8_t* d_ms_lvl = nullptr;
   size_t d_ms_lvl_cap = 0;
+  // orh_spf_batch's device rows (reused: a hipMalloc/hipFree pair per call
+  // costs more than a single-source SPF)
+  uint32_t* d_batch = nullptr;
+  size_t d_batch_cap = 0;  // in u32
 };
 
 struct orh_graph {
@@ -369,6 +373,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_req);
   hipFree(ctx->d_scratch);
   hipFree(ctx->d_ms_lvl);
+  hipFree(ctx->d_batch);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -807,11 +812,16 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
   if (!h_dist || !h_nh) return fail(ctx, ORH_E_INVALID, "orh_spf_batch: null output");
   const size_t nd = static_cast<size_t>(req->n_src) * g->n_nodes;
   hipSetDevice(ctx->device);
-  uint32_t *d_dist = nullptr, *d_nh = nullptr;
-  if (hipMalloc(&d_dist, nd * 4) != hipSuccess || hipMalloc(&d_nh, nd * words * 4) != hipSuccess) {
-    hipFree(d_dist);
-    return fail(ctx, ORH_E_NOMEM, "orh_spf_batch: device allocation failed");
+  if (nd * (1 + words) > ctx->d_batch_cap) {
+    hipFree(ctx->d_batch);
+    ctx->d_batch = nullptr;
+    ctx->d_batch_cap = 0;
+    if (hipMalloc(&ctx->d_batch, nd * (1 + words) * 4) != hipSuccess)
+      return fail(ctx, ORH_E_NOMEM, "orh_spf_batch: device allocation failed");
+    ctx->d_batch_cap = nd * (1 + words);
   }
+  uint32_t* d_dist = ctx->d_batch;
+  uint32_t* d_nh = ctx->d_batch + nd;
   int rc = orh_spf_run(g, req, words, d_dist, d_nh);
   if (rc == ORH_OK) {
     hipError_t e = hipMemcpyAsync(h_dist, d_dist, nd * 4, hipMemcpyDeviceToHost, ctx->stream);
@@ -825,8 +835,6 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
       ctx->counters.total_kernel_ms += ms;
     }
   }
-  hipFree(d_dist);
-  hipFree(d_nh);
   return rc;
 }
 
