@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-route-db", action="store_true")
+    p.add_argument("--legs", default="c1,c3,c4",
+                   help="extra BASELINE configs reported under 'legs' (c1,c3,c4,c5; '' for none)")
     return p.parse_args()
 
 
@@ -196,6 +198,9 @@ def main():
 
     if world == 1 and not args.no_cpu_baseline:
         out.update(cpu_baseline(args, adj_dbs, prefixes, n, value))
+    if world == 1 and args.legs:
+        import bench_legs
+        out["legs"] = bench_legs.run(args.legs.split(","), hip, not args.no_cpu_baseline)
 
     print(json.dumps(out), flush=True)
     barrier()

@@ -1,0 +1,163 @@
+"""The other BASELINE.json configs, reported under bench.py's "legs" (N = 1).
+
+Each leg times the HIP product with its inputs resident on the device, and
+(unless --no-cpu-baseline) the CPU oracle, a restatement of the reference's
+LinkState / SpfSolver with its containers, on a bounded sample of the same
+work, stating the sample.
+
+  c1  createGrid(10): buildRouteDb("1") ms (reference BM_DecisionGrid shape)
+  c3  Clos (~2.5k nodes, full spine mesh): all-sources SPF sweep + 100k-prefix
+      buildRouteDb, default and best-route selection
+  c4  50k-node WAN: batched single-link what-if SPFs and KSP2 (src, dst) pairs
+  c5  4 areas + 1M prefixes, best-route selection, RibPolicy area weights
+"""
+import importlib
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "build"))
+    from openr_amd.facade import Backend
+    return Backend(importlib.import_module("openr_oracle"), "oracle")
+
+
+def _route_ms(solver, me, als, ps, reps):
+    return statistics.median(solver._impl.time_build_route_db(me, als._impl, ps._impl)[0] * 1e3
+                             for _ in range(reps))
+
+
+def leg_c1(hip, cpu):
+    from openr_amd.facade import load_topology
+    from openr_amd.topology import bench_grid
+    adj, pfx = bench_grid(10, 1)
+    als, ps = load_topology(hip, adj, pfx)
+    out = {"workload": "C1 createGrid(10) buildRouteDb('1')",
+           "build_route_db_ms": round(_route_ms(hip.spf_solver("1", True), "1", als, ps, 9), 4)}
+    if cpu:
+        o = _oracle()
+        als_o, ps_o = load_topology(o, adj, pfx)
+        out["cpu_build_route_db_ms"] = round(_route_ms(o.spf_solver("1", True), "1", als_o, ps_o, 9), 4)
+    return out
+
+
+def leg_c3(hip, cpu):
+    from openr_amd.facade import load_topology
+    from openr_amd.types import K_TESTING_AREA as A
+    from openr_amd.workloads import c3_fabric
+    adj, pfx = c3_fabric()
+    als, ps = load_topology(hip, adj, pfx)
+    names = [db.thisNodeName for db in adj]
+    sweep = als[A]._impl.sweep(names, True)
+    sweep.run()
+    sweep.sync()
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sweep.run()
+    sweep.sync()
+    dt = (time.perf_counter() - t0) / reps
+    me = "2-0-0"
+    out = {"workload": f"C3 Clos N={len(names)} E={sweep.edges}, {len(pfx)} prefix advertisements",
+           "sweep_spf_sources_per_s": round(len(names) / dt, 1),
+           "sweep_ms": round(dt * 1e3, 4),
+           "build_route_db_ms": round(_route_ms(hip.spf_solver(me, True), me, als, ps, 5), 3),
+           "build_route_db_best_route_ms": round(_route_ms(
+               hip.spf_solver(me, True, enable_best_route_selection=True), me, als, ps, 5), 3)}
+    if cpu:
+        o = _oracle()
+        als_o, ps_o = load_topology(o, adj, pfx)
+        sample = names[::max(1, len(names) // 64)]
+        sec, _ = als_o[A]._impl.time_spf_sources(sample, 1)
+        out["cpu_sweep_spf_sources_per_s"] = round(len(sample) / sec, 2)
+        out["cpu_sample"] = f"{len(sample)} runSpf calls, 1 thread"
+        out["cpu_build_route_db_ms"] = round(_route_ms(o.spf_solver(me, True), me, als_o, ps_o, 1), 2)
+    return out
+
+
+def leg_c4(hip, cpu, n_links=64, n_srcs=16, n_ksp=256):
+    from openr_amd.facade import load_topology
+    from openr_amd.types import K_TESTING_AREA as A
+    from openr_amd.workloads import c4_ksp2_pairs, c4_wan, c4_what_if_pairs
+    adj, _ = c4_wan()
+    als, _ = load_topology(hip, adj, [])
+    ls = als[A]._impl
+    names = ls.node_names()
+    lids = [lid for lid, _ in ls.link_ids()]
+    pairs = c4_what_if_pairs(lids, names, n_links, n_srcs)
+    sweep = ls.what_if_sweep([s for s, _ in pairs], [[l] for _, l in pairs])
+    sweep.run()
+    sweep.sync()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        sweep.run()
+    sweep.sync()
+    dt = (time.perf_counter() - t0) / 3
+    kp = c4_ksp2_pairs(names, n_ksp)
+    t0 = time.perf_counter()
+    ls.prefetch_kth_paths(kp)
+    kdt = time.perf_counter() - t0
+    out = {"workload": f"C4 WAN N={len(names)} E={sweep.edges}, log-normal metrics",
+           "what_if_spfs_per_s": round(len(pairs) / dt, 1),
+           "what_if_batch": f"{len(pairs)} runSpf(src, true, {{link}}) = {n_links} links x {n_srcs} sources",
+           "what_if_batch_ms": round(dt * 1e3, 3),
+           "ksp2_pairs_per_s": round(n_ksp / kdt, 1),
+           "ksp2_batch": f"{n_ksp} (src, dst) getKthPaths k=1,2 (host trace + 2 device batches)"}
+    if cpu:
+        o = _oracle()
+        als_o, _ = load_topology(o, adj, [])
+        t0 = time.perf_counter()
+        sec, _ = als_o[A]._impl.time_spf_sources([pairs[0][0]], 1)
+        out["cpu_spfs_per_s"] = round(1.0 / sec, 4)
+        out["cpu_sample"] = "1 runSpf on the 50k-node WAN, 1 thread (reference DijkstraQ re-heap)"
+    return out
+
+
+def leg_c5(hip, cpu):
+    from openr_amd.facade import load_topology
+    from openr_amd.rib_policy import RibPolicy, RibPolicyStatement, RibRouteActionWeight
+    from openr_amd.workloads import C5_AREAS, C5_TAG, c5_multi_area
+    areas, pfx = c5_multi_area()
+    adj = [db for a in C5_AREAS for db in areas[a]]
+    t0 = time.perf_counter()
+    als, ps = load_topology(hip, adj, pfx)
+    load_s = time.perf_counter() - t0
+    solver = hip.spf_solver("me", True, enable_best_route_selection=True)
+    out = {"workload": f"C5 4 areas x {len(areas['A'])} nodes, {len(pfx)} prefix advertisements",
+           "load_s": round(load_s, 2),
+           "build_route_db_ms": round(_route_ms(solver, "me", als, ps, 3), 2)}
+    policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
+        0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
+    build_s, policy_s, routes, updated = solver._impl.time_build_route_db_with_policy(
+        "me", als._impl, ps._impl, policy._impl)
+    out.update({"build_plus_policy_ms": round((build_s + policy_s) * 1e3, 2),
+                "rib_policy_ms": round(policy_s * 1e3, 2), "routes": routes,
+                "policy_updated_routes": updated})
+    if cpu:
+        o = _oracle()
+        als_o, ps_o = load_topology(o, adj, pfx)
+        so = o.spf_solver("me", True, enable_best_route_selection=True)
+        out["cpu_build_route_db_ms"] = round(_route_ms(so, "me", als_o, ps_o, 1), 1)
+    return out
+
+
+LEGS = {"c1": leg_c1, "c3": leg_c3, "c4": leg_c4, "c5": leg_c5}
+
+
+def run(names, hip, cpu):
+    out = {}
+    for n in names:
+        n = n.strip()
+        if not n:
+            continue
+        t0 = time.perf_counter()
+        try:
+            out[n] = LEGS[n](hip, cpu)
+        except Exception as e:  # a failed leg is reported, not hidden
+            out[n] = {"error": f"{type(e).__name__}: {e}"}
+        out[n]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+    return out

@@ -516,6 +516,19 @@ PYBIND11_MODULE(_openr_host, m) {
              const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
              return std::make_pair(sec, n);
            })
+      .def("time_build_route_db_with_policy",  // Decision::rebuildRoutes: build, then RibPolicy
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) {
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.buildRouteDb(me, als.m, ps);
+             const auto t1 = std::chrono::steady_clock::now();
+             size_t updated = 0;
+             if (db) updated = policy.applyPolicy(db->unicastRoutes).updatedRoutes.size();
+             const auto t2 = std::chrono::steady_clock::now();
+             return py::make_tuple(std::chrono::duration<double>(t1 - t0).count(),
+                                   std::chrono::duration<double>(t2 - t1).count(),
+                                   db ? db->unicastRoutes.size() : 0, updated);
+           })
       .def("create_route_for_prefix_or_get_static_route",
            [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
               py::bytes addr, int32_t len) -> py::object {
