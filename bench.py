@@ -206,6 +206,22 @@ def main():
     barrier()
 
 
+def host_info():
+    """CPU model and core counts of this host (BASELINE.md reporting rules)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
     """Oracle (port of the reference LinkState::runSpf with its containers)
     on this host: a bounded, evenly spaced sample of the same 10k sources."""
@@ -245,6 +261,7 @@ def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
         "cpu_baseline_1t": {"value": round(v1, 2), "unit": "SPF-sources/s", "cores": 1,
                             "kind": "port", "sample": f"{len(sample)} sources"},
         "cpu_build_route_db_ms": round(brdb, 2),
+        "cpu_host": host_info(),
         "speedup_vs_cpu": round(gpu_value / vn, 1),
     }
 

@@ -127,6 +127,9 @@ int orh_last_spf_phase_ms(orh_ctx* ctx, double* dist_ms_out, double* hop_ms_out)
 int orh_device_alloc(orh_ctx* ctx, size_t bytes, void** d_out);
 int orh_device_free(orh_ctx* ctx, void* d_ptr);
 int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+/* device-to-device copy on the context stream, completed before return (hands
+ * rows to a caller-owned buffer, e.g. the RCCL all-gather of a central RIB) */
+int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 
 /* ---- graph mirror (one per area LinkState) ---------------------------- */
 int orh_graph_create(orh_ctx* ctx, orh_graph** out_graph);

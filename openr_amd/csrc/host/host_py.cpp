@@ -223,7 +223,7 @@ struct AreaMap {
 class SpfSweep {
  public:
   SpfSweep(const LinkState& ls, const std::vector<std::string>& srcs, bool useLinkMetric,
-           const std::vector<std::vector<uint32_t>>* ignore = nullptr)
+           const std::vector<std::vector<uint32_t>>* ignore = nullptr, uint32_t minWords = 1)
       : ls_(ls), useLinkMetric_(useLinkMetric) {
     if (ignore) {
       if (ignore->size() != srcs.size())
@@ -247,6 +247,7 @@ class SpfSweep {
     edges_ = ne;
     if (orh_spf_words(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), &words_) != ORH_OK)
       throw std::runtime_error("orh_spf_words failed");
+    words_ = std::max(words_, minWords);  // a shard padded to the whole batch's mask width
     const size_t nd = srcs_.size() * static_cast<size_t>(n_);
     if (orh_device_alloc(ctx_, nd * 4, reinterpret_cast<void**>(&dDist_)) != ORH_OK ||
         orh_device_alloc(ctx_, nd * 4 * words_, reinterpret_cast<void**>(&dNh_)) != ORH_OK)
@@ -289,6 +290,14 @@ class SpfSweep {
     orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_ + i * static_cast<size_t>(n_) * words_,
                    static_cast<size_t>(n_) * words_ * 4);
     return py::make_tuple(dist, nh);
+  }
+  // rows [0, sources) into caller-owned device buffers (e.g. torch tensors
+  // feeding an RCCL all-gather): dist u32[S][N], nh u32[S][N][words]
+  void copyTo(uintptr_t dDist, uintptr_t dNh) {
+    const size_t nd = srcs_.size() * static_cast<size_t>(n_);
+    if ((dDist && orh_memcpy_d2d(ctx_, reinterpret_cast<void*>(dDist), dDist_, nd * 4) != ORH_OK) ||
+        (dNh && orh_memcpy_d2d(ctx_, reinterpret_cast<void*>(dNh), dNh_, nd * 4 * words_) != ORH_OK))
+      throw std::runtime_error(std::string("SpfSweep.copy_to: ") + orh_last_error(ctx_));
   }
   uint32_t words() const { return words_; }
   uint32_t nodes() const { return n_; }
@@ -432,10 +441,24 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("prefetch_spf_results", &LinkState::prefetchSpfResults, py::arg("nodes"),
            py::arg("use_link_metric") = true)
       .def("prefetch_kth_paths", &LinkState::prefetchKthPaths)
-      .def("sweep", [](const LinkState& s, const std::vector<std::string>& srcs, bool useLinkMetric) {
-             return new SpfSweep(s, srcs, useLinkMetric);
+      .def("spf_words",  // first-hop mask words a batch over these sources needs
+           [](const LinkState& s, const std::vector<std::string>& srcs) {
+             std::vector<uint32_t> ids;
+             for (const auto& n : srcs) {
+               auto id = s.nodeId(n);
+               if (!id) throw std::invalid_argument("spf_words: unknown source " + n);
+               ids.push_back(*id);
+             }
+             uint32_t w = 1;
+             if (orh_spf_words(s.deviceGraph(), ids.data(), static_cast<uint32_t>(ids.size()), &w) != ORH_OK)
+               throw std::runtime_error(std::string("orh_spf_words: ") + orh_last_error(s.context()));
+             return w;
+           })
+      .def("sweep", [](const LinkState& s, const std::vector<std::string>& srcs, bool useLinkMetric,
+                       uint32_t minWords) {
+             return new SpfSweep(s, srcs, useLinkMetric, nullptr, minWords);
            },
-           py::arg("srcs"), py::arg("use_link_metric") = true,
+           py::arg("srcs"), py::arg("use_link_metric") = true, py::arg("min_words") = 1,
            py::return_value_policy::take_ownership, py::keep_alive<0, 1>());
 
   py::class_<SpfSweep>(m, "SpfSweep")
@@ -444,6 +467,7 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("phase_ms", &SpfSweep::phaseMs)
       .def("sync", &SpfSweep::sync)
       .def("fetch", &SpfSweep::fetch)
+      .def("copy_to", &SpfSweep::copyTo, py::arg("dist_ptr"), py::arg("nh_ptr"))
       .def_property_readonly("words", &SpfSweep::words)
       .def_property_readonly("nodes", &SpfSweep::nodes)
       .def_property_readonly("edges", &SpfSweep::edges)

@@ -423,6 +423,13 @@ int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes) {
   return ORH_OK;
 }
 
+int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes) {
+  if (!ctx || (!d_dst && bytes) || (!d_src && bytes)) return ORH_E_INVALID;
+  ORH_HIP(ctx, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ORH_OK;
+}
+
 int orh_graph_create(orh_ctx* ctx, orh_graph** out) {
   if (!ctx || !out) return ORH_E_INVALID;
   auto* g = new (std::nothrow) orh_graph();

@@ -31,3 +31,66 @@ def dist_env():
     import os
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def gather_source_tables(local_dist, local_nh, n_sources: int, group=None):
+    """All-gather per-source tables for a central RIB.
+
+    Rank r holds rows shard_bounds(n_sources, world, r) of the dist table
+    (u32 [rows, N], viewed as int32) and of the first-hop table ([rows, N*W]).
+    Blocks differ in size by at most one, so each rank pads its block to
+    ceil(n_sources / world) rows and one all_gather_into_tensor per table
+    moves everything (RCCL over xGMI on GPUs, gloo on CPU). Returns the full
+    [n_sources, ...] tables on every rank, rows in source order.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_bounds(n_sources, world, rank)
+    if local_dist.shape[0] != hi - lo or local_nh.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank}: expected {hi - lo} rows, got "
+                         f"{local_dist.shape[0]} / {local_nh.shape[0]}")
+    block = -(-n_sources // world)
+    out = []
+    for t in (local_dist, local_nh):
+        padded = t.new_zeros((block,) + tuple(t.shape[1:]))
+        padded[: hi - lo] = t
+        full = t.new_empty((block * world,) + tuple(t.shape[1:]))
+        dist.all_gather_into_tensor(full, padded, group=group)
+        keep = torch.cat([full[r * block: r * block + (shard_bounds(n_sources, world, r)[1]
+                                                        - shard_bounds(n_sources, world, r)[0])]
+                          for r in range(world)])
+        out.append(keep)
+    return out[0], out[1]
+
+
+def sharded_all_sources(ls_impl, sources: Sequence[str], use_link_metric: bool = True,
+                        group=None):
+    """All-sources SPF sharded over the ranks of `group`, gathered on every
+    rank: each rank runs its contiguous block of `sources` on its own GPU (the
+    CSR mirror is replicated), copies the rows into torch tensors and the
+    tables are all-gathered. The mask width W is the whole batch's, so every
+    rank's rows have the same shape. Returns (dist [S, N] int32 view of u32,
+    nh [S, N*W] int32 view of u32, W) on the current CUDA device."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    words = ls_impl.spf_words(list(sources))
+    mine = shard_sources(sources, world, rank)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    sweep = ls_impl.sweep(mine, use_link_metric, words) if mine else None
+    n = len(ls_impl.node_names())
+    d = torch.empty((len(mine), n), dtype=torch.int32, device=dev)
+    h = torch.empty((len(mine), n * words), dtype=torch.int32, device=dev)
+    if sweep is not None:
+        sweep.run()
+        sweep.sync()
+        sweep.copy_to(d.data_ptr(), h.data_ptr())
+    if world == 1:
+        return d, h, words
+    full_d, full_h = gather_source_tables(d, h, len(sources), group)
+    return full_d, full_h, words

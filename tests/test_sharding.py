@@ -1,0 +1,150 @@
+"""Multi-GPU path: source sharding and the all-gather of
+per-source tables for a central RIB.
+
+CPU tests run the N > 1 path with the gloo backend at world_size 2: each rank
+owns a contiguous block of the name-ordered sources, fills its rows (here
+from the oracle, the test's checker; on GPUs from its own device sweep) and
+``gather_source_tables`` assembles the full tables on every rank. The GPU test
+runs ``sharded_all_sources`` through the HIP product (world 1 on the one-GPU
+box) and checks the gathered rows against per-source fetches and the oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from openr_amd.sharding import gather_source_tables, shard_bounds, shard_sources
+from openr_amd.types import K_TESTING_AREA as A
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (7, 2), (10000, 8), (13, 5), (3, 8)])
+def test_shard_bounds_partition(n, world):
+    seen = []
+    sizes = []
+    for r in range(world):
+        lo, hi = shard_bounds(n, world, r)
+        seen.extend(range(lo, hi))
+        sizes.append(hi - lo)
+    assert seen == list(range(n))
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_bounds_rejects_bad_rank():
+    with pytest.raises(ValueError):
+        shard_bounds(10, 2, 2)
+    with pytest.raises(ValueError):
+        shard_bounds(10, 0, 0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_tables(n_grid):
+    """Full (dist, nh) tables of the benchmark grid from the oracle: dist in
+    node-name order, nh = bitmask of first hops over the source's neighbours
+    in name order (the product's layout for W = 1)."""
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle", "build"))
+    sys.path.insert(0, root)
+    from openr_amd.facade import Backend, load_topology
+    from openr_amd.topology import bench_grid
+    oracle = Backend(importlib.import_module("openr_oracle"), "oracle")
+    adj_dbs, _ = bench_grid(n_grid)
+    als, _ = load_topology(oracle, adj_dbs, [])
+    ls = als[A]
+    names = sorted(str(i) for i in range(n_grid * n_grid))
+    nbrs = {db.thisNodeName: sorted({a.otherNodeName for a in db.adjacencies}) for db in adj_dbs}
+    dist_t = np.zeros((len(names), len(names)), dtype=np.int32)
+    nh_t = np.zeros_like(dist_t)
+    col = {v: i for i, v in enumerate(names)}
+    for i, s in enumerate(names):
+        res = ls.get_spf_result(s)
+        for v, r in res.items():
+            dist_t[i, col[v]] = r.metric
+            nh_t[i, col[v]] = sum(1 << nbrs[s].index(h) for h in r.nextHops)
+    return names, dist_t, nh_t
+
+
+def _gloo_worker(rank, world, port, n_grid, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names, dist_t, nh_t = _oracle_tables(n_grid)
+        lo, hi = shard_bounds(len(names), world, rank)
+        assert shard_sources(names, world, rank) == names[lo:hi]
+        full_d, full_h = gather_source_tables(torch.from_numpy(dist_t[lo:hi]),
+                                              torch.from_numpy(nh_t[lo:hi]), len(names))
+        ok = (np.array_equal(full_d.numpy(), dist_t) and np.array_equal(full_h.numpy(), nh_t))
+        # the bench's max-over-ranks timing reduction
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put((rank, ok, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_grid", [5, 6])  # 25 sources (uneven blocks), 36 (even)
+def test_gather_source_tables_gloo_world2(n_grid):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, n_grid, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert [r[1] for r in res] == [True, True]
+    assert [r[2] for r in res] == [2.0, 2.0]
+
+
+def test_gather_rejects_wrong_block():
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with pytest.raises(ValueError):
+            gather_source_tables(torch.zeros(3, 4, dtype=torch.int32),
+                                 torch.zeros(3, 4, dtype=torch.int32), 5)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_all_sources_gpu(hip, oracle):
+    """The product path on the GPU: sharded_all_sources (world 1) returns the
+    device rows of every source; they equal the sweep's own rows and the
+    oracle's distances and first-hop sets."""
+    from openr_amd.facade import load_topology
+    from openr_amd.sharding import sharded_all_sources
+    from openr_amd.topology import bench_grid
+    torch.cuda.set_device(0)
+    n = 12
+    adj_dbs, _ = bench_grid(n)
+    als, _ = load_topology(hip, adj_dbs, [])
+    ls = als[A]
+    names = [str(i) for i in range(n * n)]
+    d, h, words = sharded_all_sources(ls._impl, names)
+    assert d.shape == (n * n, n * n) and h.shape == (n * n, n * n * words)
+    d = d.cpu().numpy().view(np.uint32)
+    h = h.cpu().numpy().view(np.uint32)
+    sweep = ls._impl.sweep(names, True)
+    sweep.run()
+    sweep.sync()
+    node_names = ls._impl.node_names()
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    for i in range(0, n * n, 7):
+        dr, nr = sweep.fetch(i)
+        assert np.array_equal(d[i], dr) and np.array_equal(h[i], nr)
+        ref = als_o[A].get_spf_result(names[i])
+        for j, v in enumerate(node_names):
+            assert d[i, j] == ref[v].metric
