@@ -112,11 +112,17 @@ int orh_reset_counters(orh_ctx* ctx);
  *                           LDS-resident per-source kernels, else the HBM
  *                           frontier kernel (graphs beyond LDS, e.g. 50k nodes)
  *   ORH_SPF_PER_SOURCE      per-source kernels only (LDS, HBM when too large)
- *   ORH_SPF_GLOBAL          the HBM frontier kernel for every graph
+ *   ORH_SPF_GLOBAL          the HBM frontier kernel for every graph, with the
+ *                           first hops fused into the search when every
+ *                           source has <= 32 distinct neighbours (AUTO fuses
+ *                           too when the two-phase scheme would need extra
+ *                           neighbour rows: what-if and KSP2 batches)
+ *   ORH_SPF_GLOBAL_TWO_PHASE the HBM frontier kernel, never fused
  * All modes produce identical results; the choice is performance only. */
 #define ORH_SPF_AUTO 0
 #define ORH_SPF_PER_SOURCE 1
 #define ORH_SPF_GLOBAL 2
+#define ORH_SPF_GLOBAL_TWO_PHASE 3
 int orh_set_spf_mode(orh_ctx* ctx, int mode);
 /* device time (HIP events on the context stream) of the last orh_spf_run;
  * waits for that launch to finish */

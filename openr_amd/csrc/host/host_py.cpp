@@ -645,6 +645,6 @@ PYBIND11_MODULE(_openr_host, m) {
   // ORH_SPF_PER_SOURCE / ORH_SPF_GLOBAL); results are identical in every mode
   m.def("set_spf_mode", [](int mode) {
     if (orh_set_spf_mode(defaultContext(), mode) != ORH_OK)
-      throw std::invalid_argument("set_spf_mode: mode must be 0, 1 or 2");
+      throw std::invalid_argument("set_spf_mode: mode must be 0, 1, 2 or 3");
   });
 }

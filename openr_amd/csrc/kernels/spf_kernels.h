@@ -38,6 +38,12 @@ struct SpfArgs {
   uint32_t* out_dist;
   uint32_t* scratch;
   uint64_t* diag;  // ORH_DIAG_STAMPS builds only
+  // HBM kernel with fused first hops (kGlobalNh): per-row {dist, nh} labels,
+  // the first-hop output rows, and the record -> neighbour-rank table
+  unsigned long long* labels;  // [n_rows][N]
+  uint32_t* out_nh;            // [n_out][N][words]
+  uint32_t words;
+  const uint16_t* rank_out;
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -63,12 +69,18 @@ struct HopArgs {
   uint32_t* out_nh;
 };
 
-enum class SpfVariant { kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal };
+enum class SpfVariant {
+  kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal,
+  kGlobalNh  // HBM frontier kernel that also derives the first hops (no phase 2)
+};
 
 // distance-kernel selection (orh_set_spf_mode): automatic (multi-source BFS
 // when eligible, else the LDS-resident per-source kernels, else the HBM
-// frontier kernel), per-source LDS kernels only, or the HBM kernel always
-enum class SpfMode { kAuto = 0, kPerSource = 1, kGlobal = 2 };
+// frontier kernel), per-source LDS kernels only, the HBM kernel always (with
+// fused first hops when every source has <= 32 distinct neighbours), or the
+// two-phase HBM kernel always
+enum class SpfMode { kAuto = 0, kPerSource = 1, kGlobal = 2, kGlobalTwoPhase = 3 };
+constexpr int kSpfModes = 4;
 
 struct SpfPlan {
   SpfVariant variant;

@@ -802,6 +802,164 @@ __global__ __launch_bounds__(256) void spf_global_kernel(SpfArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// phase 1c': HBM frontier relaxation with fused first hops
+// ---------------------------------------------------------------------------
+// The two-phase scheme derives NH(v) from the rows of the source's
+// neighbours; for a batch whose neighbour rows are not sources themselves
+// (what-if SPFs, KSP2 k=2 re-runs, a subset of sources) that multiplies the
+// searches by 1 + deg(s). Here the search carries the closed form directly:
+// each node has a 64-bit label {dist (hi), first-hop mask (lo)} in HBM, and a
+// relaxation from v offers u the candidate {d(v) + w, v == src ? bit(u) :
+// nh(v)}. Labels merge in a lattice: a smaller distance replaces, an equal
+// one ORs the masks; any change re-queues u (near if below the threshold,
+// else far). A candidate whose distance equals d*(u) comes from a predecessor
+// whose distance is already final, so stale bits never survive: the fixpoint
+// is exactly (d*, NH) of SURVEY.md Appendix A.1. Used when every source has
+// at most 32 distinct neighbours (one mask word).
+//
+// The far set also tracks a lower bound of its distances (LDS atomicMin on
+// every far push, recomputed exactly while promoting), so advancing the
+// threshold costs one pass over the far nodes instead of two.
+template <int K>
+__global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_flag[3];
+  __shared__ uint32_t s_min[2];
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
+  uint32_t* near0 = lds;
+  uint32_t* near1 = lds + NB;
+  uint32_t* far = lds + 2 * NB;
+  const Src s(a, row);
+  unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
+
+  for (uint32_t i = tid; i < 3 * NB; i += nthr) lds[i] = 0u;
+  for (uint32_t i = tid; i < N; i += nthr) lab[i] = kInfLabel;
+  if (tid < 3) s_flag[tid] = 0u;
+  if (tid < 2) s_min[tid] = kInf;
+  __syncthreads();
+  if (tid == 0) {
+    lab[s.node] = 0ull;
+    near0[s.node >> 5] = 1u << (s.node & 31u);
+  }
+  __syncthreads();
+
+  const uint32_t delta = a.delta;
+  uint32_t T = delta;  // near/far threshold
+  uint32_t* cur = near0;
+  uint32_t* nxt = near1;
+  uint32_t mpar = 0;  // s_min[mpar] bounds the far set from below
+  for (uint32_t it = 0;; ++it) {
+    bool pushed_near = false;
+    for (uint32_t w = tid; w < NB; w += nthr) {
+      uint32_t bits = cur[w];
+      if (!bits) continue;
+      cur[w] = 0u;
+      while (bits) {
+        const uint32_t v = w * 32 + __builtin_ctz(bits);
+        bits &= bits - 1;
+        uint2 rec[K];
+        load_recs<K>(a, v, rec);
+        if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) continue;  // no transit
+        const unsigned long long lv =
+            __hip_atomic_load(&lab[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t dv = static_cast<uint32_t>(lv >> 32);
+        const uint32_t nhv = static_cast<uint32_t>(lv);
+        const bool from_src = v == s.node;
+        auto relax = [&](const uint2& r, uint32_t q) {
+          if (!live(a, s, r, q)) return;
+          const uint32_t u = r.x & ORH_REC_COL_MASK;
+          const uint32_t nd = dv + (a.use_link_metric ? r.y : 1u);
+          const uint32_t cnh = from_src ? (1u << a.rank_out[q]) : nhv;
+          unsigned long long cl =
+              __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (;;) {
+            const uint32_t cd = static_cast<uint32_t>(cl >> 32);
+            if (nd > cd) return;
+            const unsigned long long nl = nd < cd
+                ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
+                : (cl | cnh);
+            if (nl == cl) return;
+            const unsigned long long old = atomicCAS(&lab[u], cl, nl);
+            if (old == cl) break;
+            cl = old;
+          }
+          const uint32_t bit = 1u << (u & 31u);
+          if (nd < T) {
+            atomicOr(&nxt[u >> 5], bit);
+            atomicAnd(&far[u >> 5], ~bit);  // expanded from the near set instead
+            pushed_near = true;
+          } else {
+            atomicOr(&far[u >> 5], bit);
+            atomicMin(&s_min[mpar], nd);
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < K; ++j) relax(rec[j], v * K + j);
+        const uint2 last = rec[K - 1];
+        if (last.x & ORH_REC_CONT) {
+          const uint32_t start = last.x & ORH_REC_COL_MASK;
+          for (uint32_t q = 0; q < last.y; ++q) relax(a.recs[start + q], start + q);
+        }
+      }
+    }
+    const uint32_t par = it % 3u;
+    if (pushed_near) s_flag[par] = 1u;
+    __syncthreads();  // relaxations (global atomics) and bitmaps settled
+    const bool more_near = s_flag[par] != 0u;
+    if (tid == 0) s_flag[(par + 2u) % 3u] = 0u;  // the previous iteration's flag
+    uint32_t* t = cur;
+    cur = nxt;
+    nxt = t;
+    if (more_near) continue;
+    // near frontier empty: advance the threshold past the far set's lower
+    // bound and promote the far nodes below it; the rest give the exact bound
+    const uint32_t m = s_min[mpar];
+    if (m == kInf) break;  // far set empty: done (every thread read the same value)
+    T = m + delta;
+    const uint32_t npar = mpar ^ 1u;
+    if (tid == 0) s_min[npar] = kInf;
+    __syncthreads();
+    uint32_t local_min = kInf;
+    for (uint32_t w = tid; w < NB; w += nthr) {
+      uint32_t bits = far[w], promote = 0u;
+      for (uint32_t q = bits; q; q &= q - 1) {
+        const uint32_t b = __builtin_ctz(q);
+        const uint32_t d = static_cast<uint32_t>(
+            __hip_atomic_load(&lab[w * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
+        if (d < T) promote |= 1u << b;
+        else local_min = min(local_min, d);
+      }
+      if (promote) {
+        far[w] = bits & ~promote;
+        cur[w] |= promote;
+      }
+    }
+    const uint32_t wm = wave_min(local_min);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
+    mpar = npar;
+    __syncthreads();
+  }
+  __syncthreads();
+  // labels -> dist row (kInf = unreachable) and first-hop row, coalesced
+  uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
+  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * a.words;
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const unsigned long long l =
+        __hip_atomic_load(&lab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_nontemporal_store(static_cast<uint32_t>(l >> 32), &od[i]);
+    if (a.words == 1) {
+      __builtin_nontemporal_store(static_cast<uint32_t>(l), &on[i]);
+    } else {
+      on[static_cast<size_t>(i) * a.words] = static_cast<uint32_t>(l);
+      for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // phase 2: first-hop masks
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
@@ -959,7 +1117,8 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   SpfPlan p{};
   p.ell_k = ell_k;
   if (ell_k != 4 && ell_k != 8) return p;
-  if (mode == SpfMode::kGlobal) return plan_global(p, n_nodes, path_bound, lds_limit);
+  if (mode == SpfMode::kGlobal || mode == SpfMode::kGlobalTwoPhase)
+    return plan_global(p, n_nodes, path_bound, lds_limit);
   const size_t nb = (n_nodes + 31) / 32;
   if (mode == SpfMode::kAuto && multi_source && uniform && path_bound < 0xFFFFFFFFull) {
     // a thread owns J <= 32 nodes (registers); the frontier arrays hold
@@ -1067,6 +1226,8 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
       return launch(spf_dist_kernel<uint32_t, K>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kGlobal:
       return launch(spf_global_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
+    case SpfVariant::kGlobalNh:
+      return launch(spf_global_nh_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     default:
       return hipErrorInvalidValue;
   }

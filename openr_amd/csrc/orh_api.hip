@@ -32,6 +32,9 @@ struct orh_ctx {
   // distance rows of neighbours that are not themselves requested sources
   uint32_t* d_scratch = nullptr;
   size_t d_scratch_cap = 0;  // in u32
+  // HBM kernel with fused first hops: {dist, nh} labels per row
+  unsigned long long* d_labels = nullptr;
+  size_t d_labels_cap = 0;  // in labels
   // multi-source BFS: node-major level bytes
   uint8_t* d_ms_lvl = nullptr;
   size_t d_ms_lvl_cap = 0;
@@ -302,6 +305,16 @@ int ensure_req(orh_ctx* ctx, size_t words) {
   return ORH_OK;
 }
 
+int ensure_labels(orh_ctx* ctx, size_t n) {
+  if (n <= ctx->d_labels_cap) return ORH_OK;
+  hipFree(ctx->d_labels);
+  ctx->d_labels = nullptr;
+  ctx->d_labels_cap = 0;
+  ORH_HIP(ctx, hipMalloc(&ctx->d_labels, n * sizeof(unsigned long long)));
+  ctx->d_labels_cap = n;
+  return ORH_OK;
+}
+
 int ensure_scratch(orh_ctx* ctx, size_t words) {
   if (words <= ctx->d_scratch_cap) return ORH_OK;
   hipFree(ctx->d_scratch);
@@ -351,7 +364,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
     delete ctx;
     return ORH_E_DEVICE;
   }
-  if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % 3);
+  if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % orh::kSpfModes);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
@@ -361,7 +374,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
 }
 
 int orh_set_spf_mode(orh_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 2) return ORH_E_INVALID;
+  if (!ctx || mode < 0 || mode >= orh::kSpfModes) return ORH_E_INVALID;
   ctx->spf_mode = static_cast<orh::SpfMode>(mode);
   return ORH_OK;
 }
@@ -372,6 +385,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   hipFree(ctx->d_req);
   hipFree(ctx->d_scratch);
+  hipFree(ctx->d_labels);
   hipFree(ctx->d_ms_lvl);
   hipFree(ctx->d_batch);
   hipEventDestroy(ctx->ev0);
@@ -729,6 +743,19 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     off_nbr_row = k[t - 3];
     n_rows = k[t - 1];
   }
+  // HBM kernel: fuse the first hops into the search (one row per source)
+  // when one mask word covers every source and the two-phase scheme would
+  // need extra neighbour rows (or the HBM kernel is forced)
+  orh::SpfPlan run_plan = plan;
+  if (plan.variant == orh::SpfVariant::kGlobal && max_nbr <= 32 &&
+      ctx->spf_mode != orh::SpfMode::kGlobalTwoPhase &&
+      (ctx->spf_mode == orh::SpfMode::kGlobal || n_rows > n_src)) {
+    run_plan.variant = orh::SpfVariant::kGlobalNh;
+    n_rows = n_src;
+    int rc = ensure_labels(ctx, static_cast<size_t>(n_src) * N);
+    if (rc) return rc;
+  }
+  const bool fused = run_plan.variant == orh::SpfVariant::kGlobalNh;
   const size_t n_extra = n_rows - n_src;
   if (n_extra) {
     int rc = ensure_scratch(ctx, n_extra * N);
@@ -761,6 +788,10 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.delta = uniform ? w0 : std::max<uint32_t>(1u, g->mean_out);
   a.out_dist = d_dist;
   a.scratch = ctx->d_scratch;
+  a.labels = ctx->d_labels;
+  a.out_nh = d_nh;
+  a.words = words;
+  a.rank_out = g->d_rank_out;
 
   orh::HopArgs h{};
   h.n_nodes = N;
@@ -788,8 +819,12 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   hipMemsetAsync(d_diag, 0, 128, ctx->stream);
   a.diag = d_diag;
 #endif
-  hipError_t e = orh::launch_spf(plan, a, n_rows, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "spf kernel launch");
+  {
+    hipError_t pre = hipGetLastError();
+    if (pre != hipSuccess) { std::string m = "pending HIP error before spf launch (variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + ")"; return hip_fail(ctx, pre, m.c_str()); }
+  }
+  hipError_t e = orh::launch_spf(run_plan, a, n_rows, ctx->stream);
+  if (e != hipSuccess) { std::string m = "spf kernel launch variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + " lds " + std::to_string(run_plan.lds_bytes) + " block " + std::to_string(run_plan.block) + " j " + std::to_string(run_plan.ms_j); return hip_fail(ctx, e, m.c_str()); }
 #ifdef ORH_DIAG_STAMPS
   {
     uint64_t h[16] = {};
@@ -802,8 +837,10 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   }
 #endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
-  e = orh::launch_first_hop(h, max_nbr, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
+  if (!fused) {
+    e = orh::launch_first_hop(h, max_nbr, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
+  }
   ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   ctx->counters.spf_runs += n_src;
   ctx->counters.spf_launches += 1;
