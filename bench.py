@@ -154,6 +154,7 @@ def main():
     kms = statistics.mean(kernel_ms)
     achieved = per_launch / (kms * 1e-3) / 1e9
 
+    traffic, traffic_src = pmc_traffic()
     out = {
         "metric": "all-source SPF runs/sec + buildRouteDb ms on 10k-node topology",
         "value": round(value, 1),
@@ -172,7 +173,8 @@ def main():
                    "parallelism": f"what-if topologies x{world} (rank r > 0: one seeded link drained)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel_ms": round(kms, 4),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel_ms": round(kms, 4),
                      "phase_ms": [round(statistics.mean(p[0] for p in phases), 4),
                                   round(statistics.mean(p[1] for p in phases), 4)],
                      "algorithmic_bytes_per_source": bytes_per_source},
@@ -204,6 +206,33 @@ def main():
 
     print(json.dumps(out), flush=True)
     barrier()
+
+
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v3_pmc.json")
+SWEEP_KERNELS = ("spf_msbfs_kernel", "ms_finalize_kernel", "first_hop_kernel")
+
+
+def pmc_traffic():
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC summary of
+    this same command (tools/profile.sh + tools/pmc_summary.py: FETCH_SIZE
+    doubled per the gfx950 wide-read correction, plus WRITE_SIZE), summed over
+    the kernels of one sweep. PMC counters cannot be read from inside the
+    timed run, so this is the profiled value, not a live one."""
+    try:
+        with open(PMC_PROFILE) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    total, seen = 0.0, []
+    for name, k in prof.items():
+        if any(s in name for s in SWEEP_KERNELS):
+            if k.get("hbm_read_bytes") is None or k.get("hbm_write_bytes") is None:
+                return None, None
+            total += k["hbm_read_bytes"] + k["hbm_write_bytes"]
+            seen.append(name.split("(")[0].replace("void ", ""))
+    if len(seen) != len(SWEEP_KERNELS):
+        return None, None
+    return round(total), os.path.relpath(PMC_PROFILE, ROOT) + ": " + " + ".join(seen)
 
 
 def host_info():

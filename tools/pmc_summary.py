@@ -10,6 +10,7 @@ usage: pmc_summary.py gpurun_out/prof_<tag> [> profiles/rNN/<tag>_pmc_summary.tx
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
@@ -25,10 +26,14 @@ def main(d):
     if os.path.exists(stats):
         for r in csv.DictReader(open(stats)):
             dur[r["Name"]] = float(r["AverageNs"])
+    summary = {}
     for k in kernels:
         if k.startswith("__amd"):
             continue
         c = {n: sum(v) / len(v) for (kk, n), v in agg.items() if kk == k}
+        summary[k] = {"avg_ns": dur.get(k), "counters": c,
+                      "hbm_read_bytes": 2 * c["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in c else None,
+                      "hbm_write_bytes": c["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in c else None}
         print(f"kernel: {k}")
         if k in dur:
             print(f"  avg duration          {dur[k] / 1e3:12.1f} us   (kernel trace)")
@@ -50,6 +55,8 @@ def main(d):
         if "GRBM_GUI_ACTIVE" in c and k in dur:
             print(f"  effective clock             {c['GRBM_GUI_ACTIVE'] / 8 / (dur[k] * 1e-9) / 1e9:10.2f} GHz")
         print()
+    with open(os.path.join(d, "pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
 
 
 if __name__ == "__main__":

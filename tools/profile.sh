@@ -6,14 +6,15 @@
 set -e
 TAG=${1:-run}
 shift || true
-ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline --no-route-db}
+ARGS=${@:---steps 10 --warmup 2 --no-cpu-baseline --no-route-db --legs=}
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 "$REPO/bench.py" $ARGS > "$OUT/trace.log" 2>&1
-for CTR in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+for CTR in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+    "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD"; do
   NAME=$(echo "$CTR" | cut -d' ' -f1)
   timeout -k 10 -s KILL 120 rocprofv3 --pmc $CTR --output-format csv -d "$OUT/pmc_$NAME" -o run \
     -- python3 "$REPO/bench.py" $ARGS > "$OUT/pmc_$NAME.log" 2>&1
