@@ -44,6 +44,8 @@ struct SpfArgs {
   uint32_t* out_nh;            // [n_out][N][words]
   uint32_t words;
   const uint16_t* rank_out;
+  uint8_t* lvl_rows;  // multi-source BFS: u8 level row per row [n_rows][lvl_pitch]
+  uint32_t lvl_pitch;  // N rounded up to 16
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -67,6 +69,11 @@ struct HopArgs {
   const uint32_t* dist;
   const uint32_t* scratch;
   uint32_t* out_nh;
+  // multi-source BFS plans: u8 level rows (255 unreached, 254 = read the u32
+  // row) replace the u32 distance rows as the input; w0 = the uniform metric
+  const uint8_t* lvl_rows;
+  uint32_t lvl_pitch;
+  uint32_t w0;
 };
 
 enum class SpfVariant {
@@ -105,6 +112,10 @@ size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
 // LDS bytes the first-hop kernel needs for max_nbr distinct neighbours
 size_t hop_lds_bytes(uint32_t max_nbr);
 hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s);
+// multi-source BFS plans, phase 2a: node-major level bytes -> requested dist
+// rows (host order) and u8 level rows of every row (a.lvl_rows), which the
+// first-hop phase reads instead of u32 distance rows
+hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
 
 struct RouteSelectArgs {
   uint32_t n_prefix;

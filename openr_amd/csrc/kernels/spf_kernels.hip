@@ -44,6 +44,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -307,7 +308,7 @@ __device__ inline void lds_barrier() {
 }
 
 template <int K, class M, int J>
-__global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
+__global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t kS = MsMask<M>::kS;
   constexpr int KH = (K + 1) / 2;
@@ -366,11 +367,16 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
   }
 
   const uint32_t w0 = a.w0;
+#ifdef ORH_DIAG_STAMPS
+  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+  uint64_t t_bar = 0, t_store = 0;
+  uint32_t n_levels = 0;
+#endif
   for (uint32_t level = 1;; ++level) {
     int prog = 0;
     // opaque per level: keeps the compiler from hoisting J * K unpacked LDS
     // addresses and J per-node pointers out of the level loop (VGPR budget:
-    // two 512-thread workgroups per CU need <= 128)
+    // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
     // groups of G owned nodes: a group is skipped when every lane holds all
@@ -414,8 +420,12 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
           nx = acc[g] & ~vis[j];
           vis[j] |= nx;
         }
+#ifdef ORH_DIAG_STAMPS
+        const uint64_t t_s0 = __builtin_amdgcn_s_memtime();
+#endif
         if (nx) {
           prog = 1;
+          {
           uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
           if (level < kLvlDirect) {
             for (uint32_t q = nx; q; q &= q - 1) lb[__builtin_ctz(q)] = static_cast<uint8_t>(level);
@@ -427,7 +437,11 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
               dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
             }
           }
+          }
         }
+#ifdef ORH_DIAG_STAMPS
+        t_store += __builtin_amdgcn_s_memtime() - t_s0;
+#endif
         if (vis[j] != full || nx) {
           if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
           f_nxt[v] = static_cast<M>(nx);
@@ -439,14 +453,32 @@ __global__ __launch_bounds__(512) void spf_msbfs_kernel(SpfArgs a) {
     // their way to memory are read by the next kernel, and waiting for their
     // write acknowledgements every level (what __syncthreads does) is wasted.
     if (prog) s_prog[level % 3u] = 1u;
+#ifdef ORH_DIAG_STAMPS
+    const uint64_t t_b0 = __builtin_amdgcn_s_memtime();
+#endif
     lds_barrier();
+#ifdef ORH_DIAG_STAMPS
+    t_bar += __builtin_amdgcn_s_memtime() - t_b0;
+    ++n_levels;
+#endif
     if (!s_prog[level % 3u]) break;
     if (tid == 0) s_prog[(level + 2u) % 3u] = 0u;  // the previous level's flag, read before this barrier
     M* t = f_cur;
     f_cur = f_nxt;
     f_nxt = t;
   }
-
+#ifdef ORH_DIAG_STAMPS
+  if ((tid & 63u) == 0) {  // per wave: total, barrier and store-block cycles, levels
+    const uint64_t tot = __builtin_amdgcn_s_memtime() - t_begin;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[0]), tot);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[1]), t_bar);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[3]), static_cast<unsigned long long>(n_levels));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[4]), 1ull);
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.diag[5]), tot);
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.diag[6]), static_cast<unsigned long long>(n_levels));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[8]), t_store);
+  }
+#endif
 }
 
 // node-major level bytes -> host-order u32 distance rows, one workgroup per
@@ -456,12 +488,16 @@ template <class M>
 __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t tiles) {
   constexpr uint32_t kS = MsMask<M>::kS;
   __shared__ uint32_t* s_out[kS];
+  __shared__ uint32_t s_row[kS];
   const uint32_t N = a.n_nodes;
   const uint32_t batch = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const uint32_t i = tile * 256 + threadIdx.x;
   const uint32_t b0 = batch * kS;
   const uint32_t S = min(kS, a.n_rows - b0);
-  if (threadIdx.x < S) s_out[threadIdx.x] = dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + threadIdx.x]);
+  if (threadIdx.x < S) {
+    s_row[threadIdx.x] = a.order[b0 + threadIdx.x];
+    s_out[threadIdx.x] = dist_row(a.out_dist, a.scratch, a.n_out, N, s_row[threadIdx.x]);
+  }
   __syncthreads();
   if (i >= N) return;
   const uint32_t v = a.dev_of[i];
@@ -480,7 +516,10 @@ __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t ti
   for (uint32_t b = 0; b < kS; ++b) {
     if (b >= S) break;
     const uint32_t l = (w[b / 4] >> ((b & 3u) * 8u)) & 0xFFu;
-    if (l == kLvlDirect) continue;
+    const uint32_t r = s_row[b];
+    a.lvl_rows[static_cast<size_t>(r) * a.lvl_pitch + i] = static_cast<uint8_t>(l);
+    // neighbour-only rows are read through their level row
+    if (l == kLvlDirect || r >= a.n_out) continue;
     __builtin_nontemporal_store(l == kLvlNone ? kInf : l * w0, &s_out[b][i]);
   }
 }
@@ -962,12 +1001,23 @@ __global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
 // ---------------------------------------------------------------------------
 // phase 2: first-hop masks
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t s_cnt;
-  const uint32_t N = a.n_nodes;
+// distance of node x in row `row`: the u32 distance row, or (multi-source
+// plans) the u8 level row scaled by w0
+template <bool kLvl>
+__device__ inline uint32_t hop_dist(const HopArgs& a, uint32_t row, uint32_t x) {
+  const uint32_t* dr = dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch),
+                                a.n_out, a.n_nodes, row);
+  if (!kLvl) return dr[x];
+  const uint32_t l = a.lvl_rows[static_cast<size_t>(row) * a.lvl_pitch + x];
+  return l == kLvlNone ? kInf : l == kLvlDirect ? dr[x] : l * a.w0;
+}
+
+// the source's tight first links into LDS: ent[k] = {n, d_s(n), n's row,
+// rank | 0x80000000 if n is overloaded}; returns the count. LDS layout:
+// minw[nb] | node[nb] | ent[nb] (hop_lds_bytes)
+template <bool kLvl>
+__device__ inline uint32_t hop_entries(const HopArgs& a, uint32_t i, uint32_t* lds, uint32_t* s_cnt) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
   const uint32_t src = a.srcs[i];
   const uint32_t nb0 = a.nbr_ptr[i], nb = a.nbr_ptr[i + 1] - nb0;
   uint32_t* minw = lds;
@@ -981,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
   }
 
   for (uint32_t r = tid; r < nb; r += kBlock) minw[r] = kInf;
-  if (tid == 0) s_cnt = 0;
+  if (tid == 0) *s_cnt = 0;
   __syncthreads();
   // the source's links: smallest live metric per distinct neighbour
   const uint32_t K = a.ell_k;
@@ -998,19 +1048,32 @@ __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
   if (last.x & ORH_REC_CONT)
     for (uint32_t j = tid; j < last.y; j += kBlock) consider((last.x & ORH_REC_COL_MASK) + j);
   __syncthreads();
-  const uint32_t* ds = dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch),
-                                a.n_out, N, i);
   // tight first links: d_s(n) equals the cheapest live link to n
   for (uint32_t r = tid; r < nb; r += kBlock) {
     if (minw[r] == kInf) continue;
     const uint32_t u = node[r];
-    const uint32_t du = ds[u];
+    const uint32_t du = hop_dist<kLvl>(a, i, u);
     if (du != minw[r]) continue;
-    const uint32_t k = atomicAdd(&s_cnt, 1u);
+    const uint32_t k = atomicAdd(s_cnt, 1u);
     ent[k] = make_uint4(u, du, a.nbr_row[nb0 + r], r | (a.overloaded[u] ? 0x80000000u : 0u));
   }
   __syncthreads();
-  const uint32_t ne = s_cnt;
+  return *s_cnt;
+}
+
+__global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_cnt;
+  const uint32_t N = a.n_nodes;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
+  const uint32_t src = a.srcs[i];
+  const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
+  const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
+  const uint32_t ne = hop_entries<false>(a, i, lds, &s_cnt);
+  const uint32_t* ds = dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch),
+                                a.n_out, N, i);
+
 
   uint32_t v[kHopPer], dv[kHopPer];
 #pragma unroll
@@ -1045,6 +1108,82 @@ __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
 #pragma unroll
     for (int k = 0; k < kHopPer; ++k)
       if (v[k] < N) __builtin_nontemporal_store(acc[k], &nh[static_cast<size_t>(v[k]) * W + word]);
+  }
+}
+
+// first hops of multi-source BFS rows: the same closed form over u8 level
+// rows (pitch a multiple of 16), 16 consecutive nodes per thread so every
+// row access is one 16-byte load and the masks leave as 16-byte stores
+constexpr uint32_t kLvlPer = 16;
+
+__device__ inline uint32_t lvl_byte(const uint4& x, uint32_t k) {
+  const uint32_t w = k < 4 ? x.x : k < 8 ? x.y : k < 12 ? x.z : x.w;
+  return (w >> ((k & 3u) * 8u)) & 0xFFu;
+}
+
+__global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_cnt;
+  const uint32_t N = a.n_nodes, P = a.lvl_pitch, w0 = a.w0;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
+  const uint32_t src = a.srcs[i];
+  const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
+  const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
+  const uint32_t ne = hop_entries<true>(a, i, lds, &s_cnt);
+  const uint32_t v0 = (tile * kBlock + tid) * kLvlPer;
+  if (v0 >= N) return;
+  auto dist_at = [&](uint32_t row, const uint4& x, uint32_t k) -> uint32_t {
+    const uint32_t l = lvl_byte(x, k);
+    if (l == kLvlNone) return kInf;
+    if (l == kLvlDirect)
+      return dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch), a.n_out,
+                      N, row)[v0 + k];
+    return l * w0;
+  };
+  const uint4 own = *reinterpret_cast<const uint4*>(a.lvl_rows + static_cast<size_t>(i) * P + v0);
+  uint32_t dv[kLvlPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kLvlPer; ++k) {
+    dv[k] = dist_at(i, own, k);
+    if (v0 + k == src || v0 + k >= N) dv[k] = kInf;  // the source has no next hops
+  }
+  const uint32_t W = a.words;
+  uint32_t* nh = a.out_nh + static_cast<size_t>(i) * N * W;
+  for (uint32_t word = 0; word < W; ++word) {
+    uint32_t acc[kLvlPer] = {};
+    for (uint32_t e = 0; e < ne; ++e) {
+      const uint4 en = ent[e];
+      const uint32_t r = en.w & 0x7FFFFFFFu;
+      if ((r >> 5) != word) continue;
+      const uint32_t bit = 1u << (r & 31u);
+      if (en.x >= v0 && en.x < v0 + kLvlPer) {
+#pragma unroll
+        for (uint32_t k = 0; k < kLvlPer; ++k)
+          if (v0 + k == en.x && dv[k] != kInf) acc[k] |= bit;
+      }
+      if (en.w & 0x80000000u) continue;  // overloaded neighbour: no transit
+      const uint4 nx = *reinterpret_cast<const uint4*>(a.lvl_rows + static_cast<size_t>(en.z) * P + v0);
+#pragma unroll
+      for (uint32_t k = 0; k < kLvlPer; ++k) {
+        if (dv[k] == kInf) continue;
+        const uint32_t x = dist_at(en.z, nx, k);
+        if (x != kInf && static_cast<uint64_t>(en.y) + x == dv[k]) acc[k] |= bit;
+      }
+    }
+    if (W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
+#pragma unroll
+      for (uint32_t q = 0; q < kLvlPer / 4; ++q) {
+        const u32x4 x = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+        __builtin_nontemporal_store(x, &o[q]);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < kLvlPer; ++k)
+        if (v0 + k < N) nh[static_cast<size_t>(v0 + k) * W + word] = acc[k];
+    }
   }
 }
 
@@ -1123,7 +1262,9 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   if (mode == SpfMode::kAuto && multi_source && uniform && path_bound < 0xFFFFFFFFull) {
     // a thread owns J <= 32 nodes (registers); the frontier arrays hold
     // N + 1 entries (the last is the always-zero target of dead slots)
-    const uint32_t block = n_nodes <= 4096 ? 256 : 512;
+    // 12 waves per workgroup beat 8 and 16 on the 10k grid (one workgroup
+    // per CU; per-level latency is what the search time is made of)
+    const uint32_t block = n_nodes <= 4096 ? 256 : 768;
     const uint32_t j = (n_nodes + block - 1) / block;
     const uint32_t pitch = (n_nodes + 1 + 15) & ~15u;
     if (j <= 32) {
@@ -1172,11 +1313,7 @@ template <int K, class M, int J>
 static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   constexpr uint32_t kS = MsMask<M>::kS;
   const uint32_t batches = (n_rows + kS - 1) / kS;
-  hipError_t e = launch(spf_msbfs_kernel<K, M, J>, a, batches, plan.block, plan.lds_bytes, s);
-  if (e != hipSuccess) return e;
-  const uint32_t tiles = (a.n_nodes + 255) / 256;
-  hipLaunchKernelGGL(ms_finalize_kernel<M>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
-  return hipGetLastError();
+  return launch(spf_msbfs_kernel<K, M, J>, a, batches, plan.block, plan.lds_bytes, s);
 }
 
 template <int K, class M>
@@ -1251,8 +1388,27 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s) {
   a.tiles = (a.n_nodes + kBlock * kHopPer - 1) / (kBlock * kHopPer);
   const uint64_t grid = static_cast<uint64_t>(a.tiles) * a.n_out;
   if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock,
-                std::max<size_t>(hop_lds_bytes(max_nbr), 16), s);
+  const size_t lds = std::max<size_t>(hop_lds_bytes(max_nbr), 16);
+  if (a.lvl_rows) {
+    a.tiles = (a.n_nodes + kBlock * kLvlPer - 1) / (kBlock * kLvlPer);
+    const uint64_t g2 = static_cast<uint64_t>(a.tiles) * a.n_out;
+    if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    return launch(first_hop_lvl_kernel, a, static_cast<uint32_t>(g2), kBlock, lds, s);
+  }
+  return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock, lds, s);
+}
+
+hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {
+  if (plan.variant != SpfVariant::kMsBfs || n_rows == 0) return hipErrorInvalidValue;
+  a.n_rows = n_rows;
+  const uint32_t kS = plan.mask_bytes * 8;
+  const uint32_t batches = (n_rows + kS - 1) / kS;
+  const uint32_t tiles = (a.n_nodes + 255) / 256;
+  if (plan.mask_bytes == 2)
+    hipLaunchKernelGGL(ms_finalize_kernel<uint16_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
+  else
+    hipLaunchKernelGGL(ms_finalize_kernel<uint32_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
+  return hipGetLastError();
 }
 
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s) {

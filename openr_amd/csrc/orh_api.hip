@@ -35,6 +35,9 @@ struct orh_ctx {
   // HBM kernel with fused first hops: {dist, nh} labels per row
   unsigned long long* d_labels = nullptr;
   size_t d_labels_cap = 0;  // in labels
+  // multi-source BFS: u8 level row per row (first-hop input)
+  uint8_t* d_lvl_rows = nullptr;
+  size_t d_lvl_rows_cap = 0;  // in bytes
   // multi-source BFS: node-major level bytes
   uint8_t* d_ms_lvl = nullptr;
   size_t d_ms_lvl_cap = 0;
@@ -305,6 +308,16 @@ int ensure_req(orh_ctx* ctx, size_t words) {
   return ORH_OK;
 }
 
+int ensure_lvl_rows(orh_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->d_lvl_rows_cap) return ORH_OK;
+  hipFree(ctx->d_lvl_rows);
+  ctx->d_lvl_rows = nullptr;
+  ctx->d_lvl_rows_cap = 0;
+  ORH_HIP(ctx, hipMalloc(&ctx->d_lvl_rows, bytes));
+  ctx->d_lvl_rows_cap = bytes;
+  return ORH_OK;
+}
+
 int ensure_labels(orh_ctx* ctx, size_t n) {
   if (n <= ctx->d_labels_cap) return ORH_OK;
   hipFree(ctx->d_labels);
@@ -386,6 +399,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_req);
   hipFree(ctx->d_scratch);
   hipFree(ctx->d_labels);
+  hipFree(ctx->d_lvl_rows);
   hipFree(ctx->d_ms_lvl);
   hipFree(ctx->d_batch);
   hipEventDestroy(ctx->ev0);
@@ -776,6 +790,10 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     a.dev_of = g->d_ms_dev_of;
     a.host_of = g->d_ms_host_of;
     a.ms_lvl = ctx->d_ms_lvl;
+    a.lvl_pitch = (N + 15u) & ~15u;
+    rc = ensure_lvl_rows(ctx, static_cast<size_t>(n_rows) * a.lvl_pitch);
+    if (rc) return rc;
+    a.lvl_rows = ctx->d_lvl_rows;
   }
   a.order = ctx->d_req + off_order;
   a.srcs = ctx->d_req + 1;
@@ -811,6 +829,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   h.dist = d_dist;
   h.scratch = ctx->d_scratch;
   h.out_nh = d_nh;
+  h.lvl_rows = run_plan.variant == orh::SpfVariant::kMsBfs ? a.lvl_rows : nullptr;
+  h.lvl_pitch = a.lvl_pitch;
+  h.w0 = w0;
 
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
 #ifdef ORH_DIAG_STAMPS
@@ -837,7 +858,12 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   }
 #endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
-  if (!fused) {
+  if (run_plan.variant == orh::SpfVariant::kMsBfs) {
+    e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
+    e = orh::launch_first_hop(h, max_nbr, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
+  } else if (!fused) {
     e = orh::launch_first_hop(h, max_nbr, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
   }
