@@ -208,8 +208,8 @@ def main():
     barrier()
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v3_pmc.json")
-SWEEP_KERNELS = ("spf_msbfs_kernel", "ms_finalize_kernel", "first_hop_kernel")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v5_pmc.json")
+SWEEP_KERNELS = ("spf_msbfs_kernel", "ms_finalize_kernel", "first_hop_lvl_kernel")
 
 
 def pmc_traffic():

@@ -56,6 +56,7 @@ struct HopArgs {
   uint32_t words;
   uint32_t ell_k;
   uint32_t tiles;  // node tiles per source
+  uint32_t tile_split;  // level-row kernel: workgroups per source (tile phases)
   const uint2* recs;
   const uint32_t* link;
   const uint16_t* rank_out;  // per record: col's rank among the row node's distinct neighbours

@@ -1112,77 +1112,127 @@ __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
 }
 
 // first hops of multi-source BFS rows: the same closed form over u8 level
-// rows (pitch a multiple of 16), 16 consecutive nodes per thread so every
-// row access is one 16-byte load and the masks leave as 16-byte stores
-constexpr uint32_t kLvlPer = 16;
+// rows (pitch a multiple of 16), P consecutive nodes per thread so every row
+// access is one P-byte load (P = 16 for large batches; 4 keeps small ones
+// spread over more workgroups)
+template <uint32_t P>
+struct LvlVec;
+template <>
+struct LvlVec<16> {
+  typedef uint4 T;
+  __device__ static uint32_t byte(const uint4& x, uint32_t k) {
+    const uint32_t w = k < 4 ? x.x : k < 8 ? x.y : k < 12 ? x.z : x.w;
+    return (w >> ((k & 3u) * 8u)) & 0xFFu;
+  }
+};
+template <>
+struct LvlVec<4> {
+  typedef uint32_t T;
+  __device__ static uint32_t byte(const uint32_t& x, uint32_t k) { return (x >> (k * 8u)) & 0xFFu; }
+};
 
-__device__ inline uint32_t lvl_byte(const uint4& x, uint32_t k) {
-  const uint32_t w = k < 4 ? x.x : k < 8 ? x.y : k < 12 ? x.z : x.w;
-  return (w >> ((k & 3u) * 8u)) & 0xFFu;
+__device__ inline bool has_byte_fe(uint32_t x) {  // some byte == kLvlDirect
+  const uint32_t z = x ^ 0xFEFEFEFEu;
+  return ((z - 0x01010101u) & ~z & 0x80808080u) != 0u;
 }
 
+// One workgroup per (source, tile phase): the source's tight first links are
+// gathered once, then the workgroup walks tiles phase, phase + split, ...
+template <uint32_t kLvlPer>
 __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_cnt;
+  typedef typename LvlVec<kLvlPer>::T Vec;
+  constexpr uint32_t kWords = kLvlPer / 4;
   const uint32_t N = a.n_nodes, P = a.lvl_pitch, w0 = a.w0;
   const uint32_t tid = threadIdx.x;
-  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
+  const uint32_t split = a.tile_split;
+  const uint32_t i = blockIdx.x / split, phase = blockIdx.x % split;
   const uint32_t src = a.srcs[i];
   const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
   const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
   const uint32_t ne = hop_entries<true>(a, i, lds, &s_cnt);
-  const uint32_t v0 = (tile * kBlock + tid) * kLvlPer;
-  if (v0 >= N) return;
-  auto dist_at = [&](uint32_t row, const uint4& x, uint32_t k) -> uint32_t {
-    const uint32_t l = lvl_byte(x, k);
-    if (l == kLvlNone) return kInf;
-    if (l == kLvlDirect)
-      return dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch), a.n_out,
-                      N, row)[v0 + k];
-    return l * w0;
-  };
-  const uint4 own = *reinterpret_cast<const uint4*>(a.lvl_rows + static_cast<size_t>(i) * P + v0);
-  uint32_t dv[kLvlPer];
-#pragma unroll
-  for (uint32_t k = 0; k < kLvlPer; ++k) {
-    dv[k] = dist_at(i, own, k);
-    if (v0 + k == src || v0 + k >= N) dv[k] = kInf;  // the source has no next hops
-  }
   const uint32_t W = a.words;
   uint32_t* nh = a.out_nh + static_cast<size_t>(i) * N * W;
-  for (uint32_t word = 0; word < W; ++word) {
-    uint32_t acc[kLvlPer] = {};
-    for (uint32_t e = 0; e < ne; ++e) {
-      const uint4 en = ent[e];
-      const uint32_t r = en.w & 0x7FFFFFFFu;
-      if ((r >> 5) != word) continue;
-      const uint32_t bit = 1u << (r & 31u);
-      if (en.x >= v0 && en.x < v0 + kLvlPer) {
-#pragma unroll
-        for (uint32_t k = 0; k < kLvlPer; ++k)
-          if (v0 + k == en.x && dv[k] != kInf) acc[k] |= bit;
+  for (uint32_t tile = phase; tile < a.tiles; tile += split) {
+    const uint32_t v0 = (tile * kBlock + tid) * kLvlPer;
+    if (v0 >= N) break;
+    auto dist_at = [&](uint32_t row, const Vec& x, uint32_t k) -> uint32_t {
+      const uint32_t l = LvlVec<kLvlPer>::byte(x, k);
+      if (l == kLvlNone) return kInf;
+      if (l == kLvlDirect)
+        return dist_row(const_cast<uint32_t*>(a.dist), const_cast<uint32_t*>(a.scratch), a.n_out,
+                        N, row)[v0 + k];
+      return l * w0;
+    };
+    auto words_of = [](const Vec& x, uint32_t (&w)[kWords]) {
+      if constexpr (kLvlPer == 16) {
+        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      } else {
+        w[0] = x;
       }
-      if (en.w & 0x80000000u) continue;  // overloaded neighbour: no transit
-      const uint4 nx = *reinterpret_cast<const uint4*>(a.lvl_rows + static_cast<size_t>(en.z) * P + v0);
+    };
+    const Vec own = *reinterpret_cast<const Vec*>(a.lvl_rows + static_cast<size_t>(i) * P + v0);
+    uint32_t ow[kWords];
+    words_of(own, ow);
+    bool own_direct = false;
 #pragma unroll
-      for (uint32_t k = 0; k < kLvlPer; ++k) {
-        if (dv[k] == kInf) continue;
-        const uint32_t x = dist_at(en.z, nx, k);
-        if (x != kInf && static_cast<uint64_t>(en.y) + x == dv[k]) acc[k] |= bit;
+    for (uint32_t q = 0; q < kWords; ++q) own_direct |= has_byte_fe(ow[q]);
+    uint32_t dv[kLvlPer], ls[kLvlPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kLvlPer; ++k) {
+      dv[k] = dist_at(i, own, k);
+      ls[k] = LvlVec<kLvlPer>::byte(own, k);
+      if (v0 + k == src || v0 + k >= N) {  // the source has no next hops
+        dv[k] = kInf;
+        ls[k] = kLvlNone;
       }
     }
-    if (W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
+    for (uint32_t word = 0; word < W; ++word) {
+      uint32_t acc[kLvlPer] = {};
+      for (uint32_t e = 0; e < ne; ++e) {
+        const uint4 en = ent[e];
+        const uint32_t r = en.w & 0x7FFFFFFFu;
+        if ((r >> 5) != word) continue;
+        const uint32_t bit = 1u << (r & 31u);
+        if (en.x >= v0 && en.x < v0 + kLvlPer) {
 #pragma unroll
-      for (uint32_t q = 0; q < kLvlPer / 4; ++q) {
-        const u32x4 x = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
-        __builtin_nontemporal_store(x, &o[q]);
+          for (uint32_t k = 0; k < kLvlPer; ++k)
+            if (v0 + k == en.x && dv[k] != kInf) acc[k] |= bit;
+        }
+        if (en.w & 0x80000000u) continue;  // overloaded neighbour: no transit
+        const Vec nx = *reinterpret_cast<const Vec*>(a.lvl_rows + static_cast<size_t>(en.z) * P + v0);
+        uint32_t nw[kWords];
+        words_of(nx, nw);
+        bool direct = own_direct || en.y != w0;
+#pragma unroll
+        for (uint32_t q = 0; q < kWords; ++q) direct |= has_byte_fe(nw[q]);
+        if (!direct) {  // plain levels: tight iff L_n(v) + 1 == L_s(v)
+#pragma unroll
+          for (uint32_t k = 0; k < kLvlPer; ++k)
+            if (((nw[k / 4] >> ((k & 3u) * 8u)) & 0xFFu) + 1u == ls[k]) acc[k] |= bit;
+        } else {
+#pragma unroll
+          for (uint32_t k = 0; k < kLvlPer; ++k) {
+            if (dv[k] == kInf) continue;
+            const uint32_t x = dist_at(en.z, nx, k);
+            if (x != kInf && static_cast<uint64_t>(en.y) + x == dv[k]) acc[k] |= bit;
+          }
+        }
       }
-    } else {
+      if (kLvlPer == 16 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
 #pragma unroll
-      for (uint32_t k = 0; k < kLvlPer; ++k)
-        if (v0 + k < N) nh[static_cast<size_t>(v0 + k) * W + word] = acc[k];
+        for (uint32_t q = 0; q < kLvlPer / 4; ++q) {
+          const u32x4 x = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+          __builtin_nontemporal_store(x, &o[q]);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kLvlPer; ++k)
+          if (v0 + k < N) nh[static_cast<size_t>(v0 + k) * W + word] = acc[k];
+      }
     }
   }
 }
@@ -1390,10 +1440,18 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s) {
   if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const size_t lds = std::max<size_t>(hop_lds_bytes(max_nbr), 16);
   if (a.lvl_rows) {
-    a.tiles = (a.n_nodes + kBlock * kLvlPer - 1) / (kBlock * kLvlPer);
-    const uint64_t g2 = static_cast<uint64_t>(a.tiles) * a.n_out;
+    // 16 nodes per thread unless that leaves fewer than ~32 workgroups per CU
+    // a workgroup per source walks the tiles (one gather of the source's
+    // first links), split over phases while that leaves < 8192 workgroups
+    const uint32_t t16 = (a.n_nodes + kBlock * 16 - 1) / (kBlock * 16);
+    const bool wide = static_cast<uint64_t>(t16) * a.n_out >= 8192;
+    a.tiles = wide ? t16 : (a.n_nodes + kBlock * 4 - 1) / (kBlock * 4);
+    a.tile_split = 1;
+    while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;
+    const uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
     if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    return launch(first_hop_lvl_kernel, a, static_cast<uint32_t>(g2), kBlock, lds, s);
+    return wide ? launch(first_hop_lvl_kernel<16>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
+                : launch(first_hop_lvl_kernel<4>, a, static_cast<uint32_t>(g2), kBlock, lds, s);
   }
   return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock, lds, s);
 }
