@@ -176,6 +176,55 @@ py::tuple routeDbToWire(const DecisionRouteDb& db) {
   return py::make_tuple(uc, mp);
 }
 
+DecisionRouteDb routeDbFromWire(const py::tuple& w) {
+  DecisionRouteDb db;
+  for (auto u : w[0]) {
+    RibUnicastEntry e = unicastFromWire(u.cast<py::tuple>());
+    auto key = e.prefix;
+    db.unicastRoutes.emplace(std::move(key), std::move(e));
+  }
+  for (auto m : w[1]) {
+    auto t = m.cast<py::tuple>();
+    RibMplsEntry e;
+    e.label = t[0].cast<int32_t>();
+    for (auto nh : t[1]) e.nexthops.insert(nhFromWire(nh.cast<py::tuple>()));
+    db.mplsRoutes.emplace(e.label, std::move(e));
+  }
+  return db;
+}
+
+// DecisionRouteUpdate as (unicast updates, unicast deletes (addr, len),
+// mpls updates (label, nexthops), mpls deletes)
+py::tuple deltaToWire(const DecisionRouteUpdate& d) {
+  py::list uu, ud, mu;
+  for (const auto& [_, e] : d.unicastRoutesToUpdate) uu.append(unicastToWire(e));
+  for (const auto& p : d.unicastRoutesToDelete) ud.append(py::make_tuple(py::bytes(p.first), p.second));
+  for (const auto& e : d.mplsRoutesToUpdate) mu.append(py::make_tuple(e.label, nhsToWire(e.nexthops)));
+  return py::make_tuple(uu, ud, mu, py::cast(d.mplsRoutesToDelete));
+}
+
+DecisionRouteUpdate deltaFromWire(const py::tuple& w) {
+  DecisionRouteUpdate d;
+  for (auto u : w[0]) {
+    RibUnicastEntry e = unicastFromWire(u.cast<py::tuple>());
+    auto key = e.prefix;
+    d.unicastRoutesToUpdate.emplace(std::move(key), std::move(e));
+  }
+  for (auto p : w[1]) {
+    auto t = p.cast<py::tuple>();
+    d.unicastRoutesToDelete.emplace_back(str(t[0]), t[1].cast<int32_t>());
+  }
+  for (auto m : w[2]) {
+    auto t = m.cast<py::tuple>();
+    RibMplsEntry e;
+    e.label = t[0].cast<int32_t>();
+    for (auto nh : t[1]) e.nexthops.insert(nhFromWire(nh.cast<py::tuple>()));
+    d.mplsRoutesToUpdate.push_back(std::move(e));
+  }
+  d.mplsRoutesToDelete = w[3].cast<std::vector<int32_t>>();
+  return d;
+}
+
 py::tuple changeToWire(const LinkStateChange& c) {
   return py::make_tuple(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged);
 }
@@ -473,6 +522,15 @@ PYBIND11_MODULE(_openr_host, m) {
       .def_property_readonly("edges", &SpfSweep::edges)
       .def_property_readonly("sources", &SpfSweep::sources);
 
+  // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
+  m.def("calculate_update", [](py::tuple old_db, py::tuple new_db) {
+    return deltaToWire(routeDbFromWire(old_db).calculateUpdate(routeDbFromWire(new_db)));
+  });
+  m.def("apply_update", [](py::tuple db, py::tuple delta) {
+    DecisionRouteDb d = routeDbFromWire(db);
+    d.update(deltaFromWire(delta));
+    return routeDbToWire(d);
+  });
   m.def("path_a_in_path_b", [](std::vector<py::tuple>, std::vector<py::tuple>) -> bool {
     throw std::runtime_error("path_a_in_path_b: use LinkState paths (ids are per LinkState)");
   });

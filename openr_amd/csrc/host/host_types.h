@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <optional>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -144,16 +145,64 @@ struct RibUnicastEntry {
   std::optional<PrefixEntry> bestPrefixEntry;
   std::string bestArea;
   bool doNotInstall{false};
+  // RibEntry.h:65-69: bestArea does not take part
+  bool operator==(const RibUnicastEntry& o) const {
+    return prefix == o.prefix && bestPrefixEntry == o.bestPrefixEntry &&
+        doNotInstall == o.doNotInstall && nexthops == o.nexthops;
+  }
+  bool operator!=(const RibUnicastEntry& o) const { return !(*this == o); }
 };
 
 struct RibMplsEntry {
   int32_t label{0};
   NextHopSet nexthops;
+  bool operator==(const RibMplsEntry& o) const { return label == o.label && nexthops == o.nexthops; }  // RibEntry.h:123-126
+  bool operator!=(const RibMplsEntry& o) const { return !(*this == o); }
+};
+
+// DecisionRouteUpdate (openr/decision/RouteUpdate.h:23-41): the delta Decision
+// publishes to Fib / PrefixManager after a rebuild
+struct DecisionRouteUpdate {
+  std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutesToUpdate;
+  std::vector<Cidr> unicastRoutesToDelete;
+  std::vector<RibMplsEntry> mplsRoutesToUpdate;
+  std::vector<int32_t> mplsRoutesToDelete;
 };
 
 struct DecisionRouteDb {
   std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutes;
   std::unordered_map<int32_t, RibMplsEntry> mplsRoutes;
+
+  // calculateUpdate (openr/decision/Decision.cpp:108-143): new or changed
+  // entries of newDb are updates; keys of this db missing from newDb are
+  // deletes. Lists follow newDb's / this db's iteration order, as there.
+  DecisionRouteUpdate calculateUpdate(DecisionRouteDb&& newDb) const {
+    DecisionRouteUpdate delta;
+    for (auto& [prefix, entry] : newDb.unicastRoutes) {
+      auto it = unicastRoutes.find(prefix);
+      if (it == unicastRoutes.end() || it->second != entry) {
+        if (!delta.unicastRoutesToUpdate.emplace(prefix, std::move(entry)).second)
+          throw std::logic_error("calculateUpdate: duplicate unicast route");  // RouteUpdate.h:39 CHECK
+      }
+    }
+    for (const auto& [prefix, _] : unicastRoutes)
+      if (!newDb.unicastRoutes.count(prefix)) delta.unicastRoutesToDelete.push_back(prefix);
+    for (const auto& [label, entry] : newDb.mplsRoutes) {
+      auto it = mplsRoutes.find(label);
+      if (it == mplsRoutes.end() || it->second != entry) delta.mplsRoutesToUpdate.push_back(entry);
+    }
+    for (const auto& [label, _] : mplsRoutes)
+      if (!newDb.mplsRoutes.count(label)) delta.mplsRoutesToDelete.push_back(label);
+    return delta;
+  }
+
+  // update (openr/decision/Decision.cpp:146-160): deletes first, then updates
+  void update(const DecisionRouteUpdate& u) {
+    for (const auto& p : u.unicastRoutesToDelete) unicastRoutes.erase(p);
+    for (const auto& [_, e] : u.unicastRoutesToUpdate) unicastRoutes.insert_or_assign(e.prefix, e);
+    for (auto l : u.mplsRoutesToDelete) mplsRoutes.erase(l);
+    for (const auto& e : u.mplsRoutesToUpdate) mplsRoutes.insert_or_assign(e.label, e);
+  }
 };
 
 struct LinkStateChange {

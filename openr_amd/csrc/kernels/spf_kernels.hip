@@ -284,6 +284,14 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
 // dword stores for whole nibbles cost more than the stores they save.) Levels
 // >= 254 are written to the output row directly (marker 254), so any depth is
 // exact; 255 = unreached.
+//
+// The search is latency-bound, not LDS-bound: on the 10k grid one workgroup
+// takes ~0.7 ms whether 32 or 313 of them run (two fit per CU), ~165 levels
+// of ~9k cycles, of which ~25 % are the level-byte stores and ~23 % the
+// barrier. A top-down form (a node reads only its own word, new frontier
+// nodes OR their bits into their neighbours' words with ds_or) issues ~4x
+// fewer LDS operations and measured slower: 0.79 vs 0.74 ms (grid), 0.21 vs
+// 0.18 ms (C3 Clos).
 constexpr uint32_t kLvlDirect = 254u, kLvlNone = 255u;
 
 template <class M>
@@ -425,6 +433,7 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #endif
         if (nx) {
           prog = 1;
+#ifndef ORH_EXP_NO_LVL_STORE  // timing experiment only: drops the level bytes
           {
           uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
           if (level < kLvlDirect) {
@@ -438,6 +447,7 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
             }
           }
           }
+#endif
         }
 #ifdef ORH_DIAG_STAMPS
         t_store += __builtin_amdgcn_s_memtime() - t_s0;

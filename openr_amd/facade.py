@@ -17,7 +17,7 @@ from collections import namedtuple
 from typing import Iterable, List, Optional
 
 from .types import (AdjacencyDatabase, BinaryAddress, IpPrefix, NextHopThrift,
-                    PrefixEntry, RouteDb, UnicastRoute, nexthop_from_wire,
+                    PrefixEntry, RouteDb, RouteDbDelta, UnicastRoute, nexthop_from_wire,
                     prefix_entry_from_wire)
 
 LinkStateChange = namedtuple(
@@ -202,6 +202,14 @@ class Backend:
                    bgp_dry_run=False, enable_best_route_selection=False) -> SpfSolver:
         return SpfSolver(self.module, my_node, enable_v4, enable_ordered_fib,
                          bgp_dry_run, enable_best_route_selection)
+
+    def calculate_update(self, old_db: RouteDb, new_db: RouteDb) -> RouteDbDelta:
+        """DecisionRouteDb::calculateUpdate (Decision.cpp:108-143)."""
+        return RouteDbDelta.from_wire(self.module.calculate_update(old_db.wire, new_db.wire))
+
+    def apply_update(self, db: RouteDb, delta_wire) -> RouteDb:
+        """DecisionRouteDb::update (Decision.cpp:146-160)."""
+        return RouteDb.from_wire(self.module.apply_update(db.wire, delta_wire))
 
     def __repr__(self):
         return f"Backend({self.name})"

@@ -250,7 +250,9 @@ class RouteDb:
             hops = sorted((nexthop_from_wire(n) for n in nhs),
                           key=NextHopThrift.sort_key)
             mp[label] = MplsRoute(label, hops)
-        return RouteDb(uc, mp)
+        db = RouteDb(uc, mp)
+        db.wire = w  # the backend's own form, for calculate_update / apply_update
+        return db
 
     def canonical(self):
         """Comparable form: nexthops as sets (the reference compares
@@ -258,6 +260,33 @@ class RouteDb:
         return (
             {str(k): (v.nexthop_set(), v.doNotInstall) for k, v in self.unicastRoutes.items()},
             {k: v.nexthop_set() for k, v in self.mplsRoutes.items()},
+        )
+
+
+@dataclass
+class RouteDbDelta:
+    """DecisionRouteUpdate (openr/decision/RouteUpdate.h:23-41) as produced by
+    DecisionRouteDb::calculateUpdate (Decision.cpp:108-143); list order is
+    the backend's container order, so compare through canonical()."""
+    unicastRoutesToUpdate: dict
+    unicastRoutesToDelete: list
+    mplsRoutesToUpdate: dict
+    mplsRoutesToDelete: list
+
+    @staticmethod
+    def from_wire(w) -> "RouteDbDelta":
+        uu, ud, mu, md = w
+        upd = RouteDb.from_wire((uu, mu))
+        return RouteDbDelta(upd.unicastRoutes,
+                            [IpPrefix(BinaryAddress(a), l) for a, l in ud],
+                            upd.mplsRoutes, list(md))
+
+    def canonical(self):
+        return (
+            {str(k): (v.nexthop_set(), v.doNotInstall) for k, v in self.unicastRoutesToUpdate.items()},
+            sorted(str(p) for p in self.unicastRoutesToDelete),
+            {k: v.nexthop_set() for k, v in self.mplsRoutesToUpdate.items()},
+            sorted(self.mplsRoutesToDelete),
         )
 
 

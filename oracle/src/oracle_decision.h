@@ -44,14 +44,63 @@ struct RibUnicastEntry {  // RibEntry.h:38-99
   bool doNotInstall{false};
 };
 
+// RibEntry.h:65-69 (bestArea is not compared) and RibEntry.h:28-31
+inline bool operator==(const RibUnicastEntry& a, const RibUnicastEntry& b) {
+  if (!(a.prefix == b.prefix && a.doNotInstall == b.doNotInstall)) return false;
+  if (a.bestPrefixEntry.has_value() != b.bestPrefixEntry.has_value()) return false;
+  if (a.bestPrefixEntry && !(*a.bestPrefixEntry == *b.bestPrefixEntry)) return false;
+  return a.nexthops == b.nexthops;
+}
+
 struct RibMplsEntry {  // RibEntry.h:101-144
   int32_t label{0};
   NextHopSet nexthops;
 };
 
+inline bool operator==(const RibMplsEntry& a, const RibMplsEntry& b) {  // RibEntry.h:123-126
+  return a.label == b.label && a.nexthops == b.nexthops;
+}
+
+struct DecisionRouteUpdate {  // RouteUpdate.h:23-41
+  std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutesToUpdate;
+  std::vector<Cidr> unicastRoutesToDelete;
+  std::vector<RibMplsEntry> mplsRoutesToUpdate;
+  std::vector<int32_t> mplsRoutesToDelete;
+};
+
 struct DecisionRouteDb {  // Decision.h:78-119
   std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutes;
   std::unordered_map<int32_t, RibMplsEntry> mplsRoutes;
+
+  // Decision.cpp:108-143
+  DecisionRouteUpdate calculateUpdate(DecisionRouteDb&& newDb) const {
+    DecisionRouteUpdate delta;
+    for (auto& kv : newDb.unicastRoutes) {
+      auto search = unicastRoutes.find(kv.first);
+      if (search == unicastRoutes.end() || !(search->second == kv.second)) {
+        auto key = kv.second.prefix;
+        delta.unicastRoutesToUpdate.emplace(std::move(key), std::move(kv.second));
+      }
+    }
+    for (auto& kv : unicastRoutes)
+      if (!newDb.unicastRoutes.count(kv.first)) delta.unicastRoutesToDelete.emplace_back(kv.first);
+    for (const auto& kv : newDb.mplsRoutes) {
+      auto search = mplsRoutes.find(kv.first);
+      if (search == mplsRoutes.end() || !(search->second == kv.second))
+        delta.mplsRoutesToUpdate.emplace_back(kv.second);
+    }
+    for (const auto& kv : mplsRoutes)
+      if (!newDb.mplsRoutes.count(kv.first)) delta.mplsRoutesToDelete.emplace_back(kv.first);
+    return delta;
+  }
+
+  // Decision.cpp:146-160
+  void update(const DecisionRouteUpdate& u) {
+    for (const auto& prefix : u.unicastRoutesToDelete) unicastRoutes.erase(prefix);
+    for (const auto& kv : u.unicastRoutesToUpdate) unicastRoutes.insert_or_assign(kv.second.prefix, kv.second);
+    for (auto label : u.mplsRoutesToDelete) mplsRoutes.erase(label);
+    for (const auto& e : u.mplsRoutesToUpdate) mplsRoutes.insert_or_assign(e.label, e);
+  }
 };
 
 struct BestRouteSelectionResult {  // Decision.h:51-76

@@ -139,6 +139,59 @@ py::tuple routeDbToWire(const DecisionRouteDb& db) {
   return py::make_tuple(uc, mp);
 }
 
+RibUnicastEntry unicastFromWire(const py::tuple& t) {
+  RibUnicastEntry e;
+  e.prefix = {bytesOf(t[0]), t[1].cast<int32_t>()};
+  for (auto nh : t[2]) e.nexthops.insert(nhFromWire(nh.cast<py::tuple>()));
+  e.doNotInstall = t[3].cast<bool>();
+  e.bestArea = t[4].cast<std::string>();
+  if (!t[5].is_none()) e.bestPrefixEntry = entryFromWire(t[5].cast<py::tuple>());
+  return e;
+}
+
+RibMplsEntry mplsFromWire(const py::tuple& t) {
+  RibMplsEntry e;
+  e.label = t[0].cast<int32_t>();
+  for (auto nh : t[1]) e.nexthops.insert(nhFromWire(nh.cast<py::tuple>()));
+  return e;
+}
+
+DecisionRouteDb routeDbFromWire(const py::tuple& w) {
+  DecisionRouteDb db;
+  for (auto u : w[0]) {
+    auto e = unicastFromWire(u.cast<py::tuple>());
+    db.unicastRoutes.emplace(e.prefix, e);
+  }
+  for (auto m : w[1]) {
+    auto e = mplsFromWire(m.cast<py::tuple>());
+    db.mplsRoutes.emplace(e.label, e);
+  }
+  return db;
+}
+
+py::tuple deltaToWire(const DecisionRouteUpdate& d) {
+  py::list uu, ud, mu;
+  for (const auto& kv : d.unicastRoutesToUpdate) uu.append(unicastToWire(kv.second));
+  for (const auto& p : d.unicastRoutesToDelete) ud.append(py::make_tuple(py::bytes(p.first), p.second));
+  for (const auto& e : d.mplsRoutesToUpdate) mu.append(py::make_tuple(e.label, nhsToWire(e.nexthops)));
+  return py::make_tuple(uu, ud, mu, py::cast(d.mplsRoutesToDelete));
+}
+
+DecisionRouteUpdate deltaFromWire(const py::tuple& w) {
+  DecisionRouteUpdate d;
+  for (auto u : w[0]) {
+    auto e = unicastFromWire(u.cast<py::tuple>());
+    d.unicastRoutesToUpdate.emplace(e.prefix, e);
+  }
+  for (auto p : w[1]) {
+    auto t = p.cast<py::tuple>();
+    d.unicastRoutesToDelete.emplace_back(bytesOf(t[0]), t[1].cast<int32_t>());
+  }
+  for (auto m : w[2]) d.mplsRoutesToUpdate.push_back(mplsFromWire(m.cast<py::tuple>()));
+  d.mplsRoutesToDelete = w[3].cast<std::vector<int32_t>>();
+  return d;
+}
+
 py::tuple changeToWire(const LinkStateChange& c) {
   return py::make_tuple(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged);
 }
@@ -163,6 +216,14 @@ struct AreaMap {
 }  // namespace
 
 PYBIND11_MODULE(openr_oracle, m) {
+  m.def("calculate_update", [](py::tuple old_db, py::tuple new_db) {
+    return deltaToWire(routeDbFromWire(old_db).calculateUpdate(routeDbFromWire(new_db)));
+  });
+  m.def("apply_update", [](py::tuple db, py::tuple delta) {
+    DecisionRouteDb d = routeDbFromWire(db);
+    d.update(deltaFromWire(delta));
+    return routeDbToWire(d);
+  });
   m.doc() = "CPU oracle (test infrastructure): restatement of the OpenR Decision SPF / route build";
 
   py::class_<LinkState>(m, "LinkState")
