@@ -155,14 +155,22 @@ std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::
   Cidr key{e.addr, e.len};
   auto [it, inserted] = prefixes_[key].emplace(NodeAndArea{node, area}, e);
   if (!inserted && it->second == e) return {};
-  if (!inserted) it->second = e;
+  if (!inserted) {
+    ksp2Entries_ -= it->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+    it->second = e;
+  }
+  ksp2Entries_ += e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
   return {key};
 }
 
 std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::string& area,
                                             const Cidr& prefix) {
   auto it = prefixes_.find(prefix);
-  if (it == prefixes_.end() || !it->second.erase(NodeAndArea{node, area})) return {};
+  if (it == prefixes_.end()) return {};
+  auto e = it->second.find(NodeAndArea{node, area});
+  if (e == it->second.end()) return {};
+  ksp2Entries_ -= e->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+  it->second.erase(e);
   if (it->second.empty()) prefixes_.erase(it);
   return {prefix};
 }
@@ -208,17 +216,25 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
   // Decision.cpp:445-613
   auto search = ps.prefixes().find(prefix);
   if (search == ps.prefixes().end()) return std::nullopt;
-  PrefixEntries entries = search->second;
+  // advertisers unreachable in their own area are dropped (:468-480); the
+  // entries are copied only when one is
+  const PrefixEntries* ep = &search->second;
+  PrefixEntries kept;
   for (const auto& [area, ls] : als) {
     const SpfRow& row = ls.getSpfResult(me);
-    for (auto it = entries.begin(); it != entries.end();) {
+    for (auto it = ep->begin(); it != ep->end();) {
       if (area != it->first.second || rowHas(ls, row, it->first.first)) {
         ++it;
+      } else if (ep != &kept) {
+        kept = *ep;
+        ep = &kept;
+        it = kept.begin();  // restart on the copy
       } else {
-        it = entries.erase(it);
+        it = kept.erase(it);
       }
     }
   }
+  const PrefixEntries& entries = *ep;
   if (entries.empty()) return std::nullopt;
   if (prefix.first.size() == 4 && !enableV4_) return std::nullopt;
 
@@ -260,7 +276,11 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
 
 BestRouteSelectionResult SpfSolver::filterDrained(BestRouteSelectionResult&& r,
                                                   const AreaLinkStates& als) const {
-  BestRouteSelectionResult f = r;  // maybeFilterDrainedNodes, Decision.cpp:840-862
+  // maybeFilterDrainedNodes, Decision.cpp:840-862
+  bool anyDrained = false;
+  for (const auto& na : r.allNodeAreas) anyDrained |= als.at(na.second).isNodeOverloaded(na.first);
+  if (!anyDrained) return std::move(r);
+  BestRouteSelectionResult f = r;
   for (auto it = f.allNodeAreas.begin(); it != f.allNodeAreas.end();) {
     if (als.at(it->second).isNodeOverloaded(it->first)) {
       it = f.allNodeAreas.erase(it);
@@ -464,15 +484,19 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsSpf(
   // Decision.cpp:904-963
   const bool isV4 = prefix.first.size() == 4;
   const bool perDst = ft == kFwdSrMpls;
-  auto filtered = r.allNodeAreas;
+  std::set<NodeAndArea> filteredCopy;
+  const std::set<NodeAndArea>* fp = &r.allNodeAreas;
   if (r.hasNode(me) && perDst) {
     for (const auto& [na, e] : entries) {
       if (na.first == me && e.prependLabel) {
-        filtered.erase(na);
+        filteredCopy = r.allNodeAreas;
+        filteredCopy.erase(na);
+        fp = &filteredCopy;
         break;
       }
     }
   }
+  const std::set<NodeAndArea>& filtered = *fp;
   if (!perDst && als.size() == 1) {
     const auto& [area, ls] = *als.begin();
     if (ls.nodeId(me)) {
@@ -598,7 +622,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // route build with the same paths and the same spf_runs count)
   RouteProf prof;
   bool hasKsp = false;
-  {
+  if (ps.ksp2Entries() > 0) {
     std::unordered_map<const LinkState*, std::vector<std::pair<std::string, std::string>>> plan;
     kspPlan_ = &plan;
     try {
@@ -631,18 +655,22 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   for (const auto& [prefix, _] : ps.prefixes()) keys.push_back(&prefix);
   auto& pool = WorkerPool::instance();
   if (!hasKsp && keys.size() >= kParallelMin && pool.size() > 1) {
-    std::vector<std::vector<RibUnicastEntry>> parts(pool.size());
+    // each worker fills a map of the output type; the merge splices nodes
+    // (no entry is copied or moved)
+    std::vector<decltype(db.unicastRoutes)> parts(pool.size());
     pool.parallelFor(keys.size(), [&](size_t w, size_t b, size_t e) {
+      parts[w].reserve(parts[w].size() + (e - b));
       for (size_t i = b; i < e; ++i)
-        if (auto r = createRouteForPrefix(me, als, ps, *keys[i])) parts[w].push_back(std::move(*r));
+        if (auto r = createRouteForPrefix(me, als, ps, *keys[i])) {
+          Cidr k = r->prefix;
+          parts[w].emplace(std::move(k), std::move(*r));
+        }
     });
     prof.mark("unicast (pool)");
-    for (auto& part : parts)
-      for (auto& r : part) {
-        Cidr k = r.prefix;
-        if (!db.unicastRoutes.emplace(std::move(k), std::move(r)).second)
-          throw std::logic_error("duplicate unicast route");
-      }
+    for (auto& part : parts) {
+      db.unicastRoutes.merge(part);
+      if (!part.empty()) throw std::logic_error("duplicate unicast route");
+    }
   } else {
     for (const Cidr* prefix : keys) {
       if (auto r = createRouteForPrefix(me, als, ps, *prefix)) {
@@ -716,6 +744,11 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       if (!cand[i]) continue;
       if (lt != labelToNode.end()) labelToNode.erase(lt);
       win[label] = {&adjDb.thisNodeName, i};
+    }
+    if (als.size() == 1) {  // one area: the winners are the routes
+      db.mplsRoutes.reserve(win.size() + 64);
+      for (auto& [label, w] : win) db.mplsRoutes.emplace(label, std::move(*cand[w.second]));
+      continue;
     }
     for (auto& [label, w] : win)
       labelToNode.emplace(label, std::make_pair(*w.first, std::move(*cand[w.second])));

@@ -25,9 +25,13 @@ class PrefixState {
   std::vector<Cidr> deletePrefix(const std::string& node, const std::string& area,
                                  const Cidr& prefix);
   const std::unordered_map<Cidr, PrefixEntries, CidrHash>& prefixes() const { return prefixes_; }
+  // advertisements with forwardingAlgorithm KSP2_ED_ECMP (lets buildRouteDb
+  // skip its KSP2 planning pass when there are none)
+  size_t ksp2Entries() const { return ksp2Entries_; }
 
  private:
   std::unordered_map<Cidr, PrefixEntries, CidrHash> prefixes_;
+  size_t ksp2Entries_{0};
 };
 
 // unordered_map<string, LinkState>; nodes are stable so LinkState can stay
