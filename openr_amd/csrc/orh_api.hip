@@ -22,6 +22,10 @@ struct orh_ctx {
   hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;  // around phase 1 | phase 2
   size_t lds_limit = 160 * 1024;
   orh::SpfMode spf_mode = orh::SpfMode::kAuto;  // orh_set_spf_mode
+  // ORH_DELTA_PCT: HBM-kernel near/far width in % of the mean live metric;
+  // 50 measured best on the C4 WAN what-if batch (25: 12.4, 50: 11.9,
+  // 100: 13.1, 200: 17.0, 400: 23.6 ms; log-normal metrics, mean ~3x median)
+  uint32_t delta_pct = 50;
   std::string err;
   orh_counters counters{};
   // reusable device staging for request arrays, keyed by the request that
@@ -378,6 +382,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
     return ORH_E_DEVICE;
   }
   if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % orh::kSpfModes);
+  if (const char* e = getenv("ORH_DELTA_PCT")) ctx->delta_pct = std::max(1, atoi(e));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
@@ -803,7 +808,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.w0 = w0;
   // near/far width of the HBM kernel: the mean live metric (one BFS level
   // when metrics are uniform)
-  a.delta = uniform ? w0 : std::max<uint32_t>(1u, g->mean_out);
+  a.delta = uniform ? w0
+                    : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                 static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
   a.out_dist = d_dist;
   a.scratch = ctx->d_scratch;
   a.labels = ctx->d_labels;
