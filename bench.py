@@ -208,7 +208,7 @@ def main():
     barrier()
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v5_pmc.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v6_pmc.json")
 SWEEP_KERNELS = ("spf_msbfs_kernel", "ms_finalize_kernel", "first_hop_lvl_kernel")
 
 
