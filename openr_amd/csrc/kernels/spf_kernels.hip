@@ -1146,6 +1146,22 @@ __device__ inline bool has_byte_fe(uint32_t x) {  // some byte == kLvlDirect
   return ((z - 0x01010101u) & ~z & 0x80808080u) != 0u;
 }
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the
+// 8 XCDs (block b -> XCD b % 8), each with its own L2. Remapped, XCD x runs a
+// contiguous range of logical blocks, so the sources resident on one XCD at a
+// time are neighbours in row order and share their neighbours' level rows in
+// that XCD's L2 instead of each XCD fetching them from HBM. Bijective for any
+// grid size.
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
+#ifdef ORH_NO_XCD_REMAP
+  return b;
+#else
+  constexpr uint32_t kXcd = 8;
+  const uint32_t x = b % kXcd, k = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+#endif
+}
+
 // One workgroup per (source, tile phase): the source's tight first links are
 // gathered once, then the workgroup walks tiles phase, phase + split, ...
 template <uint32_t kLvlPer>
@@ -1157,7 +1173,8 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
   const uint32_t N = a.n_nodes, P = a.lvl_pitch, w0 = a.w0;
   const uint32_t tid = threadIdx.x;
   const uint32_t split = a.tile_split;
-  const uint32_t i = blockIdx.x / split, phase = blockIdx.x % split;
+  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t i = blk / split, phase = blk % split;
   const uint32_t src = a.srcs[i];
   const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
   const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
