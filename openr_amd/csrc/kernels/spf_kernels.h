@@ -75,6 +75,9 @@ struct HopArgs {
   const uint8_t* lvl_rows;
   uint32_t lvl_pitch;
   uint32_t w0;
+  // level-row kernel block order: 0 = one contiguous source range per XCD,
+  // G > 0 = runs of G consecutive blocks dealt round-robin over the XCDs
+  uint32_t xcd_group;
 };
 
 enum class SpfVariant {

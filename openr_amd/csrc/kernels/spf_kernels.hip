@@ -1152,14 +1152,18 @@ __device__ inline bool has_byte_fe(uint32_t x) {  // some byte == kLvlDirect
 // time are neighbours in row order and share their neighbours' level rows in
 // that XCD's L2 instead of each XCD fetching them from HBM. Bijective for any
 // grid size.
-__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
-#ifdef ORH_NO_XCD_REMAP
-  return b;
-#else
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t group) {
   constexpr uint32_t kXcd = 8;
-  const uint32_t x = b % kXcd, k = b / kXcd, q = nb / kXcd, r = nb % kXcd;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-#endif
+  if (group == 0) {  // one contiguous range per XCD
+    const uint32_t x = b % kXcd, k = b / kXcd, q = nb / kXcd, r = nb % kXcd;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  // runs of `group` consecutive blocks per XCD, dealt round-robin; the tail
+  // that does not fill a whole round keeps its order
+  const uint32_t full = nb / (kXcd * group) * (kXcd * group);
+  if (b >= full) return b;
+  const uint32_t x = b % kXcd, k = b / kXcd;
+  return ((k / group) * kXcd + x) * group + k % group;
 }
 
 // One workgroup per (source, tile phase): the source's tight first links are
@@ -1173,7 +1177,7 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
   const uint32_t N = a.n_nodes, P = a.lvl_pitch, w0 = a.w0;
   const uint32_t tid = threadIdx.x;
   const uint32_t split = a.tile_split;
-  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, a.xcd_group);
   const uint32_t i = blk / split, phase = blk % split;
   const uint32_t src = a.srcs[i];
   const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
