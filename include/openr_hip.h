@@ -124,6 +124,25 @@ int orh_reset_counters(orh_ctx* ctx);
 #define ORH_SPF_GLOBAL 2
 #define ORH_SPF_GLOBAL_TWO_PHASE 3
 int orh_set_spf_mode(orh_ctx* ctx, int mode);
+/* kernel plan of the last orh_spf_run on this context (tests and profiling
+ * assert which variant ran; results never depend on it) */
+#define ORH_VARIANT_MSBFS 1     /* bit-parallel multi-source BFS */
+#define ORH_VARIANT_BFS8 2      /* per-source BFS, u8 / u16 / u32 levels in LDS */
+#define ORH_VARIANT_BFS16 3
+#define ORH_VARIANT_BFS32 4
+#define ORH_VARIANT_DIST16 5    /* per-source level-synchronous Dijkstra in LDS */
+#define ORH_VARIANT_DIST32 6
+#define ORH_VARIANT_GLOBAL 7    /* HBM frontier kernel, two-phase */
+#define ORH_VARIANT_GLOBAL_NH 8 /* HBM frontier kernel with fused first hops */
+typedef struct orh_spf_info {
+  int32_t variant;     /* ORH_VARIANT_* of the distance phase */
+  uint32_t rows;       /* distance rows searched (sources + neighbour rows) */
+  uint32_t mask_bits;  /* MS-BFS: sources per workgroup (32 or 16), else 0 */
+  uint32_t hop_nodes;  /* first-hop phase: nodes per thread over u8 level rows
+                          (16 or 4), 1 for the u32-row kernel, 0 when fused */
+  uint32_t hop_split;  /* first-hop phase: workgroups per source */
+} orh_spf_info;
+int orh_last_spf_info(const orh_ctx* ctx, orh_spf_info* out);
 /* device time (HIP events on the context stream) of the last orh_spf_run;
  * waits for that launch to finish */
 int orh_last_spf_ms(orh_ctx* ctx, double* ms_out);

@@ -7,7 +7,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 
+#include "parallel.h"
 #include "rib_policy.h"
 #include "spf_solver.h"
 
@@ -332,6 +334,17 @@ class SpfSweep {
   void sync() {
     if (orh_sync(ctx_) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
   }
+  py::dict info() const {  // kernel plan of the context's last run (orh_last_spf_info)
+    orh_spf_info i{};
+    orh_last_spf_info(ctx_, &i);
+    py::dict d;
+    d["variant"] = i.variant;
+    d["rows"] = i.rows;
+    d["mask_bits"] = i.mask_bits;
+    d["hop_nodes"] = i.hop_nodes;
+    d["hop_split"] = i.hop_split;
+    return d;
+  }
   py::tuple fetch(size_t i) {
     if (i >= srcs_.size()) throw std::out_of_range("SpfSweep.fetch");
     py::array_t<uint32_t> dist(n_), nh(static_cast<size_t>(n_) * words_);
@@ -364,6 +377,139 @@ class SpfSweep {
   uint32_t* dDist_{nullptr};
   uint32_t* dNh_{nullptr};
 };
+
+// ---- canonical route-db digest --------------------------------------------
+// Per route: fields serialised in order (integers little-endian, strings and
+// lists length-prefixed, optionals with a presence byte, nexthops sorted by
+// their serialised bytes; PrefixEntry.tags is not part of it), hashed with
+// FNV-1a 64. Routes in (prefix bytes, length) order, then labels. Lets a
+// caller compare full-size route databases (C3, C5) without materialising
+// them in Python.
+class DigestWriter {
+ public:
+  std::string b;
+  void raw(const void* p, size_t n) { b.append(static_cast<const char*>(p), n); }
+  void u8(uint8_t v) { raw(&v, 1); }
+  void i32(int32_t v) { raw(&v, 4); }
+  void i64(int64_t v) { raw(&v, 8); }
+  void str(const std::string& s) {
+    i32(static_cast<int32_t>(s.size()));
+    raw(s.data(), s.size());
+  }
+  void optStr(const std::optional<std::string>& o) {
+    u8(o ? 1 : 0);
+    if (o) str(*o);
+  }
+  void optI32(const std::optional<int32_t>& o) {
+    u8(o ? 1 : 0);
+    if (o) i32(*o);
+  }
+};
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+std::string nexthopBytes(const NextHopThrift& nh) {
+  DigestWriter w;
+  w.str(nh.address.addr);
+  w.optStr(nh.address.ifName);
+  w.i32(nh.weight);
+  w.u8(nh.mplsAction ? 1 : 0);
+  if (nh.mplsAction) {
+    w.i32(nh.mplsAction->action);
+    w.optI32(nh.mplsAction->swapLabel);
+    w.u8(nh.mplsAction->pushLabels ? 1 : 0);
+    if (nh.mplsAction->pushLabels) {
+      w.i32(static_cast<int32_t>(nh.mplsAction->pushLabels->size()));
+      for (int32_t l : *nh.mplsAction->pushLabels) w.i32(l);
+    }
+  }
+  w.i32(nh.metric);
+  w.optStr(nh.area);
+  w.optStr(nh.neighborNodeName);
+  return w.b;
+}
+
+void writeNexthops(DigestWriter& w, const NextHopSet& nhs) {
+  std::vector<std::string> v;
+  v.reserve(nhs.size());
+  for (const auto& nh : nhs) v.push_back(nexthopBytes(nh));
+  std::sort(v.begin(), v.end());
+  w.i32(static_cast<int32_t>(v.size()));
+  for (const auto& x : v) w.str(x);
+}
+
+void writeEntry(DigestWriter& w, const PrefixEntry& e) {
+  w.str(e.addr);
+  w.i32(e.len);
+  w.i32(e.type);
+  w.i32(e.forwardingType);
+  w.i32(e.forwardingAlgorithm);
+  w.u8(e.minNexthop ? 1 : 0);
+  if (e.minNexthop) w.i64(*e.minNexthop);
+  w.optI32(e.prependLabel);
+  w.i32(e.pathPreference);
+  w.i32(e.sourcePreference);
+  w.i32(e.distance);
+  w.u8(e.mv ? 1 : 0);
+  if (e.mv) {
+    w.i64(e.mv->version);
+    w.i32(static_cast<int32_t>(e.mv->metrics.size()));
+    for (const auto& m : e.mv->metrics) {
+      w.i64(m.type);
+      w.i64(m.priority);
+      w.i32(m.op);
+      w.u8(m.isBestPathTieBreaker ? 1 : 0);
+      w.i32(static_cast<int32_t>(m.metric.size()));
+      for (int64_t x : m.metric) w.i64(x);
+    }
+  }
+  w.optStr(e.data);
+}
+
+py::tuple routeDbDigest(const DecisionRouteDb& db) {
+  std::vector<const RibUnicastEntry*> uc;
+  uc.reserve(db.unicastRoutes.size());
+  for (const auto& kv : db.unicastRoutes) uc.push_back(&kv.second);
+  std::sort(uc.begin(), uc.end(),
+            [](const RibUnicastEntry* a, const RibUnicastEntry* b) { return a->prefix < b->prefix; });
+  std::vector<const RibMplsEntry*> mp;
+  for (const auto& kv : db.mplsRoutes) mp.push_back(&kv.second);
+  std::sort(mp.begin(), mp.end(),
+            [](const RibMplsEntry* a, const RibMplsEntry* b) { return a->label < b->label; });
+  std::string out(8 * (uc.size() + mp.size()), '\0');
+  auto put = [&](size_t i, const std::string& bytes) {
+    const uint64_t h = fnv1a(bytes);
+    std::memcpy(&out[8 * i], &h, 8);
+  };
+  auto& pool = WorkerPool::instance();
+  pool.parallelFor(uc.size(), [&](size_t, size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      DigestWriter w;
+      w.str(uc[i]->prefix.first);
+      w.i32(uc[i]->prefix.second);
+      w.u8(uc[i]->doNotInstall ? 1 : 0);
+      w.str(uc[i]->bestArea);
+      w.u8(uc[i]->bestPrefixEntry ? 1 : 0);
+      if (uc[i]->bestPrefixEntry) writeEntry(w, *uc[i]->bestPrefixEntry);
+      writeNexthops(w, uc[i]->nexthops);
+      put(i, w.b);
+    }
+  });
+  for (size_t i = 0; i < mp.size(); ++i) {
+    DigestWriter w;
+    w.i32(mp[i]->label);
+    writeNexthops(w, mp[i]->nexthops);
+    put(uc.size() + i, w.b);
+  }
+  return py::make_tuple(uc.size(), mp.size(), py::bytes(out));
+}
 
 struct RibStatementProbe {  // a lone RibPolicyStatement (RibPolicyTest.cpp statement tests)
   RibPolicyStatement st;
@@ -448,6 +594,19 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              throw std::out_of_range("no such link");
            })
+      .def("neighbors",  // distinct neighbours of src in first-hop bit order (orh_graph_neighbors)
+           [](const LinkState& s, const std::string& src) {
+             auto id = s.nodeId(src);
+             if (!id) throw std::invalid_argument("neighbors: unknown node " + src);
+             orh_graph* g = s.deviceGraph();
+             uint32_t n = 0;
+             orh_graph_neighbors(g, *id, nullptr, 0, &n);
+             std::vector<uint32_t> ids(n);
+             orh_graph_neighbors(g, *id, ids.data(), n, &n);
+             std::vector<std::string> out;
+             for (uint32_t v : ids) out.push_back(s.nodeName(v));
+             return out;
+           })
       .def("node_names",
            [](const LinkState& s) {
              std::vector<std::string> v;
@@ -515,6 +674,7 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("last_ms", &SpfSweep::lastMs)
       .def("phase_ms", &SpfSweep::phaseMs)
       .def("sync", &SpfSweep::sync)
+      .def("info", &SpfSweep::info)
       .def("fetch", &SpfSweep::fetch)
       .def("copy_to", &SpfSweep::copyTo, py::arg("dist_ptr"), py::arg("nh_ptr"))
       .def_property_readonly("words", &SpfSweep::words)
@@ -588,6 +748,13 @@ PYBIND11_MODULE(_openr_host, m) {
              auto db = s.buildRouteDb(me, als.m, ps);
              if (!db) return py::none();
              return routeDbToWire(*db);
+           })
+      .def("build_route_db_digest",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als,
+              const PrefixState& ps) -> py::object {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             if (!db) return py::none();
+             return routeDbDigest(*db);
            })
       .def("time_build_route_db",
            [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps) {

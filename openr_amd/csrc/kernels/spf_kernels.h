@@ -115,7 +115,10 @@ size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
 
 // LDS bytes the first-hop kernel needs for max_nbr distinct neighbours
 size_t hop_lds_bytes(uint32_t max_nbr);
-hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s);
+// *nodes_per_thread / *split receive the chosen kernel shape (16 or 4 nodes
+// per thread over level rows, 1 for u32 rows)
+hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s,
+                            uint32_t* nodes_per_thread = nullptr, uint32_t* split = nullptr);
 // multi-source BFS plans, phase 2a: node-major level bytes -> requested dist
 // rows (host order) and u8 level rows of every row (a.lvl_rows), which the
 // first-hop phase reads instead of u32 distance rows
@@ -132,5 +135,8 @@ struct RouteSelectArgs {
   uint32_t* nh_out;
 };
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s);
+// recs[pos[i]] = vals[i] for i < n (device pointers)
+hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* vals, uint32_t n,
+                               hipStream_t s);
 
 }  // namespace orh

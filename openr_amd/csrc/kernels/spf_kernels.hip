@@ -187,7 +187,7 @@ struct Bfs {
 template <int K, class L>
 __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t s_any[2];
+  __shared__ uint32_t s_any[3];
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
   const uint32_t lwords = a.lds_pend_off / 4;
   for (uint32_t i = tid; i < lwords; i += nthr) lds[i] = 0xFFFFFFFFu;
   for (uint32_t i = tid; i < 2 * NB; i += nthr) f0[i] = 0u;
-  if (tid < 2) s_any[tid] = 0u;
+  if (tid < 3) s_any[tid] = 0u;
   __syncthreads();
   if (tid == 0) {
     lvl[s.node] = 0;
@@ -212,7 +212,6 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
     const uint32_t par = level & 1u;
     uint32_t* cur = par ? f1 : f0;
     const Bfs<K, L> b{a, s, lvl, par ? f0 : f1, static_cast<L>(level + 1)};
-    if (tid == 0) s_any[par ^ 1u] = 0u;  // next level's flag, read one level ago
     bool pushed = false;
     // a thread owns frontier words w and w + nthr: their nodes' records go
     // out in one batch
@@ -242,12 +241,18 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
           if (i < cnt) pushed |= b.expand(vs[i], r[i]);
       }
     }
-    if (pushed) s_any[par] = 1u;
+    // exit flags rotate over three slots: level L writes and reads slot L%3
+    // around its barrier; the reset of slot (L+2)%3 = (L-1)%3 happens after
+    // barrier L, when every wave has read that slot (right after barrier
+    // L-1), and before barrier L+1, which every writer of level L+2 passes
+    const uint32_t slot = level % 3u;
+    if (pushed) s_any[slot] = 1u;
     __syncthreads();
     // every level expands >= 1 node and levels stay below the type's
     // all-ones (the planner picks L with N - 1 < kInfL), so the loop ends
     // and every wave reaches the exit
-    if (!s_any[par] || level >= N) break;
+    if (!s_any[slot] || level >= N) break;
+    if (tid == 0) s_any[(level + 2u) % 3u] = 0u;
   }
   uint32_t* out = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
   const uint32_t w0 = a.w0;
@@ -509,7 +514,12 @@ __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t ti
     s_out[threadIdx.x] = dist_row(a.out_dist, a.scratch, a.n_out, N, s_row[threadIdx.x]);
   }
   __syncthreads();
-  if (i >= N) return;
+  if (i >= N) {  // level-row padding [N, pitch): "unreached" for the 16-byte reads
+    if (i < a.lvl_pitch)
+      for (uint32_t b = 0; b < S; ++b)
+        a.lvl_rows[static_cast<size_t>(s_row[b]) * a.lvl_pitch + i] = static_cast<uint8_t>(kLvlNone);
+    return;
+  }
   const uint32_t v = a.dev_of[i];
   const uint4* blk = reinterpret_cast<const uint4*>(a.ms_lvl + (static_cast<size_t>(batch) * N + v) * kS);
   uint32_t w[kS / 4];
@@ -638,7 +648,7 @@ template <class T, int K>
 __global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
   using DW = DistWord<T>;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t s_min[2];
+  __shared__ uint32_t s_min[3];
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
@@ -650,7 +660,7 @@ __global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
   const uint32_t dwords = a.lds_pend_off / 4;
   for (uint32_t i = tid; i < dwords; i += nthr) dist[i] = 0xFFFFFFFFu;
   for (uint32_t i = tid; i < NB; i += nthr) pend[i] = 0u;
-  if (tid < 2) s_min[tid] = kInf;
+  if (tid < 3) s_min[tid] = kInf;
   __syncthreads();
   if (tid == 0) {
     bool first;
@@ -663,8 +673,7 @@ __global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
   constexpr int kScan = 8;  // pending distances read together
   uint32_t D = 0;
   for (uint32_t level = 0;; ++level) {
-    const uint32_t par = level & 1u;
-    if (tid == 0) s_min[par ^ 1u] = kInf;  // next level's slot, read one level ago
+    const uint32_t slot = level % 3u;  // rotation as in spf_bfs_kernel
     uint32_t local_min = kInf;
     for (uint32_t w = tid; w < NB; w += 2 * nthr) {
       const uint32_t w2 = w + nthr;
@@ -716,10 +725,11 @@ __global__ __launch_bounds__(kMaxBlock) void spf_dist_kernel(SpfArgs a) {
       }
     }
     const uint32_t wm = wave_min(local_min);
-    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[par], wm);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[slot], wm);
     __syncthreads();
-    const uint32_t next = s_min[par];
+    const uint32_t next = s_min[slot];
     if (next == kInf || level >= N) break;
+    if (tid == 0) s_min[(level + 2u) % 3u] = kInf;  // read before this barrier by every wave
     D = next;
   }
 
@@ -1212,11 +1222,12 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
     uint32_t dv[kLvlPer], ls[kLvlPer];
 #pragma unroll
     for (uint32_t k = 0; k < kLvlPer; ++k) {
-      dv[k] = dist_at(i, own, k);
-      ls[k] = LvlVec<kLvlPer>::byte(own, k);
       if (v0 + k == src || v0 + k >= N) {  // the source has no next hops
         dv[k] = kInf;
         ls[k] = kLvlNone;
+      } else {
+        dv[k] = dist_at(i, own, k);
+        ls[k] = LvlVec<kLvlPer>::byte(own, k);
       }
     }
     for (uint32_t word = 0; word < W; ++word) {
@@ -1464,7 +1475,8 @@ size_t hop_lds_bytes(uint32_t max_nbr) {
   return static_cast<size_t>((2 * max_nbr + 3) & ~3u) * 4 + static_cast<size_t>(max_nbr) * 16;
 }
 
-hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s) {
+hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t* nodes_per_thread,
+                            uint32_t* split) {
   if (a.n_out == 0) return hipSuccess;
   a.tiles = (a.n_nodes + kBlock * kHopPer - 1) / (kBlock * kHopPer);
   const uint64_t grid = static_cast<uint64_t>(a.tiles) * a.n_out;
@@ -1481,9 +1493,13 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s) {
     while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;
     const uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
     if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (nodes_per_thread) *nodes_per_thread = wide ? 16 : 4;
+    if (split) *split = a.tile_split;
     return wide ? launch(first_hop_lvl_kernel<16>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
                 : launch(first_hop_lvl_kernel<4>, a, static_cast<uint32_t>(g2), kBlock, lds, s);
   }
+  if (nodes_per_thread) *nodes_per_thread = 1;
+  if (split) *split = a.tiles;
   return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock, lds, s);
 }
 
@@ -1497,6 +1513,21 @@ hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, h
     hipLaunchKernelGGL(ms_finalize_kernel<uint16_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
   else
     hipLaunchKernelGGL(ms_finalize_kernel<uint32_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
+  return hipGetLastError();
+}
+
+// in-place mirror patch: recs[pos[i]] = vals[i] (one launch per delta batch)
+__global__ __launch_bounds__(kBlock) void scatter_recs_kernel(uint2* recs, const uint32_t* pos,
+                                                             const uint2* vals, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) recs[pos[i]] = vals[i];
+}
+
+hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* vals, uint32_t n,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_recs_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, recs,
+                     pos, vals, n);
   return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -27,6 +28,7 @@ struct orh_ctx {
   // 100: 13.1, 200: 17.0, 400: 23.6 ms; log-normal metrics, mean ~3x median)
   uint32_t delta_pct = 50;
   uint32_t req_xcd_group = 0;  // HopArgs::xcd_group of the staged request
+  orh_spf_info last_info{};    // orh_last_spf_info
   std::string err;
   orh_counters counters{};
   // reusable device staging for request arrays, keyed by the request that
@@ -50,11 +52,17 @@ struct orh_ctx {
   // costs more than a single-source SPF)
   uint32_t* d_batch = nullptr;
   size_t d_batch_cap = 0;  // in u32
+  // mirror-patch staging (positions + records of one delta batch)
+  uint32_t* d_patch = nullptr;
+  size_t d_patch_cap = 0;  // in u32
 };
 
 struct orh_graph {
   orh_ctx* ctx = nullptr;
-  uint64_t gen = 0;  // bumped on every structural load
+  // process-wide unique id of the uploaded structure (new on every load), so
+  // a context's staged request can never match a different or reloaded graph
+  // even when a new orh_graph reuses a freed one's address
+  uint64_t gen = 0;
   uint32_t n_nodes = 0, n_edges = 0, n_links = 0;
   // host CSR (ABI semantics) kept for deltas, neighbour tables and bounds
   std::vector<uint32_t> row_ptr, col, w_out, w_in, meta;
@@ -265,11 +273,38 @@ int sync_ms_layout(orh_graph* g) {
   return ORH_OK;
 }
 
-int upload_record(orh_graph* g, uint32_t v, uint32_t e) {
-  const uint2 r = device_record(g, v, e);
-  ORH_HIP(g->ctx, hipMemcpyAsync(g->d_recs + g->pos[e], &r, sizeof(uint2),
-                                 hipMemcpyHostToDevice, g->ctx->stream));
-  ORH_HIP(g->ctx, hipStreamSynchronize(g->ctx->stream));  // r lives on this stack frame
+uint64_t next_graph_gen() {
+  static std::atomic<uint64_t> gen{0};
+  return ++gen;
+}
+
+// re-upload the device records of CSR entries `edges` (row node, entry) with
+// one staging copy and one scatter launch
+int upload_records(orh_graph* g, const std::vector<std::pair<uint32_t, uint32_t>>& edges) {
+  if (edges.empty()) return ORH_OK;
+  orh_ctx* ctx = g->ctx;
+  const uint32_t n = static_cast<uint32_t>(edges.size());
+  // staging: pos[n] (u32, padded to 8 bytes) | vals[n] (uint2)
+  const size_t pos_words = (n + 1) & ~1u;
+  std::vector<uint32_t> staging(pos_words + 2 * static_cast<size_t>(n));
+  uint2* vals = reinterpret_cast<uint2*>(staging.data() + pos_words);
+  for (uint32_t i = 0; i < n; ++i) {
+    staging[i] = g->pos[edges[i].second];
+    vals[i] = device_record(g, edges[i].first, edges[i].second);
+  }
+  if (staging.size() > ctx->d_patch_cap) {
+    (void)hipFree(ctx->d_patch);
+    ctx->d_patch = nullptr;
+    ctx->d_patch_cap = 0;
+    ORH_HIP(ctx, hipMalloc(&ctx->d_patch, staging.size() * sizeof(uint32_t)));
+    ctx->d_patch_cap = staging.size();
+  }
+  ORH_HIP(ctx, hipMemcpyAsync(ctx->d_patch, staging.data(), staging.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, orh::launch_scatter_recs(g->d_recs, ctx->d_patch,
+                                        reinterpret_cast<const uint2*>(ctx->d_patch + pos_words), n,
+                                        ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
   g->ms_dirty = true;
   return ORH_OK;
 }
@@ -408,6 +443,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_lvl_rows);
   hipFree(ctx->d_ms_lvl);
   hipFree(ctx->d_batch);
+  hipFree(ctx->d_patch);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -478,6 +514,7 @@ int orh_graph_destroy(orh_graph* g) {
   hipSetDevice(g->ctx->device);
   hipStreamSynchronize(g->ctx->stream);
   free_graph_device(g);
+  g->ctx->req_key.clear();  // the staged request may describe this graph
   delete g;
   return ORH_OK;
 }
@@ -514,7 +551,7 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   g->meta.assign(c->meta, c->meta + c->n_edges);
   g->overloaded.assign(c->node_overloaded, c->node_overloaded + c->n_nodes);
   for (auto& o : g->overloaded) o = o ? 1 : 0;
-  g->gen += 1;
+  g->gen = next_graph_gen();
   g->row_of.assign(g->n_nodes, -1);
   recompute_bounds(g);
   build_neighbours(g);
@@ -562,14 +599,19 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
       return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_patch_edges: metric 0 on an up link");
   }
   ORH_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<std::pair<uint32_t, uint32_t>> edges;
+  edges.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = idx[i];
     g->w_out[e] = w_out[i];
     g->w_in[e] = w_in[i];
     g->meta[e] = meta[i] & ~ORH_META_COL_OVERLOADED;
-    int rc = upload_record(g, row_of(g, e), e);
-    if (rc) return rc;
+    edges.emplace_back(row_of(g, e), e);
   }
+  std::sort(edges.begin(), edges.end());
+  edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+  int rc = upload_records(g, edges);
+  if (rc) return rc;
   recompute_bounds(g);
   return ORH_OK;
 }
@@ -577,19 +619,24 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
 int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* idx, const uint8_t* ovl) {
   if (!g || (n && (!idx || !ovl))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
-  ORH_HIP(ctx, hipSetDevice(ctx->device));
-  for (uint32_t i = 0; i < n; ++i) {
+  if (!g->d_recs && n) return fail(ctx, ORH_E_STATE, "orh_graph_patch_nodes: no graph loaded");
+  for (uint32_t i = 0; i < n; ++i)
     if (idx[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_nodes: bad node");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<std::pair<uint32_t, uint32_t>> edges;
+  for (uint32_t i = 0; i < n; ++i) {
     const uint32_t v = idx[i];
     g->overloaded[v] = ovl[i] ? 1 : 0;
-    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl + v, &g->overloaded[v], 1, hipMemcpyHostToDevice,
-                                ctx->stream));
     // v's own records carry its row bit
-    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) {
-      int rc = upload_record(g, v, e);
-      if (rc) return rc;
-    }
+    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) edges.emplace_back(v, e);
   }
+  std::sort(edges.begin(), edges.end());
+  edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+  if (n && g->n_nodes)  // the whole flag array: one copy instead of one per node
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl, g->overloaded.data(), g->n_nodes, hipMemcpyHostToDevice,
+                                ctx->stream));
+  int rc = upload_records(g, edges);  // synchronizes the stream
+  if (rc) return rc;
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
@@ -880,15 +927,20 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   }
 #endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
+  orh_spf_info info{};
+  info.variant = static_cast<int32_t>(run_plan.variant);
+  info.rows = n_rows;
+  info.mask_bits = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.mask_bytes * 8 : 0;
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
     e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
-    e = orh::launch_first_hop(h, max_nbr, ctx->stream);
+    e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
   } else if (!fused) {
-    e = orh::launch_first_hop(h, max_nbr, ctx->stream);
+    e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
   }
+  ctx->last_info = info;
   ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
   ctx->counters.spf_runs += n_src;
   ctx->counters.spf_launches += 1;
@@ -956,6 +1008,12 @@ extern "C" int orh_last_spf_ms(orh_ctx* ctx, double* ms_out) {
   *ms_out = ms;
   ctx->counters.last_kernel_ms = ms;
   ctx->counters.total_kernel_ms += ms;
+  return ORH_OK;
+}
+
+extern "C" int orh_last_spf_info(const orh_ctx* ctx, orh_spf_info* out) {
+  if (!ctx || !out) return ORH_E_INVALID;
+  *out = ctx->last_info;
   return ORH_OK;
 }
 

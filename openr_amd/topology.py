@@ -238,6 +238,29 @@ def fabric(num_nodes: int, bug_compatible: bool = True,
 
 
 # ---------------------------------------------------------------------------
+# Ladder (deep BFS: every level count the device level encoding can hold)
+# ---------------------------------------------------------------------------
+
+def ladder(length: int, metric: int = 1, area: str = K_TESTING_AREA):
+    """Two rails a0..a{length-1}, b0..b{length-1} with rungs a_i-b_i; every
+    link has the same metric, so the BFS depth from one end is ~length."""
+    adjs: Dict[str, List[Adjacency]] = {}
+
+    def link(x, y):
+        for (p, q) in ((x, y), (y, x)):
+            adjs.setdefault(p, []).append(Adjacency(
+                q, f"{p}>{q}", BinaryAddress.of("fe80::1"), BinaryAddress.of("10.0.0.1"),
+                metric, 0, False, 0, 0, 1, f"{q}>{p}"))
+
+    for i in range(length):
+        link(f"a{i}", f"b{i}")
+        if i + 1 < length:
+            link(f"a{i}", f"a{i + 1}")
+            link(f"b{i}", f"b{i + 1}")
+    return [create_adj_db(n, a, 0, False, area) for n, a in adjs.items()], []
+
+
+# ---------------------------------------------------------------------------
 # Seeded WAN (SURVEY §8d config C4)
 # ---------------------------------------------------------------------------
 

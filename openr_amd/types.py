@@ -262,6 +262,20 @@ class RouteDb:
             {k: v.nexthop_set() for k, v in self.mplsRoutes.items()},
         )
 
+    def canonical_full(self):
+        """canonical() plus each route's bestArea and bestPrefixEntry (part of
+        RibUnicastEntry equality, RibEntry.h:65-69; tags left out)."""
+        def entry(e):
+            if e is None:
+                return None
+            return (e.prefix, e.type, e.data, e.forwardingType, e.forwardingAlgorithm, e.mv,
+                    e.minNexthop, e.prependLabel, e.metrics)
+        return (
+            {str(k): (v.nexthop_set(), v.doNotInstall, v.bestArea, entry(v.bestPrefixEntry))
+             for k, v in self.unicastRoutes.items()},
+            {k: v.nexthop_set() for k, v in self.mplsRoutes.items()},
+        )
+
 
 @dataclass
 class RouteDbDelta:

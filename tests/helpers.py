@@ -65,3 +65,23 @@ def pop_route(area=K_TESTING_AREA):
 def adj_label_nexthops(adjs, area=K_TESTING_AREA):
     """validateAdjLabelRoutes (DecisionTest.cpp:354-368)."""
     return {a.adjLabel: frozenset({nh_from_adj(a, False, a.metric, PHP, area)}) for a in adjs}
+
+
+def assert_digests_equal(solver_h, solver_o, me, als_h, ps_h, als_o, ps_o):
+    """Whole-route-DB parity at full size through the per-route canonical
+    digests both backends compute natively (build_route_db_digest); on a
+    mismatch, report the first differing route index."""
+    h = solver_h._impl.build_route_db_digest(me, als_h._impl, ps_h._impl)
+    o = solver_o._impl.build_route_db_digest(me, als_o._impl, ps_o._impl)
+    assert (h is None) == (o is None), me
+    if h is None:
+        return 0
+    assert h[:2] == o[:2], f"route counts differ: hip {h[:2]} oracle {o[:2]}"
+    if h[2] != o[2]:
+        import numpy as np
+        a = np.frombuffer(h[2], dtype=np.uint64)
+        b = np.frombuffer(o[2], dtype=np.uint64)
+        bad = np.nonzero(a != b)[0]
+        raise AssertionError(f"{len(bad)} routes differ (first canonical index {bad[0]} "
+                             f"of {h[0]} unicast + {h[1]} mpls)")
+    return h[0] + h[1]

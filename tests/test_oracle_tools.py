@@ -1,0 +1,41 @@
+"""The checker's own bulk helpers (CPU): oracle spf_tables must agree with its
+get_spf_result, and the route-db digest must see every field it covers."""
+import numpy as np
+
+from openr_amd.facade import load_topology
+from openr_amd.topology import bench_grid, ring
+from openr_amd.types import K_TESTING_AREA
+
+A = K_TESTING_AREA
+
+
+def test_spf_tables_match_spf_results(oracle):
+    adj_dbs, _ = bench_grid(6)
+    als, _ = load_topology(oracle, adj_dbs, [])
+    ls = als[A]
+    order = sorted(db.thisNodeName for db in adj_dbs)
+    srcs = ["0", "7", "35"]
+    nbrs = [sorted({l.n1 if l.n1 != s else l.n2 for l in ls.links_from_node(s)}) for s in srcs]
+    dist, nh = ls._impl.spf_tables(srcs, order, nbrs, 2)
+    for k, s in enumerate(srcs):
+        ref = ls.get_spf_result(s)
+        for j, v in enumerate(order):
+            assert dist[k, j] == ref[v].metric
+            hops = {nbrs[k][b] for b in range(len(nbrs[k])) if nh[k, j, b // 32] >> (b % 32) & 1}
+            assert hops == set(ref[v].nextHops), (s, v)
+
+
+def test_route_db_digest_sensitivity(oracle):
+    adj_dbs, prefixes = ring()
+    als, ps = load_topology(oracle, adj_dbs, prefixes)
+    s = oracle.spf_solver("1", True)
+    a = s._impl.build_route_db_digest("1", als._impl, ps._impl)
+    assert a == s._impl.build_route_db_digest("1", als._impl, ps._impl)
+    db = adj_dbs[0]
+    db.adjacencies[0].metric += 1  # changes nexthop metrics of some routes
+    als[A].update_adjacency_database(db)
+    b = s._impl.build_route_db_digest("1", als._impl, ps._impl)
+    assert a[:2] == b[:2] and a[2] != b[2]
+    x = np.frombuffer(a[2], np.uint64)
+    y = np.frombuffer(b[2], np.uint64)
+    assert 0 < np.count_nonzero(x != y) < len(x)
