@@ -152,6 +152,7 @@ int orh_last_spf_phase_ms(orh_ctx* ctx, double* dist_ms_out, double* hop_ms_out)
 int orh_device_alloc(orh_ctx* ctx, size_t bytes, void** d_out);
 int orh_device_free(orh_ctx* ctx, void* d_ptr);
 int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+int orh_memcpy_h2d(orh_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
 /* device-to-device copy on the context stream, completed before return (hands
  * rows to a caller-owned buffer, e.g. the RCCL all-gather of a central RIB) */
 int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
@@ -172,6 +173,9 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* h_edge_idx,
 int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* h_node_idx,
                           const uint8_t* h_overloaded);
 int orh_graph_info(const orh_graph* g, uint32_t* n_nodes, uint32_t* n_edges);
+/* device array of the graph's node overload flags (u8 [n_nodes]), valid
+ * until the next orh_graph_load (route selection's drained-node filter) */
+int orh_graph_device_flags(const orh_graph* g, const uint8_t** d_overloaded);
 /* distinct neighbour node ids of src in ascending order (bit k of an nh
  * mask is h_out[k]); *n_out receives the count even if it exceeds cap */
 int orh_graph_neighbors(const orh_graph* g, uint32_t src, uint32_t* h_out, uint32_t cap,
@@ -189,16 +193,89 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
 int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32_t* h_dist,
                   uint32_t* h_nh);
 
-/* ---- route selection (getMinCostNodes + getNextHopsWithMetric) --------- */
-/* For each prefix p with candidate advertisers h/d_adv[adv_ptr[p]..adv_ptr[p+1])
- * (node ids, already best-route-selected, Decision.cpp:794-822), over the
- * SPF row of `me` (d_dist/d_nh as produced by orh_spf_run for one source):
- *   d_min[p]            = min over advertisers of dist (ORH_UNREACHABLE if none)
- *   d_nh_out[p*W + k]   = OR of nh masks of the argmin advertisers
- * Asynchronous on the context stream; all pointers are device pointers. */
-int orh_route_select(orh_ctx* ctx, uint32_t n_prefix, const uint32_t* d_adv_ptr,
-                     const uint32_t* d_adv, const uint32_t* d_dist, const uint32_t* d_nh,
-                     uint32_t words, uint32_t* d_min, uint32_t* d_nh_out);
+/* ---- device prefix mirror (PrefixState) ------------------------------- */
+/* Replaces the per-prefix PrefixEntries map PrefixState::prefixes() hands to
+ * the route build (openr/decision/PrefixState.h:22-70, updatePrefix /
+ * deletePrefix PrefixState.cpp:17-56). Prefix p is a dense id chosen by the
+ * caller; its advertisements are an ordered list of orh_adv records (the
+ * order only numbers them: route selection reports the best one by its
+ * position). Node names and areas are caller-side ids. */
+typedef struct orh_prefix_set orh_prefix_set;
+
+typedef struct orh_adv {
+  uint32_t name;        /* advertiser node name id */
+  uint32_t meta;        /* area id (bits 0-7) | ORH_ADV_* flags */
+  int32_t path_pref;    /* PrefixMetrics.path_preference */
+  int32_t source_pref;  /* PrefixMetrics.source_preference */
+  int32_t distance;     /* PrefixMetrics.distance */
+} orh_adv;
+#define ORH_ADV_AREA_MASK 0xFFu
+#define ORH_ADV_SR_MPLS (1u << 8)     /* forwardingType == SR_MPLS */
+#define ORH_ADV_KSP2 (1u << 9)        /* forwardingAlgorithm == KSP2_ED_ECMP */
+#define ORH_ADV_BGP (1u << 10)        /* type == BGP */
+#define ORH_ADV_MIN_NEXTHOP (1u << 11) /* minNexthop is set */
+#define ORH_ADV_PREPEND (1u << 12)    /* prependLabel is set */
+#define ORH_PFX_V4 1u                 /* prefix_flags: an IPv4 prefix */
+
+int orh_prefix_create(orh_ctx* ctx, orh_prefix_set** out);
+int orh_prefix_destroy(orh_prefix_set* ps);
+/* full upload: prefix p owns advs[adv_ptr[p] .. adv_ptr[p+1]) */
+int orh_prefix_load(orh_prefix_set* ps, uint32_t n_prefix, const uint32_t* h_adv_ptr,
+                    const orh_adv* h_advs, const uint8_t* h_prefix_flags);
+/* incremental: prefix ids[i] gets advs[adv_ptr[i] .. adv_ptr[i+1]) (an empty
+ * list withdraws it; ids beyond the current count grow the set) */
+int orh_prefix_apply_delta(orh_prefix_set* ps, uint32_t n, const uint32_t* h_ids,
+                           const uint32_t* h_adv_ptr, const orh_adv* h_advs,
+                           const uint8_t* h_prefix_flags);
+/* string order of the name and area ids (std::set<NodeAndArea> order, which
+ * picks bestNodeArea, Decision.cpp:817 / Util.cpp:902-913) */
+int orh_prefix_set_order(orh_prefix_set* ps, uint32_t n_names, const uint32_t* h_name_rank,
+                         uint32_t n_areas, const uint32_t* h_area_rank);
+int orh_prefix_info(const orh_prefix_set* ps, uint32_t* n_prefix, uint32_t* n_adv_live,
+                    uint32_t* n_adv_pool);
+
+/* ---- route selection (createRouteForPrefix -> getNextHopsWithMetric) --- */
+/* One thread per prefix, for the solver's node `me`:
+ *   drop advertisers unreachable in their own area   Decision.cpp:468-480
+ *   best-route (max PrefixMetrics) or all-advertiser
+ *   selection, bestNodeArea, drained-node filter     :794-862, Util.h:491-526
+ *   forwarding type / algorithm                      Util.cpp:452-480
+ *   getMinCostNodes per area (area ignored) and the
+ *   cross-area min + first-hop mask OR               :1152-1228
+ * status[p]: ORH_SEL_NONE (no route), ORH_SEL_ROUTE (metric[p] = shortest,
+ * best[p] = position of bestNodeArea in p's list, mask[p] = per area the OR of
+ * the argmin advertisers' first-hop masks, zero for areas above the minimum),
+ * or ORH_SEL_HOST (a case the host path keeps: BGP metric vectors, SR_MPLS /
+ * KSP2 forwarding, minNexthop, self-advertised, unknown area, > 255
+ * advertisers). */
+#define ORH_SEL_NONE 0
+#define ORH_SEL_ROUTE 1
+#define ORH_SEL_HOST 2
+#define ORH_NO_NODE 0xFFFFFFFFu
+#define ORH_SELECT_BEST_ROUTE 1u /* enable_best_route_selection */
+#define ORH_SELECT_V4 2u         /* enable_v4 */
+
+typedef struct orh_select_area {
+  uint32_t present;            /* 0: the solver has no LinkState of this area id */
+  const uint32_t* d_dist;      /* me's distance row (device), NULL: me not in this area */
+  const uint32_t* d_nh;        /* me's first-hop rows [N][words] (device) */
+  const uint8_t* d_overloaded; /* [N] node overload flags (device) */
+  const uint32_t* d_name_node; /* [n_names] node id of each name id, ORH_NO_NODE if absent */
+  uint32_t words;              /* mask words of this area */
+  uint32_t word_off;           /* this area's first word in a prefix's mask */
+} orh_select_area;
+
+typedef struct orh_select_out {
+  uint8_t* d_status;  /* [n_prefix] ORH_SEL_* */
+  uint32_t* d_metric; /* [n_prefix] shortest metric */
+  uint32_t* d_best;   /* [n_prefix] position of the best advertisement */
+  uint32_t* d_mask;   /* [n_prefix][total_words] */
+  uint32_t total_words;
+} orh_select_out;
+
+/* asynchronous on the context stream; the area table is copied */
+int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
+                     const orh_select_area* h_areas, const orh_select_out* out);
 
 #ifdef __cplusplus
 }

@@ -24,8 +24,10 @@ EXT = sysconfig.get_config_var("EXT_SUFFIX")
 HOST_MOD = os.path.join(PKG, "_openr_host" + EXT)
 ARCH = os.environ.get("OPENR_HIP_ARCH", "gfx950")
 
-HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "spf_kernels.hip")]
-HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "spf_solver.cpp", "rib_policy.cpp", "host_py.cpp")]
+HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "spf_kernels.hip"),
+            os.path.join(CSRC, "kernels", "route_kernels.hip")]
+HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "prefix_state.cpp", "spf_solver.cpp",
+                                                   "rib_policy.cpp", "host_py.cpp")]
 
 
 def _hipcc() -> str:

@@ -808,7 +808,9 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              s.updateStaticMplsRoutes(u, del);
            })
-      .def_property_readonly("route_build_runs", &SpfSolver::routeBuildRuns);
+      .def_property_readonly("route_build_runs", &SpfSolver::routeBuildRuns)
+      .def_property_readonly("device_selected", &SpfSolver::deviceSelected)
+      .def_property_readonly("host_selected", &SpfSolver::hostSelected);
 
   py::class_<RibPolicy>(m, "RibPolicy")
       .def(py::init([](py::list statements, int64_t ttlSecs) {

@@ -1,0 +1,204 @@
+// PrefixState (openr/decision/PrefixState.cpp:17-56) and its device mirror
+// (orh_prefix_set): see spf_solver.h.
+#include <algorithm>
+#include <numeric>
+#include <stdexcept>
+
+#include "spf_solver.h"
+
+namespace openr_amd {
+
+namespace {
+
+void check(orh_ctx* ctx, int rc, const char* what) {
+  if (rc != ORH_OK)
+    throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) +
+                             "): " + (ctx ? orh_last_error(ctx) : ""));
+}
+
+}  // namespace
+
+PrefixState::~PrefixState() {
+  if (dev_) orh_prefix_destroy(dev_);
+}
+
+std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
+                                            const PrefixEntry& e) {
+  Cidr key{e.addr, e.len};
+  auto [it, inserted] = prefixes_[key].emplace(NodeAndArea{node, area}, e);
+  if (!inserted && it->second == e) return {};
+  if (!inserted) {
+    ksp2Entries_ -= it->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+    it->second = e;
+  }
+  ksp2Entries_ += e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+  internName(node);
+  internArea(area);
+  touch(key, false);
+  return {key};
+}
+
+std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::string& area,
+                                            const Cidr& prefix) {
+  auto it = prefixes_.find(prefix);
+  if (it == prefixes_.end()) return {};
+  auto e = it->second.find(NodeAndArea{node, area});
+  if (e == it->second.end()) return {};
+  ksp2Entries_ -= e->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+  it->second.erase(e);
+  const bool gone = it->second.empty();
+  if (gone) prefixes_.erase(it);
+  touch(prefix, gone);
+  return {prefix};
+}
+
+uint32_t PrefixState::internName(const std::string& n) {
+  auto [it, inserted] = nameIds_.emplace(n, static_cast<uint32_t>(names_.size()));
+  if (inserted) names_.push_back(n);
+  return it->second;
+}
+
+uint32_t PrefixState::internArea(const std::string& a) {
+  auto [it, inserted] = areaIds_.emplace(a, static_cast<uint32_t>(areas_.size()));
+  if (inserted) areas_.push_back(a);
+  return it->second;
+}
+
+std::optional<uint32_t> PrefixState::nameId(const std::string& n) const {
+  auto it = nameIds_.find(n);
+  if (it == nameIds_.end()) return std::nullopt;
+  return it->second;
+}
+
+std::optional<uint32_t> PrefixState::areaId(const std::string& a) const {
+  auto it = areaIds_.find(a);
+  if (it == areaIds_.end()) return std::nullopt;
+  return it->second;
+}
+
+// a prefix whose advertisement list changed: give it a dense id (or free the
+// id when its last advertisement is withdrawn) and queue it for upload
+void PrefixState::touch(const Cidr& prefix, bool erased) {
+  uint32_t pid;
+  auto it = pid_.find(prefix);
+  if (it != pid_.end()) {
+    pid = it->second;
+    if (erased) {
+      pid_.erase(it);
+      live_[pid] = 0;
+      freePids_.push_back(pid);
+    }
+  } else {
+    if (erased) return;
+    if (!freePids_.empty()) {
+      pid = freePids_.back();
+      freePids_.pop_back();
+      cidrOf_[pid] = prefix;
+    } else {
+      pid = static_cast<uint32_t>(cidrOf_.size());
+      cidrOf_.push_back(prefix);
+      live_.push_back(0);
+      isDirty_.push_back(0);
+      run_.emplace_back(0u, 0u);
+    }
+    pid_.emplace(prefix, pid);
+    live_[pid] = 1;
+  }
+  if (!isDirty_[pid]) {
+    isDirty_[pid] = 1;
+    dirty_.push_back(pid);
+  }
+}
+
+// pid's advertisements appended to the host pool (the numbering the device
+// reports best positions in) and as device records
+void PrefixState::buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const {
+  advLive_ -= run_[pid].second;
+  run_[pid] = {static_cast<uint32_t>(advPool_.size()), 0u};
+  *flags = 0;
+  if (!live_[pid]) return;
+  auto it = prefixes_.find(cidrOf_[pid]);
+  if (it == prefixes_.end()) return;
+  *flags = it->first.first.size() == 4 ? ORH_PFX_V4 : 0;
+  for (const auto& [na, e] : it->second) {
+    advPool_.push_back(AdvRef{&na, &e});
+    uint32_t meta = areaIds_.at(na.second) & ORH_ADV_AREA_MASK;
+    if (e.forwardingType == kFwdSrMpls) meta |= ORH_ADV_SR_MPLS;
+    if (e.forwardingAlgorithm == kAlgoKsp2EdEcmp) meta |= ORH_ADV_KSP2;
+    if (e.type == kPrefixTypeBgp) meta |= ORH_ADV_BGP;
+    if (e.minNexthop) meta |= ORH_ADV_MIN_NEXTHOP;
+    if (e.prependLabel) meta |= ORH_ADV_PREPEND;
+    out.push_back(orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference,
+                          e.distance});
+  }
+  run_[pid].second = static_cast<uint32_t>(advPool_.size()) - run_[pid].first;
+  advLive_ += run_[pid].second;
+}
+
+orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
+  if (areas_.size() > ORH_ADV_AREA_MASK + 1)
+    throw std::runtime_error("PrefixState: more than 256 areas for the device mirror");
+  if (dev_ && devCtx_ != ctx) {
+    orh_prefix_destroy(dev_);
+    dev_ = nullptr;
+  }
+  if (!dev_) {
+    check(ctx, orh_prefix_create(ctx, &dev_), "orh_prefix_create");
+    devCtx_ = ctx;
+    devFull_ = true;
+    namesOrdered_ = areasOrdered_ = 0;
+  }
+  auto& self = const_cast<PrefixState&>(*this);  // dirty list: bookkeeping only
+  // host pool mostly garbage: renumber every prefix (device reloaded too)
+  if (advPool_.size() > 4096 && advPool_.size() > 2 * advLive_) devFull_ = true;
+  if (devFull_) {
+    advPool_.clear();
+    advLive_ = 0;
+    std::vector<orh_adv> recs;
+    std::vector<uint32_t> ptr(cidrOf_.size() + 1, 0);
+    std::vector<uint8_t> fl(cidrOf_.size(), 0);
+    recs.reserve(prefixes_.size() + prefixes_.size() / 8);
+    advPool_.reserve(recs.capacity());
+    for (uint32_t pid = 0; pid < cidrOf_.size(); ++pid) {
+      run_[pid] = {0u, 0u};
+      buildRun(pid, recs, &fl[pid]);
+      ptr[pid + 1] = static_cast<uint32_t>(recs.size());
+    }
+    check(ctx, orh_prefix_load(dev_, static_cast<uint32_t>(cidrOf_.size()), ptr.data(), recs.data(),
+                               fl.data()),
+          "orh_prefix_load");
+    devFull_ = false;
+  } else if (!dirty_.empty()) {
+    std::vector<orh_adv> recs;
+    std::vector<uint32_t> ptr(1, 0);
+    std::vector<uint8_t> fl(dirty_.size(), 0);
+    for (size_t i = 0; i < dirty_.size(); ++i) {
+      buildRun(dirty_[i], recs, &fl[i]);
+      ptr.push_back(static_cast<uint32_t>(recs.size()));
+    }
+    check(ctx, orh_prefix_apply_delta(dev_, static_cast<uint32_t>(dirty_.size()), dirty_.data(),
+                                      ptr.data(), recs.data(), fl.data()),
+          "orh_prefix_apply_delta");
+  }
+  for (uint32_t pid : dirty_) self.isDirty_[pid] = 0;
+  self.dirty_.clear();
+  if (namesOrdered_ != names_.size() || areasOrdered_ != areas_.size()) {
+    // std::set<NodeAndArea> order = byte order of the names, then areas
+    auto ranks = [](const std::vector<std::string>& v) {
+      std::vector<uint32_t> idx(v.size()), rank(v.size());
+      std::iota(idx.begin(), idx.end(), 0u);
+      std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return v[a] < v[b]; });
+      for (uint32_t r = 0; r < idx.size(); ++r) rank[idx[r]] = r;
+      return rank;
+    };
+    const auto nr = ranks(names_), ar = ranks(areas_);
+    check(ctx, orh_prefix_set_order(dev_, static_cast<uint32_t>(names_.size()), nr.data(),
+                                    static_cast<uint32_t>(areas_.size()), ar.data()),
+          "orh_prefix_set_order");
+    namesOrdered_ = static_cast<uint32_t>(names_.size());
+    areasOrdered_ = static_cast<uint32_t>(areas_.size());
+  }
+  return dev_;
+}
+
+}  // namespace openr_amd

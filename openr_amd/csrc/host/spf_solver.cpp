@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <list>
 #include <stdexcept>
@@ -149,32 +150,6 @@ Cmp compareMv(MetricVector l, MetricVector r) {
 
 }  // namespace
 
-// ---- PrefixState (PrefixState.cpp:17-56) ------------------------------------
-std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
-                                            const PrefixEntry& e) {
-  Cidr key{e.addr, e.len};
-  auto [it, inserted] = prefixes_[key].emplace(NodeAndArea{node, area}, e);
-  if (!inserted && it->second == e) return {};
-  if (!inserted) {
-    ksp2Entries_ -= it->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
-    it->second = e;
-  }
-  ksp2Entries_ += e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
-  return {key};
-}
-
-std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::string& area,
-                                            const Cidr& prefix) {
-  auto it = prefixes_.find(prefix);
-  if (it == prefixes_.end()) return {};
-  auto e = it->second.find(NodeAndArea{node, area});
-  if (e == it->second.end()) return {};
-  ksp2Entries_ -= e->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
-  it->second.erase(e);
-  if (it->second.empty()) prefixes_.erase(it);
-  return {prefix};
-}
-
 // ---- SpfSolver ----------------------------------------------------------------
 SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool enableOrderedFib, bool bgpDryRun,
                      bool enableBestRouteSelection)
@@ -183,6 +158,14 @@ SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool enableOrderedFib
       enableOrderedFib_(enableOrderedFib),
       bgpDryRun_(bgpDryRun),
       enableBestRouteSelection_(enableBestRouteSelection) {}
+
+SpfSolver::~SpfSolver() {
+  for (auto& w : areaWork_) {
+    if (w.dNameNode) orh_device_free(selCtx_, w.dNameNode);
+    if (w.dRow) orh_device_free(selCtx_, w.dRow);
+  }
+  if (dSel_) orh_device_free(selCtx_, dSel_);
+}
 
 void SpfSolver::updateStaticUnicastRoutes(
     const std::vector<std::pair<Cidr, std::vector<NextHopThrift>>>& upd,
@@ -608,6 +591,196 @@ std::optional<RibUnicastEntry> SpfSolver::addBestPaths(const std::string& me, co
   return e;
 }
 
+// Device route selection (route_select_kernel) for every prefix of the
+// PrefixState mirror: status / shortest metric / best advertisement / per-area
+// first-hop masks land in selStatus_ .. selMask_. The kernel's area list is
+// the mirror's area ids, then every other area of `als` (getMinCostNodes
+// reads every area's SPF, Decision.cpp:1194-1197). Returns false (all
+// prefixes on the host path) when the inputs are outside what it covers.
+bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
+                               const PrefixState& ps) {
+  deviceSelected_ = hostSelected_ = 0;
+  if (std::getenv("ORH_HOST_SELECT")) return false;  // A/B switch: host selection
+  if (ps.numPrefixIds() == 0 || als.empty()) return false;
+  orh_ctx* ctx = als.begin()->second.context();
+  for (const auto& [_, ls] : als)
+    if (ls.context() != ctx) return false;
+  if (selCtx_ && selCtx_ != ctx) return false;
+  // getNextHopsWithMetric keys nexthops by neighbour name only (:1221): a
+  // neighbour name shared by two areas couples their links, keep those
+  // topologies on the host path
+  if (als.size() > 1) {
+    std::unordered_set<std::string> seen;
+    for (const auto& [_, ls] : als) {
+      auto myId = ls.nodeId(me);
+      if (!myId) continue;
+      std::unordered_set<std::string> mine;
+      for (uint32_t lid : ls.linksFromNode(me)) mine.insert(ls.nodeName(ls.link(lid).other(*myId)));
+      for (const auto& n : mine)
+        if (!seen.insert(n).second) return false;
+    }
+  }
+  std::vector<const LinkState*> order;  // kernel area index -> LinkState (or null)
+  for (uint32_t a = 0; a < ps.numAreas(); ++a) {
+    auto it = als.find(ps.area(a));
+    order.push_back(it == als.end() ? nullptr : &it->second);
+  }
+  for (const auto& [area, ls] : als)
+    if (!ps.areaId(area)) order.push_back(&ls);
+  if (order.size() > 32) return false;
+  selCtx_ = ctx;
+  orh_prefix_set* set = ps.syncDevice(ctx);
+  areaWork_.resize(order.size());
+  std::vector<orh_select_area> sel(order.size());
+  uint32_t words = 0;
+  const uint32_t nNames = ps.numNames();
+  for (size_t a = 0; a < order.size(); ++a) {
+    AreaWork& w = areaWork_[a];
+    sel[a] = orh_select_area{};
+    w.words = 0;
+    w.tmpl4.clear();
+    w.tmpl6.clear();
+    const LinkState* ls = order[a];
+    if (!ls) continue;
+    sel[a].present = 1;
+    const SpfRow& row = ls->getSpfResult(me);
+    orh_graph* g = ls->deviceGraph();
+    if (!row.known) continue;  // me's SpfResult holds only me: nothing reachable
+    const uint32_t N = static_cast<uint32_t>(row.dist.size());
+    // names -> node ids of this area (incremental while both only grow)
+    if (w.ls != ls || w.lsNodes != ls->numNodeIds() || w.psNames > nNames) {
+      w.ls = ls;
+      w.lsNodes = ls->numNodeIds();
+      w.psNames = 0;
+      w.nameNode.clear();
+    }
+    if (w.psNames != nNames) {
+      w.nameNode.resize(nNames);
+      for (uint32_t n = w.psNames; n < nNames; ++n) {
+        auto id = ls->nodeId(ps.name(n));
+        w.nameNode[n] = id && *id < N ? *id : ORH_NO_NODE;
+      }
+      if (nNames > w.dNameNodeCap) {
+        if (w.dNameNode) orh_device_free(ctx, w.dNameNode);
+        w.dNameNodeCap = std::max<size_t>(nNames, 2 * w.dNameNodeCap);
+        w.dNameNode = nullptr;
+        if (orh_device_alloc(ctx, w.dNameNodeCap * 4, reinterpret_cast<void**>(&w.dNameNode)) != ORH_OK)
+          throw std::runtime_error("route select: device allocation failed");
+      }
+      if (orh_memcpy_h2d(ctx, w.dNameNode, w.nameNode.data(), nNames * 4ull) != ORH_OK)
+        throw std::runtime_error(std::string("route select: ") + orh_last_error(ctx));
+      w.psNames = nNames;
+    }
+    // me's rows of this area
+    const size_t rowWords = static_cast<size_t>(N) * (1 + row.words);
+    if (rowWords > w.dRowCap) {
+      if (w.dRow) orh_device_free(ctx, w.dRow);
+      w.dRow = nullptr;
+      w.dRowCap = rowWords;
+      if (orh_device_alloc(ctx, rowWords * 4, reinterpret_cast<void**>(&w.dRow)) != ORH_OK)
+        throw std::runtime_error("route select: device allocation failed");
+    }
+    if (orh_memcpy_h2d(ctx, w.dRow, row.dist.data(), N * 4ull) != ORH_OK ||
+        orh_memcpy_h2d(ctx, w.dRow + N, row.nh.data(), row.nh.size() * 4ull) != ORH_OK)
+      throw std::runtime_error(std::string("route select: ") + orh_last_error(ctx));
+    const uint8_t* dOvl = nullptr;
+    if (orh_graph_device_flags(g, &dOvl) != ORH_OK)
+      throw std::runtime_error(std::string("route select: ") + orh_last_error(ctx));
+    w.words = row.words;
+    w.wordOff = words;
+    words += row.words;
+    sel[a].d_dist = w.dRow;
+    sel[a].d_nh = w.dRow + N;
+    sel[a].d_overloaded = dOvl;
+    sel[a].d_name_node = w.dNameNode;
+    sel[a].words = w.words;
+    sel[a].word_off = w.wordOff;
+    // nexthop templates per first-hop bit: my up links whose metric equals
+    // the distance to their neighbour (getNextHopsThrift's distOverLink ==
+    // minMetric, Decision.cpp:1271-1276, for a neighbour on a shortest path)
+    w.tmpl4.assign(row.nbrs.size(), {});
+    w.tmpl6.assign(row.nbrs.size(), {});
+    const uint32_t myId = row.src;
+    for (uint32_t lid : ls->linksFromNode(me)) {
+      const Link& l = ls->link(lid);
+      const uint32_t nbr = l.other(myId);
+      if (!l.isUp() || !row.reachable(nbr) || l.metricFrom(myId) != row.metric(nbr)) continue;
+      auto k = std::lower_bound(row.nbrs.begin(), row.nbrs.end(), nbr) - row.nbrs.begin();
+      if (k >= static_cast<ptrdiff_t>(row.nbrs.size()) || row.nbrs[k] != nbr) continue;
+      const std::string& nbrName = ls->nodeName(nbr);
+      w.tmpl6[k].push_back(nextHop(l.nhV6From(myId), l.ifFrom(myId), 0, std::nullopt, l.area, nbrName));
+      w.tmpl4[k].push_back(nextHop(l.nhV4From(myId), l.ifFrom(myId), 0, std::nullopt, l.area, nbrName));
+    }
+  }
+  // outputs: status [n] | metric [n] | best [n] | mask [n][words]
+  const uint32_t n = ps.numPrefixIds();
+  const size_t n4 = (static_cast<size_t>(n) + 3) & ~static_cast<size_t>(3);
+  const size_t bytes = n4 + 8ull * n + 4ull * n * std::max(words, 1u);
+  if (bytes > dSelCap_) {
+    if (dSel_) orh_device_free(ctx, dSel_);
+    dSel_ = nullptr;
+    dSelCap_ = std::max(bytes, dSelCap_ * 2);
+    if (orh_device_alloc(ctx, dSelCap_, reinterpret_cast<void**>(&dSel_)) != ORH_OK)
+      throw std::runtime_error("route select: device allocation failed");
+  }
+  orh_select_out out{};
+  out.d_status = dSel_;
+  out.d_metric = reinterpret_cast<uint32_t*>(dSel_ + n4);
+  out.d_best = out.d_metric + n;
+  out.d_mask = out.d_best + n;
+  out.total_words = words;
+  const auto meName = ps.nameId(me);
+  uint32_t flags = (enableBestRouteSelection_ ? ORH_SELECT_BEST_ROUTE : 0u) |
+      (enableV4_ ? ORH_SELECT_V4 : 0u);
+  if (orh_route_select(set, meName ? *meName : ORH_NO_NODE, flags,
+                       static_cast<uint32_t>(order.size()), sel.data(), &out) != ORH_OK)
+    throw std::runtime_error(std::string("orh_route_select: ") + orh_last_error(ctx));
+  selStatus_.resize(n);
+  selMetric_.resize(n);
+  selBest_.resize(n);
+  selMask_.resize(static_cast<size_t>(n) * words);
+  selWords_ = words;
+  if (orh_memcpy_d2h(ctx, selStatus_.data(), out.d_status, n) != ORH_OK ||
+      orh_memcpy_d2h(ctx, selMetric_.data(), out.d_metric, 4ull * n) != ORH_OK ||
+      orh_memcpy_d2h(ctx, selBest_.data(), out.d_best, 4ull * n) != ORH_OK ||
+      orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
+    throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
+  return true;
+}
+
+RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) const {
+  // selectBestPathsSpf -> getNextHopsThrift -> addBestPaths (Decision.cpp
+  // :904-963, :1230-1334, :1089-1150) for a device-selected IP / SP_ECMP
+  // prefix: every set first-hop bit contributes its tight links, each with
+  // metric = the shortest distance
+  RibUnicastEntry e;
+  e.prefix = ps.prefixOf(pid);
+  const bool v4 = e.prefix.first.size() == 4;
+  const int32_t metric = static_cast<int32_t>(selMetric_[pid]);
+  const uint32_t* m = selMask_.data() + static_cast<size_t>(pid) * selWords_;
+  for (const AreaWork& w : areaWork_) {
+    const auto& tmpl = v4 ? w.tmpl4 : w.tmpl6;
+    for (uint32_t k = 0; k < w.words; ++k) {
+      for (uint32_t bits = m[w.wordOff + k]; bits; bits &= bits - 1) {
+        const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
+        if (b >= tmpl.size()) continue;
+        for (const auto& t : tmpl[b]) {
+          NextHopThrift nh = t;
+          nh.metric = metric;
+          e.nexthops.insert(std::move(nh));
+        }
+      }
+    }
+  }
+  uint32_t cnt = 0;
+  const AdvRef* advs = ps.advs(pid, &cnt);
+  const AdvRef& best = advs[selBest_[pid]];
+  e.bestPrefixEntry = *best.entry;
+  e.bestArea = best.key->second;
+  e.doNotInstall = false;  // BGP prefixes take the host path
+  return e;
+}
+
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
                                                        const AreaLinkStates& als,
                                                        const PrefixState& ps) {
@@ -650,11 +823,56 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   prof.mark("spf(me)");
   DecisionRouteDb db;
   db.unicastRoutes.reserve(ps.prefixes().size());
-  std::vector<const Cidr*> keys;
-  keys.reserve(ps.prefixes().size());
-  for (const auto& [prefix, _] : ps.prefixes()) keys.push_back(&prefix);
   auto& pool = WorkerPool::instance();
-  if (!hasKsp && keys.size() >= kParallelMin && pool.size() > 1) {
+  // per-prefix selection on the device; the host materialises the routes it
+  // selected and runs the full reference logic for the prefixes it returns
+  // as ORH_SEL_HOST (BGP, SR_MPLS / KSP2, minNexthop, self-advertised)
+  const bool dev = selectOnDevice(me, als, ps);
+  prof.mark("select (device)");
+  std::vector<const Cidr*> keys;
+  if (dev) {
+    const uint32_t n = ps.numPrefixIds();
+    uint64_t nHost = 0, nDev = 0;
+    for (uint32_t pid = 0; pid < n; ++pid) {
+      if (!ps.prefixLive(pid)) continue;
+      if (selStatus_[pid] == ORH_SEL_HOST) ++nHost; else ++nDev;
+    }
+    deviceSelected_ = nDev;
+    hostSelected_ = nHost;
+    auto one = [&](uint32_t pid, decltype(db.unicastRoutes)& out) {
+      if (!ps.prefixLive(pid)) return;
+      if (selStatus_[pid] == ORH_SEL_ROUTE) {
+        RibUnicastEntry e = materialize(pid, ps);
+        Cidr k = e.prefix;
+        out.emplace(std::move(k), std::move(e));
+      } else if (selStatus_[pid] == ORH_SEL_HOST) {
+        if (auto r = createRouteForPrefix(me, als, ps, ps.prefixOf(pid))) {
+          Cidr k = r->prefix;
+          out.emplace(std::move(k), std::move(*r));
+        }
+      }
+    };
+    if (!hasKsp && n >= kParallelMin && pool.size() > 1) {
+      std::vector<decltype(db.unicastRoutes)> parts(pool.size());
+      pool.parallelFor(n, [&](size_t w, size_t b, size_t e) {
+        parts[w].reserve(parts[w].size() + (e - b));
+        for (size_t pid = b; pid < e; ++pid) one(static_cast<uint32_t>(pid), parts[w]);
+      });
+      prof.mark("unicast (pool)");
+      for (auto& part : parts) {
+        db.unicastRoutes.merge(part);
+        if (!part.empty()) throw std::logic_error("duplicate unicast route");
+      }
+    } else {
+      for (uint32_t pid = 0; pid < n; ++pid) one(pid, db.unicastRoutes);
+    }
+  } else {
+    keys.reserve(ps.prefixes().size());
+    for (const auto& [prefix, _] : ps.prefixes()) keys.push_back(&prefix);
+  }
+  if (dev) {
+    // routes built above
+  } else if (!hasKsp && keys.size() >= kParallelMin && pool.size() > 1) {
     // each worker fills a map of the output type; the merge splices nodes
     // (no entry is copied or moved)
     std::vector<decltype(db.unicastRoutes)> parts(pool.size());

@@ -18,8 +18,25 @@ namespace openr_amd {
 
 using PrefixEntries = std::unordered_map<NodeAndArea, PrefixEntry, StrPairHash>;
 
+// one advertisement as the device mirror numbers it (order within a prefix)
+struct AdvRef {
+  const NodeAndArea* key;
+  const PrefixEntry* entry;
+};
+
+// PrefixState (openr/decision/PrefixState.h:22-70) plus a device mirror of
+// it for SpfSolver's device route selection: every prefix gets a dense id,
+// advertiser names and areas get ids, and updatePrefix / deletePrefix record
+// the prefix as dirty; the next route build uploads only the dirty prefixes'
+// advertisement lists (orh_prefix_apply_delta), the first one everything
+// (orh_prefix_load).
 class PrefixState {
  public:
+  PrefixState() = default;
+  PrefixState(const PrefixState&) = delete;
+  PrefixState& operator=(const PrefixState&) = delete;
+  ~PrefixState();
+
   std::vector<Cidr> updatePrefix(const std::string& node, const std::string& area,
                                  const PrefixEntry& e);
   std::vector<Cidr> deletePrefix(const std::string& node, const std::string& area,
@@ -29,9 +46,49 @@ class PrefixState {
   // skip its KSP2 planning pass when there are none)
   size_t ksp2Entries() const { return ksp2Entries_; }
 
+  // ---- device mirror (used by SpfSolver) ----
+  // brings the mirror on `ctx` up to date; returns it
+  orh_prefix_set* syncDevice(orh_ctx* ctx) const;
+  uint32_t numPrefixIds() const { return static_cast<uint32_t>(cidrOf_.size()); }
+  const Cidr& prefixOf(uint32_t pid) const { return cidrOf_[pid]; }
+  bool prefixLive(uint32_t pid) const { return live_[pid] != 0; }
+  // the advertisements of pid in the order the device numbers them
+  const AdvRef* advs(uint32_t pid, uint32_t* n) const {
+    *n = run_[pid].second;
+    return advPool_.data() + run_[pid].first;
+  }
+  std::optional<uint32_t> nameId(const std::string& n) const;
+  uint32_t numNames() const { return static_cast<uint32_t>(names_.size()); }
+  const std::string& name(uint32_t id) const { return names_[id]; }
+  std::optional<uint32_t> areaId(const std::string& a) const;
+  uint32_t numAreas() const { return static_cast<uint32_t>(areas_.size()); }
+  const std::string& area(uint32_t id) const { return areas_[id]; }
+
  private:
+  void touch(const Cidr& prefix, bool erased);
+  uint32_t internName(const std::string& n);
+  uint32_t internArea(const std::string& a);
+  void buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const;
+
   std::unordered_map<Cidr, PrefixEntries, CidrHash> prefixes_;
   size_t ksp2Entries_{0};
+
+  std::unordered_map<Cidr, uint32_t, CidrHash> pid_;
+  std::vector<Cidr> cidrOf_;
+  std::vector<uint8_t> live_;
+  std::vector<uint32_t> freePids_;
+  std::vector<uint32_t> dirty_;
+  std::vector<uint8_t> isDirty_;
+  std::unordered_map<std::string, uint32_t> nameIds_, areaIds_;
+  std::vector<std::string> names_, areas_;
+
+  mutable std::vector<AdvRef> advPool_;
+  mutable std::vector<std::pair<uint32_t, uint32_t>> run_;  // pid -> (offset, count)
+  mutable size_t advLive_{0};
+  mutable orh_prefix_set* dev_{nullptr};
+  mutable orh_ctx* devCtx_{nullptr};
+  mutable bool devFull_{true};
+  mutable uint32_t namesOrdered_{0}, areasOrdered_{0};
 };
 
 // unordered_map<string, LinkState>; nodes are stable so LinkState can stay
@@ -68,6 +125,11 @@ class SpfSolver {
       const Cidr& prefix);
 
   uint64_t routeBuildRuns() const { return routeBuildRuns_; }
+  // prefixes of the last buildRouteDb whose selection ran on the device /
+  // took the host path (BGP, SR_MPLS, KSP2, minNexthop, self-advertised)
+  uint64_t deviceSelected() const { return deviceSelected_; }
+  uint64_t hostSelected() const { return hostSelected_; }
+  ~SpfSolver();
 
  private:
   using NhKey = std::pair<std::string, std::string>;
@@ -106,6 +168,34 @@ class SpfSolver {
   bool fastSpEcmp(const std::string& me, const LinkState& ls, const std::string& area,
                   const std::set<NodeAndArea>& dsts, bool isV4, std::optional<int32_t> swapLabel,
                   NextHopSet& out) const;
+
+  // device route selection over the PrefixState mirror; false when the
+  // inputs need the host path for every prefix
+  bool selectOnDevice(const std::string& me, const AreaLinkStates& als, const PrefixState& ps);
+  RibUnicastEntry materialize(uint32_t pid, const PrefixState& ps) const;
+
+  // device selection workspace (per solver)
+  struct AreaWork {
+    const LinkState* ls{nullptr};
+    uint32_t lsNodes{0}, psNames{0};      // name_node built for these sizes
+    std::vector<uint32_t> nameNode;       // ps name id -> node id in ls
+    uint32_t* dNameNode{nullptr};
+    size_t dNameNodeCap{0};
+    uint32_t* dRow{nullptr};              // me's dist row | first-hop rows
+    size_t dRowCap{0};
+    uint32_t words{0}, wordOff{0};
+    // per first-hop bit: tight up links of me to that neighbour as nexthop
+    // templates (metric set per route), v6 and v4 addresses
+    std::vector<std::vector<NextHopThrift>> tmpl6, tmpl4;
+  };
+  std::vector<AreaWork> areaWork_;
+  orh_ctx* selCtx_{nullptr};
+  uint8_t* dSel_{nullptr};  // status | metric | best | mask
+  size_t dSelCap_{0};
+  std::vector<uint8_t> selStatus_;
+  std::vector<uint32_t> selMetric_, selBest_, selMask_;
+  uint32_t selWords_{0};
+  uint64_t deviceSelected_{0}, hostSelected_{0};
 
   std::unordered_map<int32_t, std::vector<NextHopThrift>> staticMplsRoutes_;
   std::unordered_map<Cidr, std::vector<NextHopThrift>, CidrHash> staticUnicastRoutes_;

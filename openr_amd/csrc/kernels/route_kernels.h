@@ -1,0 +1,48 @@
+// Internal interface of the route-selection kernels (route_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/openr_hip.h"
+
+namespace orh {
+
+constexpr uint32_t kMaxSelectAreas = 32;
+
+// one area of a route-selection launch (device pointers; see orh_select_area)
+struct SelArea {
+  uint32_t present;
+  const uint32_t* dist;
+  const uint32_t* nh;
+  const uint8_t* ovl;
+  const uint32_t* name_node;
+  uint32_t words;
+  uint32_t word_off;
+};
+
+struct RouteSelectArgs {
+  uint32_t n_prefix;
+  const uint2* hdr;  // per prefix {pool offset, count | prefix flags << 16}
+  const orh_adv* adv;
+  const uint32_t* name_rank;
+  const uint32_t* area_rank;
+  uint32_t n_names;
+  uint32_t me_name;
+  uint32_t flags;  // ORH_SELECT_*
+  uint32_t n_areas;
+  const SelArea* areas;  // [n_areas], device
+  uint8_t* status;
+  uint32_t* metric;
+  uint32_t* best;
+  uint32_t* mask;
+  uint32_t total_words;
+};
+
+hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s);
+
+// hdr[ids[i]] = vals[i]
+hipError_t launch_scatter_hdr(uint2* hdr, const uint32_t* ids, const uint2* vals, uint32_t n,
+                              hipStream_t s);
+
+}  // namespace orh

@@ -124,17 +124,6 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s,
 // first-hop phase reads instead of u32 distance rows
 hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
 
-struct RouteSelectArgs {
-  uint32_t n_prefix;
-  uint32_t words;
-  const uint32_t* adv_ptr;
-  const uint32_t* adv;
-  const uint32_t* dist;
-  const uint32_t* nh;
-  uint32_t* min_out;
-  uint32_t* nh_out;
-};
-hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s);
 // recs[pos[i]] = vals[i] for i < n (device pointers)
 hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* vals, uint32_t n,
                                hipStream_t s);

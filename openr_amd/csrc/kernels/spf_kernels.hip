@@ -1280,28 +1280,6 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// route selection: getMinCostNodes + nexthop OR (Decision.cpp:1152-1228)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void route_select_kernel(RouteSelectArgs a) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  if (p >= a.n_prefix) return;
-  const uint32_t b = a.adv_ptr[p], e = a.adv_ptr[p + 1];
-  uint32_t best = kInf;
-  for (uint32_t i = b; i < e; ++i) best = min(best, a.dist[a.adv[i]]);
-  a.min_out[p] = best;
-  for (uint32_t k = 0; k < a.words; ++k) {
-    uint32_t m = 0;
-    if (best != kInf) {
-      for (uint32_t i = b; i < e; ++i) {
-        const uint32_t v = a.adv[i];
-        if (a.dist[v] == best) m |= a.nh[static_cast<size_t>(v) * a.words + k];
-      }
-    }
-    a.nh_out[static_cast<size_t>(p) * a.words + k] = m;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // planning and launch
 // ---------------------------------------------------------------------------
 // dynamic-LDS opt-in, raised once per kernel to the largest size launched
@@ -1528,13 +1506,6 @@ hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* va
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_recs_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, recs,
                      pos, vals, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s) {
-  if (a.n_prefix == 0) return hipSuccess;
-  const uint32_t grid = (a.n_prefix + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(route_select_kernel, dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/openr_hip.h"
+#include "kernels/route_kernels.h"
 #include "kernels/spf_kernels.h"
 
 struct orh_ctx {
@@ -488,7 +489,16 @@ int orh_device_free(orh_ctx* ctx, void* d_ptr) {
 
 int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes) {
   if (!ctx || (!h_dst && bytes) || (!d_src && bytes)) return ORH_E_INVALID;
+  if (!bytes) return ORH_OK;
   ORH_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ORH_OK;
+}
+
+int orh_memcpy_h2d(orh_ctx* ctx, void* d_dst, const void* h_src, size_t bytes) {
+  if (!ctx || (!d_dst && bytes) || (!h_src && bytes)) return ORH_E_INVALID;
+  if (!bytes) return ORH_OK;
+  ORH_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
@@ -638,6 +648,13 @@ int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* idx, const u
   int rc = upload_records(g, edges);  // synchronizes the stream
   if (rc) return rc;
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ORH_OK;
+}
+
+int orh_graph_device_flags(const orh_graph* g, const uint8_t** d_overloaded) {
+  if (!g || !d_overloaded) return ORH_E_INVALID;
+  if (!g->d_ovl) return fail(g->ctx, ORH_E_STATE, "orh_graph_device_flags: no graph loaded");
+  *d_overloaded = g->d_ovl;
   return ORH_OK;
 }
 
@@ -982,17 +999,251 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
   return rc;
 }
 
-int orh_route_select(orh_ctx* ctx, uint32_t n_prefix, const uint32_t* d_adv_ptr,
-                     const uint32_t* d_adv, const uint32_t* d_dist, const uint32_t* d_nh,
-                     uint32_t words, uint32_t* d_min, uint32_t* d_nh_out) {
-  if (!ctx) return ORH_E_INVALID;
+// ---- device prefix mirror + route selection ---------------------------------
+}  // extern "C"
+
+struct orh_prefix_set {
+  orh_ctx* ctx = nullptr;
+  // host mirror of the device arrays (compaction and growth)
+  std::vector<uint2> hdr;     // {pool offset, count | prefix flags << 16}
+  std::vector<orh_adv> pool;  // advertisement runs, appended on update
+  uint32_t live = 0;          // records referenced by a header
+  uint2* d_hdr = nullptr;
+  size_t hdr_cap = 0;
+  orh_adv* d_pool = nullptr;
+  size_t pool_cap = 0;
+  uint32_t* d_rank = nullptr;  // name ranks then area ranks
+  size_t rank_cap = 0;
+  uint32_t n_names = 0, n_areas = 0;
+  orh::SelArea* d_areas = nullptr;
+  std::vector<orh::SelArea> h_areas;
+  uint32_t* d_stage = nullptr;
+  size_t stage_cap = 0;  // in u32
+};
+
+namespace {
+
+int grow(orh_ctx* ctx, void** d, size_t* cap, size_t need, size_t elem, size_t keep) {
+  if (need <= *cap) return ORH_OK;
+  const size_t ncap = std::max(need, *cap * 2);
+  void* nd = nullptr;
+  ORH_HIP(ctx, hipMalloc(&nd, ncap * elem));
+  if (*d && keep)
+    ORH_HIP(ctx, hipMemcpyAsync(nd, *d, keep * elem, hipMemcpyDeviceToDevice, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  (void)hipFree(*d);
+  *d = nd;
+  *cap = ncap;
+  return ORH_OK;
+}
+
+int stage(orh_prefix_set* ps, size_t words) {
+  return grow(ps->ctx, reinterpret_cast<void**>(&ps->d_stage), &ps->stage_cap, words, 4, 0);
+}
+
+int upload_all(orh_prefix_set* ps) {
+  orh_ctx* ctx = ps->ctx;
+  int rc = grow(ctx, reinterpret_cast<void**>(&ps->d_hdr), &ps->hdr_cap,
+                std::max<size_t>(ps->hdr.size(), 1), sizeof(uint2), 0);
+  if (rc) return rc;
+  rc = grow(ctx, reinterpret_cast<void**>(&ps->d_pool), &ps->pool_cap,
+            std::max<size_t>(ps->pool.size(), 1), sizeof(orh_adv), 0);
+  if (rc) return rc;
+  if (!ps->hdr.empty())
+    ORH_HIP(ctx, hipMemcpyAsync(ps->d_hdr, ps->hdr.data(), ps->hdr.size() * sizeof(uint2),
+                                hipMemcpyHostToDevice, ctx->stream));
+  if (!ps->pool.empty())
+    ORH_HIP(ctx, hipMemcpyAsync(ps->d_pool, ps->pool.data(), ps->pool.size() * sizeof(orh_adv),
+                                hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return ORH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orh_prefix_create(orh_ctx* ctx, orh_prefix_set** out) {
+  if (!ctx || !out) return ORH_E_INVALID;
+  auto* ps = new (std::nothrow) orh_prefix_set();
+  if (!ps) return ORH_E_NOMEM;
+  ps->ctx = ctx;
+  *out = ps;
+  return ORH_OK;
+}
+
+int orh_prefix_destroy(orh_prefix_set* ps) {
+  if (!ps) return ORH_E_INVALID;
+  hipSetDevice(ps->ctx->device);
+  hipStreamSynchronize(ps->ctx->stream);
+  hipFree(ps->d_hdr);
+  hipFree(ps->d_pool);
+  hipFree(ps->d_rank);
+  hipFree(ps->d_areas);
+  hipFree(ps->d_stage);
+  delete ps;
+  return ORH_OK;
+}
+
+int orh_prefix_load(orh_prefix_set* ps, uint32_t n_prefix, const uint32_t* adv_ptr,
+                    const orh_adv* advs, const uint8_t* pflags) {
+  if (!ps || (n_prefix && (!adv_ptr || !pflags))) return ORH_E_INVALID;
+  orh_ctx* ctx = ps->ctx;
+  const uint32_t n_adv = n_prefix ? adv_ptr[n_prefix] : 0;
+  if (n_adv && !advs) return fail(ctx, ORH_E_INVALID, "orh_prefix_load: null advertisements");
+  for (uint32_t p = 0; p < n_prefix; ++p)
+    if (adv_ptr[p + 1] < adv_ptr[p] || adv_ptr[p + 1] - adv_ptr[p] > 0xFFFFu)
+      return fail(ctx, ORH_E_INVALID, "orh_prefix_load: bad adv_ptr / > 65535 advertisements");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  ps->hdr.resize(n_prefix);
+  for (uint32_t p = 0; p < n_prefix; ++p)
+    ps->hdr[p] = make_uint2(adv_ptr[p], (adv_ptr[p + 1] - adv_ptr[p]) | (uint32_t(pflags[p]) << 16));
+  ps->pool.assign(advs, advs + n_adv);
+  ps->live = n_adv;
+  return upload_all(ps);
+}
+
+int orh_prefix_apply_delta(orh_prefix_set* ps, uint32_t n, const uint32_t* ids,
+                           const uint32_t* adv_ptr, const orh_adv* advs, const uint8_t* pflags) {
+  if (!ps || (n && (!ids || !adv_ptr || !pflags))) return ORH_E_INVALID;
+  if (n == 0) return ORH_OK;
+  orh_ctx* ctx = ps->ctx;
+  const uint32_t n_adv = adv_ptr[n];
+  if (n_adv && !advs) return fail(ctx, ORH_E_INVALID, "orh_prefix_apply_delta: null advertisements");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  uint32_t max_id = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (adv_ptr[i + 1] < adv_ptr[i] || adv_ptr[i + 1] - adv_ptr[i] > 0xFFFFu)
+      return fail(ctx, ORH_E_INVALID, "orh_prefix_apply_delta: bad adv_ptr");
+    max_id = std::max(max_id, ids[i]);
+  }
+  const size_t old_n = ps->hdr.size();
+  if (max_id >= old_n) ps->hdr.resize(static_cast<size_t>(max_id) + 1, make_uint2(0u, 0u));
+  const uint32_t base = static_cast<uint32_t>(ps->pool.size());
+  std::vector<uint2> vals(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint2& h = ps->hdr[ids[i]];
+    ps->live -= h.y & 0xFFFFu;
+    const uint32_t c = adv_ptr[i + 1] - adv_ptr[i];
+    h = make_uint2(base + adv_ptr[i], c | (uint32_t(pflags[i]) << 16));
+    ps->live += c;
+    vals[i] = h;
+  }
+  ps->pool.insert(ps->pool.end(), advs, advs + n_adv);
+  // mostly garbage: rebuild the pool from the live runs and re-upload
+  if (ps->pool.size() > 4096 && ps->pool.size() > 2 * static_cast<size_t>(ps->live)) {
+    std::vector<orh_adv> packed;
+    packed.reserve(ps->live);
+    for (auto& h : ps->hdr) {
+      const uint32_t c = h.y & 0xFFFFu;
+      const uint32_t off = static_cast<uint32_t>(packed.size());
+      packed.insert(packed.end(), ps->pool.begin() + h.x, ps->pool.begin() + h.x + c);
+      h.x = off;
+    }
+    ps->pool.swap(packed);
+    return upload_all(ps);
+  }
+  int rc = grow(ctx, reinterpret_cast<void**>(&ps->d_hdr), &ps->hdr_cap, ps->hdr.size(),
+                sizeof(uint2), old_n);
+  if (rc) return rc;
+  if (ps->hdr.size() > old_n)  // new ids start withdrawn
+    ORH_HIP(ctx, hipMemsetAsync(ps->d_hdr + old_n, 0, (ps->hdr.size() - old_n) * sizeof(uint2),
+                                ctx->stream));
+  rc = grow(ctx, reinterpret_cast<void**>(&ps->d_pool), &ps->pool_cap, std::max<size_t>(ps->pool.size(), 1),
+            sizeof(orh_adv), base);
+  if (rc) return rc;
+  if (n_adv)
+    ORH_HIP(ctx, hipMemcpyAsync(ps->d_pool + base, advs, static_cast<size_t>(n_adv) * sizeof(orh_adv),
+                                hipMemcpyHostToDevice, ctx->stream));
+  // staging: ids[n] (padded to 8 bytes) | headers[n]
+  const size_t id_words = (n + 1) & ~1u;
+  std::vector<uint32_t> st(id_words + 2 * static_cast<size_t>(n));
+  std::copy(ids, ids + n, st.begin());
+  std::memcpy(st.data() + id_words, vals.data(), n * sizeof(uint2));
+  rc = stage(ps, st.size());
+  if (rc) return rc;
+  ORH_HIP(ctx, hipMemcpyAsync(ps->d_stage, st.data(), st.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, orh::launch_scatter_hdr(ps->d_hdr, ps->d_stage,
+                                       reinterpret_cast<const uint2*>(ps->d_stage + id_words), n,
+                                       ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // st is a local
+  return ORH_OK;
+}
+
+int orh_prefix_set_order(orh_prefix_set* ps, uint32_t n_names, const uint32_t* name_rank,
+                         uint32_t n_areas, const uint32_t* area_rank) {
+  if (!ps || (n_names && !name_rank) || (n_areas && !area_rank)) return ORH_E_INVALID;
+  orh_ctx* ctx = ps->ctx;
+  if (n_areas > 256) return fail(ctx, ORH_E_UNSUPPORTED, "orh_prefix_set_order: more than 256 areas");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t words = static_cast<size_t>(n_names) + 256;
+  int rc = grow(ctx, reinterpret_cast<void**>(&ps->d_rank), &ps->rank_cap, words, 4, 0);
+  if (rc) return rc;
+  std::vector<uint32_t> r(words, 0xFFFFFFFFu);
+  std::copy(name_rank, name_rank + n_names, r.begin());
+  std::copy(area_rank, area_rank + n_areas, r.begin() + n_names);
+  ORH_HIP(ctx, hipMemcpyAsync(ps->d_rank, r.data(), words * 4, hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ps->n_names = n_names;
+  ps->n_areas = n_areas;
+  return ORH_OK;
+}
+
+int orh_prefix_info(const orh_prefix_set* ps, uint32_t* n_prefix, uint32_t* n_live, uint32_t* n_pool) {
+  if (!ps) return ORH_E_INVALID;
+  if (n_prefix) *n_prefix = static_cast<uint32_t>(ps->hdr.size());
+  if (n_live) *n_live = ps->live;
+  if (n_pool) *n_pool = static_cast<uint32_t>(ps->pool.size());
+  return ORH_OK;
+}
+
+int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
+                     const orh_select_area* areas, const orh_select_out* out) {
+  if (!ps || !out || (n_areas && !areas)) return ORH_E_INVALID;
+  orh_ctx* ctx = ps->ctx;
+  const uint32_t n_prefix = static_cast<uint32_t>(ps->hdr.size());
   if (n_prefix == 0) return ORH_OK;
-  if (!d_adv_ptr || !d_adv || !d_dist || !d_nh || !d_min || !d_nh_out || words == 0)
-    return fail(ctx, ORH_E_INVALID, "orh_route_select: null argument");
-  hipSetDevice(ctx->device);
-  orh::RouteSelectArgs a{n_prefix, words, d_adv_ptr, d_adv, d_dist, d_nh, d_min, d_nh_out};
+  if (n_areas > orh::kMaxSelectAreas)
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_route_select: more than 32 areas");
+  if (!out->d_status || !out->d_metric || !out->d_best || (out->total_words && !out->d_mask))
+    return fail(ctx, ORH_E_INVALID, "orh_route_select: null output");
+  if (!ps->d_rank) return fail(ctx, ORH_E_STATE, "orh_route_select: orh_prefix_set_order not called");
+  uint32_t words = 0;
+  for (uint32_t b = 0; b < n_areas; ++b) {
+    const orh_select_area& A = areas[b];
+    if (A.d_dist && (!A.d_nh || !A.d_overloaded || !A.d_name_node || A.words == 0))
+      return fail(ctx, ORH_E_INVALID, "orh_route_select: incomplete area");
+    if (A.word_off + A.words > out->total_words)
+      return fail(ctx, ORH_E_INVALID, "orh_route_select: area words exceed total_words");
+    words += A.words;
+  }
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  if (!ps->d_areas) ORH_HIP(ctx, hipMalloc(&ps->d_areas, orh::kMaxSelectAreas * sizeof(orh::SelArea)));
+  ps->h_areas.assign(orh::kMaxSelectAreas, orh::SelArea{});
+  for (uint32_t b = 0; b < n_areas; ++b)
+    ps->h_areas[b] = orh::SelArea{areas[b].present, areas[b].d_dist, areas[b].d_nh, areas[b].d_overloaded,
+                                  areas[b].d_name_node, areas[b].words, areas[b].word_off};
+  ORH_HIP(ctx, hipMemcpyAsync(ps->d_areas, ps->h_areas.data(), n_areas * sizeof(orh::SelArea),
+                              hipMemcpyHostToDevice, ctx->stream));
+  orh::RouteSelectArgs a{};
+  a.n_prefix = n_prefix;
+  a.hdr = ps->d_hdr;
+  a.adv = ps->d_pool;
+  a.name_rank = ps->d_rank;
+  a.area_rank = ps->d_rank + ps->n_names;
+  a.n_names = ps->n_names;
+  a.me_name = me_name;
+  a.flags = flags;
+  a.n_areas = n_areas;
+  a.areas = ps->d_areas;
+  a.status = out->d_status;
+  a.metric = out->d_metric;
+  a.best = out->d_best;
+  a.mask = out->d_mask;
+  a.total_words = out->total_words;
   hipError_t e = orh::launch_route_select(a, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "route_select launch");
+  (void)words;
   return ORH_OK;
 }
 

@@ -181,6 +181,15 @@ class SpfSolver:
     def route_build_runs(self) -> int:
         return self._impl.route_build_runs
 
+    @property
+    def device_selected(self) -> int:
+        """Prefixes of the last build selected by the device kernel (product only)."""
+        return getattr(self._impl, "device_selected", 0)
+
+    @property
+    def host_selected(self) -> int:
+        return getattr(self._impl, "host_selected", 0)
+
 
 class Backend:
     """Bundle of the facade classes bound to one wire-level module."""

@@ -215,3 +215,68 @@ def test_many_workgroups_per_cu(hip, oracle, mode):
                 assert info["variant"] in ((BFS8, BFS16) if max_metric == 1 else (DIST16,)), info
     finally:
         mod.set_spf_mode(0)
+
+
+def test_device_selection_covers_bulk(hip, oracle):
+    """The IP / SP_ECMP prefixes of C3 are selected by route_select_kernel
+    (not the host path), and the result equals both the oracle's and the
+    product's own host-path selection (ORH_HOST_SELECT)."""
+    import os
+    adj_dbs, prefixes = c3_fabric(num_prefixes=20_000)
+    als_h, ps_h = load_topology(hip, adj_dbs, prefixes)
+    als_o, ps_o = load_topology(oracle, adj_dbs, prefixes)
+    me = "2-0-0"
+    sh = hip.spf_solver(me, True, enable_best_route_selection=True)
+    so = oracle.spf_solver(me, True, enable_best_route_selection=True)
+    assert_digests_equal(sh, so, me, als_h, ps_h, als_o, ps_o)
+    assert sh.device_selected >= 20_000 and sh.host_selected == 0
+    os.environ["ORH_HOST_SELECT"] = "1"
+    try:
+        assert_digests_equal(sh, so, me, als_h, ps_h, als_o, ps_o)
+        assert sh.device_selected == 0
+    finally:
+        del os.environ["ORH_HOST_SELECT"]
+
+
+def test_prefix_mirror_incremental(hip, oracle):
+    """Prefix deltas (add, withdraw, metric / forwarding changes, anycast
+    growth) applied in rounds: the device mirror is patched incrementally
+    (orh_prefix_apply_delta, id reuse, pool compaction) and every round's
+    route DB equals the oracle's."""
+    from openr_amd.types import (PrefixEntry, PrefixForwardingAlgorithm, PrefixForwardingType,
+                                 PrefixMetrics, IpPrefix, BinaryAddress)
+    adj_dbs, _ = bench_grid(12)
+    als_h, ps_h = load_topology(hip, adj_dbs, [])
+    als_o, ps_o = load_topology(oracle, adj_dbs, [])
+    nodes = [db.thisNodeName for db in adj_dbs]
+    rng = random.Random(77)
+    live = {}
+
+    def pfx(i):
+        return IpPrefix(BinaryAddress(bytes([0xfd, 1, (i >> 8) & 255, i & 255]) + bytes(12)), 64)
+
+    for rnd in range(30):
+        for _ in range(400):
+            i = rng.randrange(3000)
+            node = rng.choice(nodes)
+            op = rng.random()
+            if op < 0.25 and (i, node) in live:
+                ps_h.delete_prefix(node, A, pfx(i))
+                ps_o.delete_prefix(node, A, pfx(i))
+                del live[(i, node)]
+                continue
+            e = PrefixEntry(pfx(i), metrics=PrefixMetrics(1, rng.randint(0, 2), rng.randint(0, 2),
+                                                            rng.randint(0, 2)))
+            if op > 0.95:
+                e.forwardingType = PrefixForwardingType.SR_MPLS
+            if op > 0.98:
+                e.forwardingAlgorithm = PrefixForwardingAlgorithm.KSP2_ED_ECMP
+            ps_h.update_prefix(node, A, e)
+            ps_o.update_prefix(node, A, e)
+            live[(i, node)] = e
+        me = str(rng.randrange(144))
+        best = rnd % 2 == 1
+        sh = hip.spf_solver(me, True, enable_best_route_selection=best)
+        so = oracle.spf_solver(me, True, enable_best_route_selection=best)
+        assert_digests_equal(sh, so, me, als_h, ps_h, als_o, ps_o)
+        assert sh.device_selected > 0
