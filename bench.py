@@ -3,18 +3,27 @@
 
 Workload (BASELINE.json configs[1]): the benchmark grid
 createGrid(n=100, 1 prefix, SP_ECMP) of RoutingBenchmarkUtils.cpp:271-313,
-N = 10,000 nodes, E = 39,600 directed adjacencies, unit metrics. One step is
-one all-sources sweep: LinkState::runSpf from every node (dist row + ECMP
-first-hop mask row per source, written to HBM), with the CSR mirror already
-resident in HBM. With --gpus N (torch.distributed.run, one rank per GPU) the
-10,000 sources are split into contiguous blocks; no collective touches the
-data path (timing only: barrier + max over ranks).
+N = 10,000 nodes, E = 39,600 directed adjacencies, unit metrics. One sweep is
+LinkState::runSpf from every node (dist row + ECMP first-hop mask row per
+source, written to HBM) with the CSR mirror already resident in HBM.
+
+A step (--scaling):
+  whatif (default)  a fixed batch of --topologies what-if variants of the grid
+                    (variant 0 the grid itself, variant t > 0 the grid with one
+                    seeded link drained), every one swept from all 10,000
+                    sources; the variants are split over the ranks (strong
+                    scaling: total work fixed, no data-path collective)
+  strong            one topology, its 10,000 sources split into contiguous
+                    degree-weighted blocks over the ranks
+  weak              every rank sweeps all sources of its own variant
+With --gpus N the driver starts one process per GPU (torch.distributed.run);
+the only cross-rank traffic is the barrier and the max-over-ranks time.
 
 Also reported: buildRouteDb("1") ms (cold: right after a topology-changing
 adjacency update, so it includes the device mirror patch and the SPF; warm:
-memoized SPF), the dominant kernel's HBM roofline figures, and the CPU
-oracle (a port of the reference algorithm with its data structures) timed on
-a bounded sample of the same workload on this host.
+memoized SPF), the dominant kernels' HBM roofline figures, and the CPU oracle
+(a port of the reference algorithm with its data structures) timed on a
+bounded sample of the same workload on this host.
 """
 import argparse
 import json
@@ -37,11 +46,15 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--grid", type=int, default=100)
+    p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
+    p.add_argument("--topologies", type=int, default=8,
+                   help="what-if variants per step (--scaling whatif)")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="oracle threads (0: every CPU this process may use)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-route-db", action="store_true")
-    p.add_argument("--legs", default="c1,c3,c4",
+    p.add_argument("--legs", default="c1,c3,c4,c5",
                    help="extra BASELINE configs reported under 'legs' (c1,c3,c4,c5; '' for none)")
     return p.parse_args()
 
@@ -88,73 +101,109 @@ def main():
 
     from openr_amd import host_backend
     from openr_amd.facade import load_topology
+    from openr_amd.sharding import degree_weighted_sources, shard_bounds
     from openr_amd.topology import bench_grid
     from openr_amd.types import K_TESTING_AREA
 
     n = args.grid
-    adj_dbs, prefixes = bench_grid(n, 1)
-    if rank > 0:
-        # weak scaling: rank r sweeps all sources of its own what-if topology,
-        # the grid with one seeded link drained (LinkState overload bit on
-        # both adjacencies), so per-GPU work is fixed as N grows
-        drain_what_if_link(adj_dbs, n, rank)
-    hip = host_backend()
-    als, ps = load_topology(hip, adj_dbs, prefixes)
-    ls = als[K_TESTING_AREA]
     names = [str(i) for i in range(n * n)]
-    mine = names
-    sweep = ls._impl.sweep(mine, True)
+    hip = host_backend()
+    # (variant, sources) units of this rank
+    if args.scaling == "whatif":
+        T = max(1, args.topologies)
+        lo, hi = shard_bounds(T, world, rank)
+        units = [(t, names) for t in range(lo, hi)]
+        total_units = T * n * n
+    elif args.scaling == "strong":
+        units = [(0, None)]  # sources picked below (degree-weighted block)
+        total_units = n * n
+    else:
+        units = [(rank, names)]
+        total_units = n * n * world
+    sweeps, base = [], None
+    for t, srcs in units:
+        adj_dbs, prefixes = bench_grid(n, 1)
+        if t > 0:
+            drain_what_if_link(adj_dbs, n, t)
+        als, ps = load_topology(hip, adj_dbs, prefixes)
+        ls = als[K_TESTING_AREA]
+        if srcs is None:
+            degrees = [len(db.adjacencies) for db in adj_dbs]
+            srcs = degree_weighted_sources(names, degrees, world, rank)
+        sweeps.append((t, srcs, ls, ls._impl.sweep(srcs, True) if srcs else None))
+        if t == 0:
+            base = (adj_dbs, prefixes, als, ps, ls)
+
+    def run_all():
+        for _, _, _, sw in sweeps:
+            if sw is not None:
+                sw.run()  # asynchronous on the context stream
+
+    def sync_all():
+        for _, _, _, sw in sweeps:
+            if sw is not None:
+                sw.sync()
 
     for _ in range(args.warmup):
-        sweep.run()
-    sweep.sync()
+        run_all()
+    sync_all()
 
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sweep.run()  # asynchronous on the context stream
-    sweep.sync()
+        run_all()
+    sync_all()
     torch.cuda.synchronize()
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
 
-    # device time of one launch pair (HIP events on the sweep's own stream),
-    # measured outside the timed region
+    # device time of one sweep's launches (HIP events on the sweep's own
+    # stream), measured outside the timed region
+    probe = next((sw for _, srcs, _, sw in sweeps if sw is not None and len(srcs) == n * n),
+                 next((sw for *_, sw in sweeps if sw is not None), None))
     kernel_ms, phases = [], []
-    for _ in range(max(3, min(args.steps, 10))):
-        sweep.run()
-        kernel_ms.append(sweep.last_ms())
-        phases.append(sweep.phase_ms())
+    if probe is not None:
+        for _ in range(max(3, min(args.steps, 10))):
+            probe.run()
+            kernel_ms.append(probe.last_ms())
+            phases.append(probe.phase_ms())
 
-    total_sources = n * n * args.steps * world  # all ranks together
-    value = total_sources / elapsed
+    value = total_units * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
     # size-independent correctness check on the timed output: unit metrics,
-    # so dist(src, v) is the Manhattan distance on the grid
-    node_ids = {name: i for i, name in enumerate(ls._impl.node_names())}
+    # so dist(src, v) is the Manhattan distance on the undrained grid
     import numpy as np
-    ids = np.array([node_ids[str(v)] for v in range(n * n)])
     rr, cc = np.divmod(np.arange(n * n), n)
-    for i in (0, len(mine) // 2, len(mine) - 1) if rank == 0 else ():
-        s = int(mine[i])
-        dist_row, _ = sweep.fetch(i)
-        if not np.array_equal(dist_row[ids], np.abs(rr - rr[s]) + np.abs(cc - cc[s])):
-            raise SystemExit(f"bench: wrong distances for source {s}")
+    for t, srcs, ls, sw in sweeps:
+        if t != 0 or sw is None:
+            continue
+        node_ids = {name: i for i, name in enumerate(ls._impl.node_names())}
+        ids = np.array([node_ids[str(v)] for v in range(n * n)])
+        for i in (0, len(srcs) // 2, len(srcs) - 1):
+            s_ = int(srcs[i])
+            dist_row, _ = sw.fetch(i)
+            if not np.array_equal(dist_row[ids], np.abs(rr - rr[s_]) + np.abs(cc - cc[s_])):
+                raise SystemExit(f"bench: wrong distances for source {s_}")
 
     if rank != 0:
         barrier()
         return
 
-    # roofline of the SPF kernel: B = 4(N+1) + 8E + N(4D + 4W)
-    N, E, W = sweep.nodes, sweep.edges, sweep.words
+    # roofline of the sweep: B = 4(N+1) + 8E + N(4D + 4W)
+    N, E, W = probe.nodes, probe.edges, probe.words
+    srcs_probe = probe.sources
     bytes_per_source = 4 * (N + 1) + 8 * E + N * (4 * 1 + 4 * W)
-    per_launch = bytes_per_source * len(mine)
+    per_launch = bytes_per_source * srcs_probe
     kms = statistics.mean(kernel_ms)
     achieved = per_launch / (kms * 1e-3) / 1e9
+    out_bytes = srcs_probe * N * (4 + 4 * W)  # the dist + first-hop rows alone
 
     traffic, traffic_src = pmc_traffic()
+    parallelism = {"whatif": f"{args.topologies} what-if variants split over {world} rank(s)",
+                   "strong": f"one topology, sources in {world} degree-weighted block(s)",
+                   "weak": f"{world} variant(s), one per rank"}[args.scaling]
     out = {
         "metric": "all-source SPF runs/sec + buildRouteDb ms on 10k-node topology",
         "value": round(value, 1),
@@ -164,23 +213,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.scaling == "weak" else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: reference benchmark grid generator (createGrid n=100)",
         "config": {"workload": f"C2 {n}x{n} grid all-sources SPF (N={N}, E={E})",
-                   "sources_per_step_per_gpu": n * n,
-                   "parallelism": f"what-if topologies x{world} (rank r > 0: one seeded link drained)"},
+                   "step": (f"{args.topologies} x {n * n} sources" if args.scaling == "whatif"
+                            else f"{total_units} sources"),
+                   "parallelism": parallelism},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel_ms": round(kms, 4),
                      "phase_ms": [round(statistics.mean(p[0] for p in phases), 4),
                                   round(statistics.mean(p[1] for p in phases), 4)],
-                     "algorithmic_bytes_per_source": bytes_per_source},
+                     "algorithmic_bytes_per_source": bytes_per_source,
+                     "sources_per_launch": srcs_probe,
+                     "output_floor": {"bytes": out_bytes,
+                                      "frac": round(out_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
     }
 
-    if not args.no_route_db:
+    if not args.no_route_db and base is not None:
+        adj_dbs, prefixes, als, ps, ls = base
         solver = hip.spf_solver("1", True)
         solver.build_route_db("1", als, ps)
         db = adj_dbs[n * n // 2]
@@ -198,8 +252,8 @@ def main():
         db.adjacencies[0].metric = 1
         ls.update_adjacency_database(db)
 
-    if world == 1 and not args.no_cpu_baseline:
-        out.update(cpu_baseline(args, adj_dbs, prefixes, n, value))
+    if world == 1 and not args.no_cpu_baseline and base is not None:
+        out.update(cpu_baseline(args, base[0], base[1], n, value))
     if world == 1 and args.legs:
         import bench_legs
         out["legs"] = bench_legs.run(args.legs.split(","), hip, not args.no_cpu_baseline)
@@ -208,7 +262,11 @@ def main():
     barrier()
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "v6_pmc.json")
+# newest committed PMC summary of this command (tools/profile.sh +
+# tools/pmc_summary.py), per sweep launch
+PMC_PROFILES = [os.path.join(ROOT, "profiles", "r02", "pmc.json"),
+                os.path.join(ROOT, "profiles", "r01", "v6_pmc.json")]
+PMC_PROFILE = next((p for p in PMC_PROFILES if os.path.exists(p)), PMC_PROFILES[-1])
 SWEEP_KERNELS = ("spf_msbfs_kernel", "ms_finalize_kernel", "first_hop_lvl_kernel")
 
 
@@ -235,6 +293,22 @@ def pmc_traffic():
     return round(total), os.path.relpath(PMC_PROFILE, ROOT) + ": " + " + ".join(seen)
 
 
+def cgroup_cpu_quota():
+    """CPUs allowed by the cgroup v2 cpu.max quota (None: no quota)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus():
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    return min(n, q) if q else n
+
+
 def host_info():
     """CPU model and core counts of this host (BASELINE.md reporting rules)."""
     model = "unknown"
@@ -247,7 +321,7 @@ def host_info():
     except OSError:
         pass
     return {"model": model, "nproc": os.cpu_count(),
-            "affinity": len(os.sched_getaffinity(0)),
+            "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": cgroup_cpu_quota(),
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -264,8 +338,11 @@ def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
     step = max(1, (n * n) // args.cpu_sample)
     sample = [str(i) for i in range(0, n * n, step)][:args.cpu_sample]
     sec1, _ = ls._impl.time_spf_sources(sample, 1)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    sample_mt = sample * min(threads, 4)
+    usable = usable_cpus()
+    threads = max(1, min(args.cpu_threads or usable, usable))
+    # >= cpu_sample sources and >= 2 per thread, evenly spaced over the grid
+    k = max(args.cpu_sample, 2 * threads)
+    sample_mt = [str((i * (n * n)) // k) for i in range(k)]
     secn, _ = ls._impl.time_spf_sources(sample_mt, threads)
     solver = oracle.spf_solver("1", True)
     db = adj_dbs[n * n // 2]
@@ -284,9 +361,15 @@ def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
     return {
         "cpu_baseline": {"value": round(vn, 2), "unit": "SPF-sources/s", "cores": threads,
                          "kind": "port",
-                         "sample": f"{len(sample_mt)} runSpf calls ({len(sample)} evenly spaced "
-                                   f"sources x {threads} threads, one deep LinkState copy per "
-                                   f"thread), extrapolated per source"},
+                         "sample": f"{len(sample_mt)} evenly spaced sources of the 10k grid, "
+                                   f"runSpf on {threads} threads (every CPU this process may "
+                                   f"use: affinity {len(os.sched_getaffinity(0))}, cgroup quota "
+                                   f"{cgroup_cpu_quota()}), one deep LinkState copy per thread"},
+        "cpu_baseline_per_core": round(vn / threads, 2),
+        "cpu_baseline_all_cores_linear": {
+            "value": round(vn / threads * (os.cpu_count() or threads), 1),
+            "cores": os.cpu_count(),
+            "note": "per-core rate x nproc (linear extrapolation, not measured)"},
         "cpu_baseline_1t": {"value": round(v1, 2), "unit": "SPF-sources/s", "cores": 1,
                             "kind": "port", "sample": f"{len(sample)} sources"},
         "cpu_build_route_db_ms": round(brdb, 2),

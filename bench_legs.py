@@ -31,6 +31,19 @@ def _route_ms(solver, me, als, ps, reps):
                              for _ in range(reps))
 
 
+def _select_roofline(solver, me, als, ps):
+    """Route-selection kernel of one build: device time and B_sel roofline."""
+    solver._impl.time_build_route_db(me, als._impl, ps._impl)
+    ms = solver._impl.last_select_ms
+    b = solver._impl.last_select_bytes
+    if ms <= 0:
+        return {"select_kernel": None}
+    gbs = b / (ms * 1e-3) / 1e9
+    return {"select_kernel": {"ms": round(ms, 4), "bytes": b, "achieved_gbs": round(gbs, 1),
+                              "frac": round(gbs / 8000.0, 4),
+                              "prefixes_selected_on_device": solver._impl.device_selected}}
+
+
 def leg_c1(hip, cpu):
     from openr_amd.facade import load_topology
     from openr_amd.topology import bench_grid
@@ -68,6 +81,19 @@ def leg_c3(hip, cpu):
            "build_route_db_ms": round(_route_ms(hip.spf_solver(me, True), me, als, ps, 5), 3),
            "build_route_db_best_route_ms": round(_route_ms(
                hip.spf_solver(me, True, enable_best_route_selection=True), me, als, ps, 5), 3)}
+    out.update(_select_roofline(hip.spf_solver(me, True, enable_best_route_selection=True),
+                                me, als, ps))
+    # prefix-sharded build (route selection sharded over 8
+    # GPUs): each shard's build timed here, one after the other on this GPU;
+    # on an 8-GPU node each runs on its own GPU, so the per-GPU time is the max
+    shard_ms = []
+    for r in range(8):
+        s8 = hip.spf_solver(me, True)
+        s8._impl.set_prefix_shard(r, 8)
+        shard_ms.append(_route_ms(s8, me, als, ps, 3))
+    out["build_route_db_8_prefix_shards_max_ms"] = round(max(shard_ms), 3)
+    out["build_route_db_8_prefix_shards_note"] = ("8 prefix shards built one after the other on "
+                                                  "this GPU; max shard time = per-GPU time at 8")
     if cpu:
         o = _oracle()
         als_o, ps_o = load_topology(o, adj, pfx)
@@ -110,10 +136,13 @@ def leg_c4(hip, cpu, n_links=64, n_srcs=16, n_ksp=256):
     if cpu:
         o = _oracle()
         als_o, _ = load_topology(o, adj, [])
-        t0 = time.perf_counter()
-        sec, _ = als_o[A]._impl.time_spf_sources([pairs[0][0]], 1)
-        out["cpu_spfs_per_s"] = round(1.0 / sec, 4)
-        out["cpu_sample"] = "1 runSpf on the 50k-node WAN, 1 thread (reference DijkstraQ re-heap)"
+        k = 8
+        threads = min(k, os.cpu_count() or 1)
+        sample = [s for s, _ in pairs[:k]]
+        sec, _ = als_o[A]._impl.time_spf_sources(sample, threads)
+        out["cpu_spfs_per_s"] = round(k / sec, 4)
+        out["cpu_sample"] = (f"{k} runSpf on the 50k-node WAN on {threads} threads "
+                             "(reference DijkstraQ re-heap), per-thread LinkState copies")
     return out
 
 
@@ -130,6 +159,31 @@ def leg_c5(hip, cpu):
     out = {"workload": f"C5 4 areas x {len(areas['A'])} nodes, {len(pfx)} prefix advertisements",
            "load_s": round(load_s, 2),
            "build_route_db_ms": round(_route_ms(solver, "me", als, ps, 3), 2)}
+    out.update(_select_roofline(solver, "me", als, ps))
+    # incremental stress: 10k prefix add / withdraw
+    # advertisements plus 100 adjacency-metric changes, then one rebuild
+    import random
+    from openr_amd.types import PrefixEntry, PrefixMetrics
+    rng = random.Random(55)
+    t0 = time.perf_counter()
+    for i in range(10_000):
+        node, area, e = pfx[rng.randrange(len(pfx))]
+        if i % 2:
+            ps.delete_prefix(node, area, e.prefix)
+        else:
+            ps.update_prefix(node, area, PrefixEntry(e.prefix, metrics=PrefixMetrics(
+                1, rng.randint(0, 3), rng.randint(0, 3), rng.randint(0, 3)), tags=e.tags))
+    for _ in range(100):
+        a = rng.choice(C5_AREAS)
+        db = areas[a][rng.randrange(len(areas[a]) - 1)]
+        db.adjacencies[rng.randrange(len(db.adjacencies))].metric = rng.randint(1, 4)
+        als[a].update_adjacency_database(db)
+    upd_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    solver._impl.time_build_route_db("me", als._impl, ps._impl)
+    out["incremental"] = {"updates": "10k prefix add/withdraw + 100 adjacency metric changes",
+                          "apply_s": round(upd_s, 3),
+                          "rebuild_ms": round((time.perf_counter() - t0) * 1e3, 2)}
     policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
         0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
     build_s, policy_s, routes, updated = solver._impl.time_build_route_db_with_policy(

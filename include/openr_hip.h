@@ -276,6 +276,8 @@ typedef struct orh_select_out {
 /* asynchronous on the context stream; the area table is copied */
 int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
                      const orh_select_area* h_areas, const orh_select_out* out);
+/* device time of the last orh_route_select kernel (HIP events; waits for it) */
+int orh_last_select_ms(orh_prefix_set* ps, double* ms_out);
 
 #ifdef __cplusplus
 }

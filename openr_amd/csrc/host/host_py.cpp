@@ -809,6 +809,9 @@ PYBIND11_MODULE(_openr_host, m) {
              s.updateStaticMplsRoutes(u, del);
            })
       .def_property_readonly("route_build_runs", &SpfSolver::routeBuildRuns)
+      .def("set_prefix_shard", &SpfSolver::setPrefixShard, py::arg("rank"), py::arg("world"))
+      .def_property_readonly("last_select_ms", &SpfSolver::lastSelectMs)
+      .def_property_readonly("last_select_bytes", &SpfSolver::lastSelectBytes)
       .def_property_readonly("device_selected", &SpfSolver::deviceSelected)
       .def_property_readonly("host_selected", &SpfSolver::hostSelected);
 

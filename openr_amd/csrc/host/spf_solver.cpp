@@ -159,6 +159,12 @@ SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool enableOrderedFib
       bgpDryRun_(bgpDryRun),
       enableBestRouteSelection_(enableBestRouteSelection) {}
 
+void SpfSolver::setPrefixShard(uint32_t rank, uint32_t world) {
+  if (world == 0 || rank >= world) throw std::invalid_argument("setPrefixShard: bad rank / world");
+  shardRank_ = rank;
+  shardWorld_ = world;
+}
+
 SpfSolver::~SpfSolver() {
   for (auto& w : areaWork_) {
     if (w.dNameNode) orh_device_free(selCtx_, w.dNameNode);
@@ -601,7 +607,11 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
                                const PrefixState& ps) {
   deviceSelected_ = hostSelected_ = 0;
   if (std::getenv("ORH_HOST_SELECT")) return false;  // A/B switch: host selection
-  if (ps.numPrefixIds() == 0 || als.empty()) return false;
+  // below ORH_DEVICE_SELECT_MIN prefixes (default 1024) the launch and the
+  // row uploads cost more than selecting on the host (C1: 100 prefixes)
+  size_t minPrefixes = 1024;
+  if (const char* e = std::getenv("ORH_DEVICE_SELECT_MIN")) minPrefixes = std::strtoull(e, nullptr, 10);
+  if (ps.numPrefixIds() == 0 || ps.numPrefixIds() < minPrefixes || als.empty()) return false;
   orh_ctx* ctx = als.begin()->second.context();
   for (const auto& [_, ls] : als)
     if (ls.context() != ctx) return false;
@@ -735,6 +745,14 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   if (orh_route_select(set, meName ? *meName : ORH_NO_NODE, flags,
                        static_cast<uint32_t>(order.size()), sel.data(), &out) != ORH_OK)
     throw std::runtime_error(std::string("orh_route_select: ") + orh_last_error(ctx));
+  {
+    uint32_t np = 0, live = 0;
+    orh_prefix_info(set, &np, &live, nullptr);
+    uint32_t areasWithRow = 0;
+    for (const auto& sa : sel) areasWithRow += sa.d_dist ? 1 : 0;
+    lastSelectBytes_ = 8ull * np + 20ull * live + 4ull * live * areasWithRow +
+        static_cast<uint64_t>(np) * (9 + 4ull * words);
+  }
   selStatus_.resize(n);
   selMetric_.resize(n);
   selBest_.resize(n);
@@ -745,6 +763,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
       orh_memcpy_d2h(ctx, selBest_.data(), out.d_best, 4ull * n) != ORH_OK ||
       orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
     throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
+  if (orh_last_select_ms(set, &lastSelectMs_) != ORH_OK) lastSelectMs_ = -1;
   return true;
 }
 
@@ -829,6 +848,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // as ORH_SEL_HOST (BGP, SR_MPLS / KSP2, minNexthop, self-advertised)
   const bool dev = selectOnDevice(me, als, ps);
   prof.mark("select (device)");
+  bool labelsDone = false;  // node-label routes built by the pipelined path
   std::vector<const Cidr*> keys;
   if (dev) {
     const uint32_t n = ps.numPrefixIds();
@@ -840,7 +860,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     deviceSelected_ = nDev;
     hostSelected_ = nHost;
     auto one = [&](uint32_t pid, decltype(db.unicastRoutes)& out) {
-      if (!ps.prefixLive(pid)) return;
+      if (!ps.prefixLive(pid) || !ownsPid(pid, n)) return;
       if (selStatus_[pid] == ORH_SEL_ROUTE) {
         RibUnicastEntry e = materialize(pid, ps);
         Cidr k = e.prefix;
@@ -852,7 +872,97 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
         }
       }
     };
-    if (!hasKsp && n >= kParallelMin && pool.size() > 1) {
+    // one area with nexthop templates: unicast routes and node-label
+    // candidates in one pool pass, then the two output maps are assembled
+    // concurrently (their insertion is the sequential part of the build)
+    const AreaWork* tw = nullptr;
+    if (als.size() == 1)
+      for (const auto& w : areaWork_)
+        if (w.ls == &als.begin()->second && w.words) tw = &w;
+    if (!hasKsp && tw && shardWorld_ == 1 && n >= kParallelMin && pool.size() > 1) {
+      const auto& [area, ls] = *als.begin();
+      const SpfRow& myRow = ls.getSpfResult(me);
+      std::vector<const AdjacencyDatabase*> dbs;
+      dbs.reserve(ls.getAdjacencyDatabases().size());
+      for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
+      std::vector<std::optional<RibMplsEntry>> cand(dbs.size());
+      auto label = [&, &area = area, &ls = ls](size_t i) {
+        const AdjacencyDatabase& adjDb = *dbs[i];
+        const int32_t lbl = adjDb.nodeLabel;
+        if (lbl == 0 || !isMplsLabelValid(lbl)) return;
+        RibMplsEntry entry{lbl, {}};
+        if (adjDb.thisNodeName == me) {  // POP_AND_LOOKUP (Decision.cpp:690-703)
+          NextHopThrift nh;
+          nh.address.addr = std::string(16, '\0');
+          nh.area = area;
+          nh.mplsAction = mpls(kPopAndLookup);
+          entry.nexthops.insert(std::move(nh));
+        } else {
+          auto v = ls.nodeId(adjDb.thisNodeName);
+          if (!v || !myRow.reachable(*v)) return;
+          const int32_t metric = static_cast<int32_t>(myRow.metric(*v));
+          bool any = false;
+          for (uint32_t k = 0; k < tw->words; ++k) {
+            for (uint32_t bits = myRow.nh[static_cast<size_t>(*v) * tw->words + k]; bits;
+                 bits &= bits - 1) {
+              any = true;
+              const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
+              for (const auto& t : tw->tmpl6[b]) {
+                NextHopThrift nh = t;
+                nh.metric = metric;
+                nh.mplsAction = *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
+                                                                           : mpls(kSwap, lbl);
+                entry.nexthops.insert(std::move(nh));
+              }
+            }
+          }
+          if (!any) return;
+        }
+        cand[i] = std::move(entry);
+      };
+      std::vector<decltype(db.unicastRoutes)> parts(pool.size());
+      pool.parallelFor(n + dbs.size(), [&](size_t w, size_t b, size_t e) {
+        parts[w].reserve(parts[w].size() + (std::min<size_t>(e, n) - std::min<size_t>(b, n)));
+        for (size_t i = b; i < e; ++i) {
+          if (i < n) one(static_cast<uint32_t>(i), parts[w]);
+          else label(i - n);
+        }
+      });
+      prof.mark("unicast + labels (pool)");
+      pool.parallelFor(2, [&](size_t, size_t b, size_t e) {
+        for (size_t c = b; c < e; ++c) {
+          if (c == 0) {
+            for (auto& part : parts) {
+              db.unicastRoutes.merge(part);
+              if (!part.empty()) throw std::logic_error("duplicate unicast route");
+            }
+            for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
+              if (db.unicastRoutes.count(prefix)) continue;
+              RibUnicastEntry se;
+              se.prefix = prefix;
+              se.nexthops.insert(nhs.begin(), nhs.end());
+              db.unicastRoutes.emplace(prefix, std::move(se));
+            }
+          } else {
+            // duplicate labels: the smaller node name wins (:675-688)
+            std::unordered_map<int32_t, std::pair<const std::string*, size_t>> win;
+            win.reserve(dbs.size());
+            for (size_t i = 0; i < dbs.size(); ++i) {
+              const int32_t lbl = dbs[i]->nodeLabel;
+              if (lbl == 0 || !isMplsLabelValid(lbl)) continue;
+              auto it = win.find(lbl);
+              if (it != win.end() && *it->second.first < dbs[i]->thisNodeName) continue;
+              if (!cand[i]) continue;
+              win[lbl] = {&dbs[i]->thisNodeName, i};
+            }
+            db.mplsRoutes.reserve(win.size() + 64);
+            for (auto& [lbl, w] : win) db.mplsRoutes.emplace(lbl, std::move(*cand[w.second]));
+          }
+        }
+      });
+      prof.mark("unicast merge || label map");
+      labelsDone = true;
+    } else if (!hasKsp && n >= kParallelMin && pool.size() > 1) {
       std::vector<decltype(db.unicastRoutes)> parts(pool.size());
       pool.parallelFor(n, [&](size_t w, size_t b, size_t e) {
         parts[w].reserve(parts[w].size() + (e - b));
@@ -868,7 +978,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     }
   } else {
     keys.reserve(ps.prefixes().size());
-    for (const auto& [prefix, _] : ps.prefixes()) keys.push_back(&prefix);
+    const uint32_t n = ps.numPrefixIds();
+    for (const auto& [prefix, _] : ps.prefixes())
+      if (shardWorld_ == 1 || ownsPid(*ps.pidOf(prefix), n)) keys.push_back(&prefix);
   }
   if (dev) {
     // routes built above
@@ -897,24 +1009,38 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       }
     }
   }
-  for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
-    if (db.unicastRoutes.count(prefix)) continue;
-    RibUnicastEntry e;
-    e.prefix = prefix;
-    e.nexthops.insert(nhs.begin(), nhs.end());
-    db.unicastRoutes.emplace(prefix, std::move(e));
+  if (!labelsDone) {
+    for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
+      if (db.unicastRoutes.count(prefix)) continue;
+      if (shardWorld_ > 1) {  // the shard of its prefix id, shard 0 if PrefixState lacks it
+        auto pid = ps.pidOf(prefix);
+        if (pid ? !ownsPid(*pid, ps.numPrefixIds()) : shardRank_ != 0) continue;
+      }
+      RibUnicastEntry e;
+      e.prefix = prefix;
+      e.nexthops.insert(nhs.begin(), nhs.end());
+      db.unicastRoutes.emplace(prefix, std::move(e));
+    }
+    prof.mark("unicast merge");
   }
-
-  prof.mark("unicast merge");
   // node-label routes; duplicate labels resolve to the smaller node name.
   // The candidate entry of every adjacency database is computed on the
   // worker pool, then the duplicate resolution walks them in the reference's
   // iteration order (Decision.cpp:655-744).
   std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
   for (const auto& [area, ls] : als) {
+    if (labelsDone || shardRank_ != 0) break;
     std::vector<const AdjacencyDatabase*> dbs;
     for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
     std::vector<std::optional<RibMplsEntry>> cand(dbs.size());
+    // one area with device-selection templates: the route to node v is its
+    // first-hop mask in me's row, each bit's tight links with PHP when the
+    // neighbour is v, else SWAP(label) (getNextHopsThrift, :1278-1287)
+    const AreaWork* tw = nullptr;
+    if (dev && als.size() == 1)
+      for (const auto& w : areaWork_)
+        if (w.ls == &ls && w.words) tw = &w;
+    const SpfRow* myRow = tw ? &ls.getSpfResult(me) : nullptr;
     auto compute = [&, &area = area, &ls = ls](size_t i) {
       const AdjacencyDatabase& adjDb = *dbs[i];
       const int32_t label = adjDb.nodeLabel;
@@ -926,6 +1052,26 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
         nh.area = area;
         nh.mplsAction = mpls(kPopAndLookup);
         entry.nexthops.insert(std::move(nh));
+      } else if (tw) {
+        auto v = ls.nodeId(adjDb.thisNodeName);
+        if (!v || !myRow->reachable(*v)) return;
+        const int32_t metric = static_cast<int32_t>(myRow->metric(*v));
+        bool any = false;
+        for (uint32_t k = 0; k < tw->words; ++k) {
+          for (uint32_t bits = myRow->nh[static_cast<size_t>(*v) * tw->words + k]; bits;
+               bits &= bits - 1) {
+            any = true;
+            const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
+            for (const auto& t : tw->tmpl6[b]) {
+              NextHopThrift nh = t;
+              nh.metric = metric;
+              nh.mplsAction = *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
+                                                                         : mpls(kSwap, label);
+              entry.nexthops.insert(std::move(nh));
+            }
+          }
+        }
+        if (!any) return;
       } else {
         const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};
         if (als.size() == 1 && ls.nodeId(me)) {
@@ -976,6 +1122,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
 
   // adjacency-label routes for all my links, up or not (:749-775)
   for (const auto& [_, ls] : als) {
+    if (shardRank_ != 0) break;
     auto myId = ls.nodeId(me);
     if (!myId) continue;
     for (uint32_t lid : ls.linksFromNode(me)) {
@@ -991,6 +1138,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     }
   }
   for (const auto& [label, nhs] : staticMplsRoutes_) {
+    if (shardRank_ != 0) break;
     RibMplsEntry e{label, {}};
     e.nexthops.insert(nhs.begin(), nhs.end());
     if (!db.mplsRoutes.emplace(label, std::move(e)).second)

@@ -57,6 +57,11 @@ class PrefixState {
     *n = run_[pid].second;
     return advPool_.data() + run_[pid].first;
   }
+  std::optional<uint32_t> pidOf(const Cidr& prefix) const {
+    auto it = pid_.find(prefix);
+    if (it == pid_.end()) return std::nullopt;
+    return it->second;
+  }
   std::optional<uint32_t> nameId(const std::string& n) const;
   uint32_t numNames() const { return static_cast<uint32_t>(names_.size()); }
   const std::string& name(uint32_t id) const { return names_[id]; }
@@ -128,7 +133,18 @@ class SpfSolver {
   // prefixes of the last buildRouteDb whose selection ran on the device /
   // took the host path (BGP, SR_MPLS, KSP2, minNexthop, self-advertised)
   uint64_t deviceSelected() const { return deviceSelected_; }
+  // prefix sharding over `world` route builders: this
+  // solver builds the unicast routes of the prefix ids in its contiguous
+  // block (and the static routes of prefixes it owns); node-label, adj-label
+  // and static MPLS routes are built by shard 0. The union of the shards'
+  // databases is the unsharded database.
+  void setPrefixShard(uint32_t rank, uint32_t world);
   uint64_t hostSelected() const { return hostSelected_; }
+  // device time of the last build's selection kernel and its algorithmic
+  // bytes (B_sel: headers 8 B + records 20 B per advertisement + per
+  // advertisement and area a 4 B distance gather + outputs 9 + 4 W bytes)
+  double lastSelectMs() const { return lastSelectMs_; }
+  uint64_t lastSelectBytes() const { return lastSelectBytes_; }
   ~SpfSolver();
 
  private:
@@ -196,6 +212,16 @@ class SpfSolver {
   std::vector<uint32_t> selMetric_, selBest_, selMask_;
   uint32_t selWords_{0};
   uint64_t deviceSelected_{0}, hostSelected_{0};
+  uint32_t shardRank_{0}, shardWorld_{1};
+  double lastSelectMs_{0};
+  uint64_t lastSelectBytes_{0};
+  bool ownsPid(uint32_t pid, uint32_t n) const {
+    if (shardWorld_ <= 1) return true;
+    const uint64_t base = n / shardWorld_, rem = n % shardWorld_;
+    const uint64_t lo = shardRank_ * base + std::min<uint64_t>(shardRank_, rem);
+    const uint64_t hi = lo + base + (shardRank_ < rem ? 1 : 0);
+    return pid >= lo && pid < hi;
+  }
 
   std::unordered_map<int32_t, std::vector<NextHopThrift>> staticMplsRoutes_;
   std::unordered_map<Cidr, std::vector<NextHopThrift>, CidrHash> staticUnicastRoutes_;

@@ -1019,6 +1019,7 @@ struct orh_prefix_set {
   std::vector<orh::SelArea> h_areas;
   uint32_t* d_stage = nullptr;
   size_t stage_cap = 0;  // in u32
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the last route_select launch
 };
 
 namespace {
@@ -1081,6 +1082,8 @@ int orh_prefix_destroy(orh_prefix_set* ps) {
   hipFree(ps->d_rank);
   hipFree(ps->d_areas);
   hipFree(ps->d_stage);
+  if (ps->ev0) hipEventDestroy(ps->ev0);
+  if (ps->ev1) hipEventDestroy(ps->ev1);
   delete ps;
   return ORH_OK;
 }
@@ -1241,9 +1244,25 @@ int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint3
   a.best = out->d_best;
   a.mask = out->d_mask;
   a.total_words = out->total_words;
+  if (!ps->ev0) {
+    ORH_HIP(ctx, hipEventCreate(&ps->ev0));
+    ORH_HIP(ctx, hipEventCreate(&ps->ev1));
+  }
+  ORH_HIP(ctx, hipEventRecord(ps->ev0, ctx->stream));
   hipError_t e = orh::launch_route_select(a, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "route_select launch");
+  ORH_HIP(ctx, hipEventRecord(ps->ev1, ctx->stream));
   (void)words;
+  return ORH_OK;
+}
+
+int orh_last_select_ms(orh_prefix_set* ps, double* ms_out) {
+  if (!ps || !ms_out) return ORH_E_INVALID;
+  if (!ps->ev1) return fail(ps->ctx, ORH_E_STATE, "orh_last_select_ms: no route_select yet");
+  ORH_HIP(ps->ctx, hipEventSynchronize(ps->ev1));
+  float ms = 0.f;
+  ORH_HIP(ps->ctx, hipEventElapsedTime(&ms, ps->ev0, ps->ev1));
+  *ms_out = ms;
   return ORH_OK;
 }
 

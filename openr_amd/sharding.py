@@ -26,6 +26,36 @@ def shard_sources(sources: Sequence[str], world: int, rank: int) -> List[str]:
     return list(sources[lo:hi])
 
 
+def weighted_blocks(weights: Sequence[float], world: int) -> List[Tuple[int, int]]:
+    """Contiguous blocks [lo, hi) of units whose total weights are as equal as
+    a contiguous split allows (prefix-sum cut points). Used for source shards
+    weighted by per-source work, so high-degree nodes (Clos spines: many
+    first-hop rows) spread over the ranks while every block stays a run of
+    name-ordered sources (the multi-source BFS batches consecutive sources)."""
+    n = len(weights)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    total = float(sum(weights))
+    cuts, acc, k = [0], 0.0, 1
+    for i, w in enumerate(weights):
+        acc += w
+        while k < world and acc >= total * k / world and len(cuts) <= k:
+            cuts.append(i + 1)
+            k += 1
+    while len(cuts) < world:
+        cuts.append(n)
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def degree_weighted_sources(sources: Sequence[str], degrees: Sequence[int], world: int,
+                            rank: int, per_neighbour: float = 1.0 / 16) -> List[str]:
+    """Rank's contiguous block of `sources` with work weight 1 + deg/16 per
+    source (degree-weighted sharding for Clos spines)."""
+    lo, hi = weighted_blocks([1.0 + d * per_neighbour for d in degrees], world)[rank]
+    return list(sources[lo:hi])
+
+
 def dist_env():
     """(rank, world_size, local_rank) from torch.distributed.run's env."""
     import os

@@ -20,6 +20,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# route-DB parity tests run the device route selection at every size (the
+# product keeps fewer than 1024 prefixes on the host path by default)
+os.environ.setdefault("ORH_DEVICE_SELECT_MIN", "0")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

@@ -148,3 +148,88 @@ def test_sharded_all_sources_gpu(hip, oracle):
         ref = als_o[A].get_spf_result(names[i])
         for j, v in enumerate(node_names):
             assert d[i, j] == ref[v].metric
+
+
+@pytest.mark.parametrize("weights,world", [([1] * 10, 3), ([5] + [1] * 9, 4), ([1] * 3, 8),
+                                           ([1 + (i % 7) for i in range(1000)], 8), ([], 2)])
+def test_weighted_blocks_partition(weights, world):
+    from openr_amd.sharding import weighted_blocks
+    blocks = weighted_blocks(weights, world)
+    assert len(blocks) == world
+    assert [i for lo, hi in blocks for i in range(lo, hi)] == list(range(len(weights)))
+    if weights:
+        loads = [sum(weights[lo:hi]) for lo, hi in blocks]
+        assert max(loads) - sum(weights) / world <= max(weights) + 1e-9
+
+
+def _clos_partition_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from openr_amd.sharding import degree_weighted_sources
+        from openr_amd.workloads import c3_fabric
+        adj, _ = c3_fabric(num_prefixes=0)
+        names = [db.thisNodeName for db in adj]
+        degrees = [len(db.adjacencies) for db in adj]
+        mine = degree_weighted_sources(names, degrees, world, rank)
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        q.put((rank, got, names, degrees))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_degree_weighted_clos_sharding_gloo_world2():
+    """C3 Clos sources split over 2 ranks by degree weight:
+    every rank sees the same partition; it covers every source once, in
+    contiguous name-ordered blocks, with the spine-heavy block smaller."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_clos_partition_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    # drain the queue before joining: a child exits only after its (large)
+    # result has left the pipe
+    res = sorted((q.get(timeout=180) for _ in range(2)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    parts, names, degrees = res[0][1], res[0][2], res[0][3]
+    assert res[1][1] == parts
+    assert parts[0] + parts[1] == names
+    w = {n: 1 + d / 16 for n, d in zip(names, degrees)}
+    loads = [sum(w[x] for x in p) for p in parts]
+    assert abs(loads[0] - loads[1]) <= 2 * max(w.values())
+    assert len(parts[0]) < len(parts[1])  # spines (degree 39) are in the first block
+
+
+@pytest.mark.gpu
+def test_prefix_sharded_route_build(hip, oracle):
+    """C3 route build split over 3 prefix shards (set_prefix_shard): the
+    shards' unicast routes are disjoint and their union, with shard 0's MPLS
+    routes, is the unsharded database (and the oracle's)."""
+    from openr_amd.facade import load_topology
+    from openr_amd.workloads import c3_fabric
+    adj_dbs, prefixes = c3_fabric(num_prefixes=3000)
+    als, ps = load_topology(hip, adj_dbs, prefixes)
+    als_o, ps_o = load_topology(oracle, adj_dbs, prefixes)
+    me = "2-0-0"
+    full = hip.spf_solver(me, True).build_route_db(me, als, ps)
+    ref = oracle.spf_solver(me, True).build_route_db(me, als_o, ps_o)
+    assert full.canonical_full() == ref.canonical_full()
+    uc, mp_ = {}, {}
+    for r in range(3):
+        s = hip.spf_solver(me, True)
+        s._impl.set_prefix_shard(r, 3)
+        db = s.build_route_db(me, als, ps)
+        assert not set(db.unicastRoutes) & set(uc)
+        uc.update(db.unicastRoutes)
+        if r == 0:
+            mp_ = db.mplsRoutes
+        else:
+            assert not db.mplsRoutes
+    from openr_amd.types import RouteDb
+    assert RouteDb(uc, mp_).canonical_full() == full.canonical_full()
