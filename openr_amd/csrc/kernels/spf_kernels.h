@@ -26,6 +26,7 @@ struct SpfArgs {
   uint8_t* ms_lvl;            // multi-source BFS: node-major level bytes [batches][N][S]
   uint32_t ms_pitch;          // multi-source BFS: frontier-array entries (> N)
   uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
+  uint32_t ms_radius;         // multi-source BFS: neighbour reach in 64-node slices (0: no skip)
   const uint2* recs;       // ELL slots [N * K] then overflow records
   const uint32_t* link;    // per record: link id (ignore sets)
   const uint32_t* srcs;    // [n_rows]

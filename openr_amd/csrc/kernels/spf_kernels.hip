@@ -290,6 +290,18 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
 // >= 254 are written to the output row directly (marker 254), so any depth is
 // exact; 255 = unreached.
 //
+// Activity skip: nodes are numbered in Cuthill-McKee order, so every live
+// record v -> u has |u - v| <= bandwidth. A 64-node slice (one wave's nodes
+// of one j) can only gain bits at level L if some slice within
+// ms_radius = ceil(bandwidth / 64) had a new bit at level L-1; every other
+// slice is skipped without reading its neighbours' frontier entries (their
+// stale entries only repeat visited bits, see below). Slice activity lives in
+// three rotating LDS bitmaps; each wave dilates the previous level's bitmap
+// by the radius in registers (lanes 0..15 hold one 32-slice word each) and
+// reads its slices' bits with readlane. On the 10k grid this skips the
+// unreached and settled bands around the frontier: ~30-70 % of the wave
+// groups of a batch, most for the corner batches that set the sweep time.
+//
 // The search is latency-bound, not LDS-bound: on the 10k grid one workgroup
 // takes ~0.7 ms whether 32 or 313 of them run (two fit per CU), ~165 levels
 // of ~9k cycles, of which ~25 % are the level-byte stores and ~23 % the
@@ -332,12 +344,14 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   const uint32_t S = min(kS, a.n_rows - b0);
   const uint32_t full = S == 32u ? 0xFFFFFFFFu : (1u << S) - 1u;
   __shared__ uint32_t s_prog[3];
+  __shared__ uint32_t s_act[3][16];  // slice activity (<= 512 slices of 64 nodes)
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
   uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
 
   for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
   if (tid < 3) s_prog[tid] = 0u;
+  if (tid < 48) (&s_act[0][0])[tid] = 0u;
   {  // every level byte starts as "unreached"
     uint4* l4 = reinterpret_cast<uint4*>(lvl);
     for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -349,6 +363,11 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     const uint32_t sh = (reinterpret_cast<uintptr_t>(f_cur + src) & 3u) * 8u;
     atomicOr(w, (1u << tid) << sh);
     lvl[static_cast<size_t>(src) * kS + tid] = 0;
+  }
+  __syncthreads();  // s_act zeroed before the sources mark their slices
+  if (tid < S) {
+    const uint32_t k = a.dev_of[a.srcs[a.order[b0 + tid]]] >> 6;
+    atomicOr(&s_act[0][k >> 5], 1u << (k & 31u));
   }
 
   uint32_t col[J][KH];
@@ -385,6 +404,8 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   uint64_t t_bar = 0, t_store = 0;
   uint32_t n_levels = 0;
 #endif
+  const uint32_t R = a.ms_radius;
+  const uint32_t lane = tid & 63u, wave = tid >> 6, nwaves = B >> 6;
   for (uint32_t level = 1;; ++level) {
     int prog = 0;
     // opaque per level: keeps the compiler from hoisting J * K unpacked LDS
@@ -392,6 +413,20 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
+    uint32_t* act_now = s_act[level % 3u];
+    if (tid < 16) s_act[(level + 1u) % 3u][tid] = 0u;  // read at level - 1, written at level + 1
+    // previous level's active slices dilated by R: lane l < 16 holds word l
+    uint32_t dil = 0xFFFFFFFFu;
+    if (R) {
+      const uint32_t* prev = s_act[(level + 2u) % 3u];
+      dil = 0u;
+      if (lane < 16) {
+        const uint64_t p = lane ? prev[lane - 1] : 0u, c = prev[lane], n = lane < 15 ? prev[lane + 1] : 0u;
+        const uint64_t lo = (c << 32) | p, hi = (n << 32) | c;
+        for (uint32_t d = 0; d <= R; ++d)
+          dil |= static_cast<uint32_t>((lo << d) >> 32) | static_cast<uint32_t>(hi >> d);
+      }
+    }
     // groups of G owned nodes: a group is skipped when every lane holds all
     // bits for all G nodes (wave-uniform branch); otherwise all G * K
     // frontier reads go out back to back before any is consumed
@@ -402,6 +437,15 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) open |= vis[j0 + g] != full;
       if (!__builtin_amdgcn_ballot_w64(open)) continue;
+      // slices of this group's G nodes per lane: k = j * nwaves + wave
+      uint32_t actm = 0u;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const uint32_t k = (j0 + g) * nwaves + wave;
+        const uint32_t wd = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dil), k >> 5));
+        actm |= ((wd >> (k & 31u)) & 1u) << g;
+      }
+      if (!actm) continue;  // no frontier within reach: nothing can arrive
       uint32_t acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g)
@@ -410,6 +454,7 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         acc[g] = 0u;
+        if (!((actm >> g) & 1u)) continue;
 #pragma unroll
         for (int h = 0; h < KH; ++h) {
           acc[g] |= f_cur[col[j0 + g][h] & 0xFFFFu];
@@ -419,6 +464,7 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int j = j0 + g;
+        if (!((actm >> g) & 1u)) continue;  // its f_nxt entries stay stale: harmless
         const uint32_t v = j * B + me;
         uint32_t nx = 0u;
         if (vis[j] != full) {  // also every v >= N
@@ -460,6 +506,10 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
         if (vis[j] != full || nx) {
           if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
           f_nxt[v] = static_cast<M>(nx);
+        }
+        if (R && __builtin_amdgcn_ballot_w64(nx != 0u) && lane == 0) {
+          const uint32_t k = j * nwaves + wave;
+          atomicOr(&act_now[k >> 5], 1u << (k & 31u));
         }
       }
     }

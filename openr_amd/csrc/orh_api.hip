@@ -89,6 +89,7 @@ struct orh_graph {
   // after attribute patches. Rows in HBM are always indexed by host id.
   std::vector<uint32_t> ms_dev_of, ms_host_of;  // host -> CM id, CM id -> host
   bool ms_dirty = true;
+  uint32_t ms_radius = 0;  // ceil(CM bandwidth / 64) over live records, 0 if > 31
   uint2* d_ms_recs = nullptr;
   uint32_t* d_ms_dev_of = nullptr;
   uint32_t* d_ms_host_of = nullptr;
@@ -235,20 +236,32 @@ void build_layout(orh_graph* g, std::vector<uint2>& recs, std::vector<uint32_t>&
 }
 
 // the ELL records again, rows and columns in Cuthill-McKee ids
-void build_ms_layout(const orh_graph* g, std::vector<uint2>& recs) {
+void build_ms_layout(orh_graph* g, std::vector<uint2>& recs) {
   const uint32_t K = g->ell_k, N = g->n_nodes;
   recs.assign(g->n_recs, make_uint2(ORH_REC_SKIP, 1));
-  uint32_t ovf = N * K;
+  uint32_t ovf = N * K, bw = 0;
+  auto put = [&](uint32_t q, uint32_t dv, uint32_t v, uint32_t e) {
+    recs[q] = device_record(g, v, e, g->ms_dev_of.data());
+    if (!(recs[q].x & ORH_REC_SKIP)) {
+      const uint32_t u = recs[q].x & ORH_REC_COL_MASK;
+      bw = std::max(bw, u > dv ? u - dv : dv - u);
+    }
+  };
   for (uint32_t dv = 0; dv < N; ++dv) {
     const uint32_t v = g->ms_host_of[dv];
     const uint32_t e0 = g->row_ptr[v], d = g->row_ptr[v + 1] - e0, base = dv * K;
     const uint32_t inl = d <= K ? d : K - 1;
-    for (uint32_t j = 0; j < inl; ++j) recs[base + j] = device_record(g, v, e0 + j, g->ms_dev_of.data());
+    for (uint32_t j = 0; j < inl; ++j) put(base + j, dv, v, e0 + j);
     if (d > K) {
       recs[base + K - 1] = make_uint2(ovf | ORH_REC_CONT, d - inl);
-      for (uint32_t j = inl; j < d; ++j) recs[ovf++] = device_record(g, v, e0 + j, g->ms_dev_of.data());
+      for (uint32_t j = inl; j < d; ++j) put(ovf++, dv, v, e0 + j);
     }
   }
+  // a slice (64 consecutive ids) reaches the slices within ceil(bw / 64);
+  // the kernel's dilation handles up to 31 (ORH_MS_SKIP=0 turns it off)
+  const uint32_t r = (bw + 63) / 64;
+  const char* e = getenv("ORH_MS_SKIP");
+  g->ms_radius = (r <= 31 && !(e && atoi(e) == 0)) ? std::max(r, 1u) : 0u;
 }
 
 int sync_ms_layout(orh_graph* g) {
@@ -867,6 +880,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   if (plan.variant == orh::SpfVariant::kMsBfs) {
     int rc = sync_ms_layout(g);
     if (rc) return rc;
+    a.ms_radius = g->ms_radius;
     rc = ensure_ms_lvl(ctx, orh::ms_scratch_bytes(plan, N, n_rows));
     if (rc) return rc;
     a.recs = g->d_ms_recs;
