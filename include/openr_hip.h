@@ -78,6 +78,9 @@ typedef struct orh_csr {
   const uint32_t* w_in;           /* [n_edges] Link::getMetricFromNode(col) */
   const uint32_t* meta;           /* [n_edges] ORH_META_* bits | link id */
   const uint8_t* node_overloaded; /* [n_nodes] LinkState::isNodeOverloaded */
+  /* [n_nodes] rank of each node's name in byte order (the reference's
+   * DijkstraQ tie order, LinkState.h:488-498); NULL: node id order */
+  const uint32_t* name_rank;
 } orh_csr;
 
 typedef struct orh_spf_request {
@@ -123,6 +126,9 @@ int orh_reset_counters(orh_ctx* ctx);
 #define ORH_SPF_PER_SOURCE 1
 #define ORH_SPF_GLOBAL 2
 #define ORH_SPF_GLOBAL_TWO_PHASE 3
+/* the exact kernel (reference extraction order) for every graph; it runs
+ * anyway for graphs with a zero-metric live link */
+#define ORH_SPF_EXACT 4
 int orh_set_spf_mode(orh_ctx* ctx, int mode);
 /* kernel plan of the last orh_spf_run on this context (tests and profiling
  * assert which variant ran; results never depend on it) */
@@ -192,6 +198,23 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
 /* synchronous convenience form: results copied into host buffers */
 int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32_t* h_dist,
                   uint32_t* h_nh);
+
+/* Exact SPF: LinkState::runSpf (LinkState.cpp:808-882) in the reference's own
+ * extraction order, with 64-bit path metrics (LinkStateMetric = uint64_t,
+ * LinkState.h:22). Needed when a live link has metric 0 (the first hops of a
+ * node then depend on which equal-metric neighbour is extracted first) or
+ * when path metrics can reach 2^32 (orh_spf_run then returns
+ * ORH_E_UNSUPPORTED). d_dist [n_src*N] u64 (~0 = unreachable), d_nh as in
+ * orh_spf_run, d_rank [n_src*N] (nullable): extraction order of every node
+ * (the order of NodeSpfResult::pathLinks' predecessors; ~0 = unreachable). */
+int orh_spf_run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint64_t* d_dist,
+                      uint32_t* d_nh, uint32_t* d_rank);
+int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words,
+                        uint64_t* h_dist, uint32_t* h_nh, uint32_t* h_rank);
+/* ORH_GRAPH_* properties of the loaded graph */
+#define ORH_GRAPH_ZERO_METRIC 1u /* a live link has metric 0 */
+#define ORH_GRAPH_WIDE_METRIC 2u /* link-metric path sums can reach 2^32 - 1 */
+int orh_graph_flags(const orh_graph* g, uint32_t* flags);
 
 /* ---- device prefix mirror (PrefixState) ------------------------------- */
 /* Replaces the per-prefix PrefixEntries map PrefixState::prefixes() hands to

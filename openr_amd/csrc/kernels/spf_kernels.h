@@ -83,16 +83,44 @@ struct HopArgs {
 
 enum class SpfVariant {
   kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal,
-  kGlobalNh  // HBM frontier kernel that also derives the first hops (no phase 2)
+  kGlobalNh,  // HBM frontier kernel that also derives the first hops (no phase 2)
+  kExact      // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
 };
+
+// exact Dijkstra (spf_exact_kernel): one wave per source row; heap, 64-bit
+// metrics and first-hop masks in LDS (or per-row global scratch when the
+// graph is too large); outputs u32 or u64 distances, masks and the
+// extraction rank of every node (the reference's pathLinks order)
+struct ExactArgs {
+  uint32_t n_nodes;
+  uint32_t n_rows;
+  uint32_t words;
+  int32_t use_link_metric;
+  uint32_t ell_k;
+  const uint2* recs;
+  const uint32_t* link;
+  const uint16_t* rank_out;
+  const uint32_t* name_rank;  // [N] byte order of the node names (heap ties)
+  const uint32_t* srcs;
+  const uint32_t* ignore_ptr;
+  const uint32_t* ignore_links;
+  uint32_t* out_dist32;  // nullable: [rows][N], ORH_UNREACHABLE
+  uint64_t* out_dist64;  // nullable: [rows][N], ~0 unreachable
+  uint32_t* out_nh;      // [rows][N][words]
+  uint32_t* out_rank;    // nullable: [rows][N], extraction order (~0 unreached)
+  uint8_t* scratch;      // global per-row state when not in LDS
+  size_t scratch_stride;
+};
+size_t exact_state_bytes(uint32_t n_nodes, uint32_t words);
+hipError_t launch_exact(const ExactArgs& a, size_t lds_limit, hipStream_t s);
 
 // distance-kernel selection (orh_set_spf_mode): automatic (multi-source BFS
 // when eligible, else the LDS-resident per-source kernels, else the HBM
 // frontier kernel), per-source LDS kernels only, the HBM kernel always (with
 // fused first hops when every source has <= 32 distinct neighbours), or the
 // two-phase HBM kernel always
-enum class SpfMode { kAuto = 0, kPerSource = 1, kGlobal = 2, kGlobalTwoPhase = 3 };
-constexpr int kSpfModes = 4;
+enum class SpfMode { kAuto = 0, kPerSource = 1, kGlobal = 2, kGlobalTwoPhase = 3, kExact = 4 };
+constexpr int kSpfModes = 5;
 
 struct SpfPlan {
   SpfVariant variant;

@@ -332,7 +332,21 @@ __device__ inline void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int K, class M, int J>
+// wave-wide OR (same DPP pattern as wave_min)
+__device__ inline uint32_t wave_or(uint32_t v) {
+#define ORH_DPP_OR(ctrl, rmask)                                                     \
+  v |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, rmask, 0xF, false))
+  ORH_DPP_OR(0x111, 0xF);
+  ORH_DPP_OR(0x112, 0xF);
+  ORH_DPP_OR(0x114, 0xF);
+  ORH_DPP_OR(0x118, 0xF);
+  ORH_DPP_OR(0x142, 0xA);
+  ORH_DPP_OR(0x143, 0xC);
+#undef ORH_DPP_OR
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
+template <int K, class M, int J, bool kSkip>
 __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t kS = MsMask<M>::kS;
@@ -413,18 +427,26 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
-    uint32_t* act_now = s_act[level % 3u];
-    if (tid < 16) s_act[(level + 1u) % 3u][tid] = 0u;  // read at level - 1, written at level + 1
-    // previous level's active slices dilated by R: lane l < 16 holds word l
-    uint32_t dil = 0xFFFFFFFFu;
-    if (R) {
+    // slices of this wave (j, wave) whose neighbourhood had a new bit at the
+    // previous level: bit j of amask (all ones without the skip)
+    uint32_t amask = 0xFFFFFFFFu, jm = 0u;
+    if constexpr (kSkip) {
+      if (tid < 16) s_act[(level + 1u) % 3u][tid] = 0u;  // read at level - 1, written at level + 1
+      // previous level's active slices dilated by R: lane l < 16 holds word l
       const uint32_t* prev = s_act[(level + 2u) % 3u];
-      dil = 0u;
+      uint32_t dil = 0u;
       if (lane < 16) {
         const uint64_t p = lane ? prev[lane - 1] : 0u, c = prev[lane], n = lane < 15 ? prev[lane + 1] : 0u;
         const uint64_t lo = (c << 32) | p, hi = (n << 32) | c;
         for (uint32_t d = 0; d <= R; ++d)
           dil |= static_cast<uint32_t>((lo << d) >> 32) | static_cast<uint32_t>(hi >> d);
+      }
+      amask = 0u;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const uint32_t k = j * nwaves + wave;
+        const uint32_t wd = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dil), k >> 5));
+        amask |= ((wd >> (k & 31u)) & 1u) << j;
       }
     }
     // groups of G owned nodes: a group is skipped when every lane holds all
@@ -437,15 +459,10 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) open |= vis[j0 + g] != full;
       if (!__builtin_amdgcn_ballot_w64(open)) continue;
-      // slices of this group's G nodes per lane: k = j * nwaves + wave
-      uint32_t actm = 0u;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const uint32_t k = (j0 + g) * nwaves + wave;
-        const uint32_t wd = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dil), k >> 5));
-        actm |= ((wd >> (k & 31u)) & 1u) << g;
-      }
-      if (!actm) continue;  // no frontier within reach: nothing can arrive
+      // no frontier within reach of any of the G slices: nothing can arrive,
+      // and the group's f_nxt entries stay stale (harmless, see above); an
+      // active group processes all G nodes (branch-free loads)
+      if (kSkip && !((amask >> j0) & ((1u << G) - 1u))) continue;
       uint32_t acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g)
@@ -454,7 +471,6 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         acc[g] = 0u;
-        if (!((actm >> g) & 1u)) continue;
 #pragma unroll
         for (int h = 0; h < KH; ++h) {
           acc[g] |= f_cur[col[j0 + g][h] & 0xFFFFu];
@@ -464,7 +480,6 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const int j = j0 + g;
-        if (!((actm >> g) & 1u)) continue;  // its f_nxt entries stay stale: harmless
         const uint32_t v = j * B + me;
         uint32_t nx = 0u;
         if (vis[j] != full) {  // also every v >= N
@@ -507,11 +522,17 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
           if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
           f_nxt[v] = static_cast<M>(nx);
         }
-        if (R && __builtin_amdgcn_ballot_w64(nx != 0u) && lane == 0) {
-          const uint32_t k = j * nwaves + wave;
+        if constexpr (kSkip) jm |= (nx != 0u ? 1u : 0u) << j;
+      }
+    }
+    if constexpr (kSkip) {  // this wave's slices with a new bit, into the level's bitmap
+      uint32_t* act_now = s_act[level % 3u];
+      uint32_t wm = wave_or(jm);
+      if (lane == 0)
+        for (; wm; wm &= wm - 1) {
+          const uint32_t k = static_cast<uint32_t>(__builtin_ctz(wm)) * nwaves + wave;
           atomicOr(&act_now[k >> 5], 1u << (k & 31u));
         }
-      }
     }
     // every level that makes progress adds >= 1 visited bit: at most S * N
     // levels. The barrier waits for LDS traffic only: the level bytes on
@@ -1069,6 +1090,143 @@ __global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// exact Dijkstra in the reference's extraction order
+// ---------------------------------------------------------------------------
+// LinkState::runSpf (LinkState.cpp:808-882) step for step: a binary heap on
+// (metric, name), `>=` relaxations that union the first-hop sets, reset on a
+// strictly better metric, no transit through overloaded nodes. With a
+// zero-metric link the closed form of the other kernels does not hold (a node
+// at the same metric contributes its first hops only if it is extracted
+// first), and path metrics may exceed 32 bits; this kernel covers both. Lane 0
+// of one wave per source runs the search (its state is one source's heap),
+// the other lanes initialise and copy out.
+size_t exact_state_bytes(uint32_t n, uint32_t words) {
+  // metric u64 | pos u32 | heap u32 | nh u32 * words, 16-byte aligned
+  return ((static_cast<size_t>(n) * (16 + 4 * words)) + 15) & ~static_cast<size_t>(15);
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(64) void spf_exact_kernel(ExactArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t N = a.n_nodes, W = a.words, row = blockIdx.x, lane = threadIdx.x;
+  uint8_t* base = kLds ? reinterpret_cast<uint8_t*>(lds) : a.scratch + row * a.scratch_stride;
+  uint64_t* metric = reinterpret_cast<uint64_t*>(base);
+  uint32_t* pos = reinterpret_cast<uint32_t*>(metric + N);  // heap index + 1, kRec when extracted
+  uint32_t* heap = pos + N;
+  uint32_t* nh = heap + N;
+  constexpr uint64_t kInf64 = ~0ull;
+  constexpr uint32_t kRec = 0xFFFFFFFFu;
+  for (uint32_t v = lane; v < N; v += 64) {
+    metric[v] = kInf64;
+    pos[v] = 0u;
+  }
+  for (uint32_t i = lane; i < N * W; i += 64) nh[i] = 0u;
+  __syncthreads();
+  const uint32_t src = a.srcs[row];
+  const uint32_t* ign = nullptr;
+  uint32_t n_ign = 0;
+  if (a.ignore_ptr) {
+    ign = a.ignore_links + a.ignore_ptr[row];
+    n_ign = a.ignore_ptr[row + 1] - a.ignore_ptr[row];
+  }
+  uint32_t* rank_out = a.out_rank ? a.out_rank + static_cast<size_t>(row) * N : nullptr;
+  if (lane == 0) {
+    auto less = [&](uint32_t x, uint32_t y) {
+      const uint64_t mx = metric[x], my = metric[y];
+      return mx < my || (mx == my && a.name_rank[x] < a.name_rank[y]);
+    };
+    auto sift_up = [&](uint32_t i) {
+      const uint32_t x = heap[i];
+      while (i > 0) {
+        const uint32_t p = (i - 1) >> 1, y = heap[p];
+        if (!less(x, y)) break;
+        heap[i] = y;
+        pos[y] = i + 1;
+        i = p;
+      }
+      heap[i] = x;
+      pos[x] = i + 1;
+    };
+    auto sift_down = [&](uint32_t i, uint32_t n) {
+      const uint32_t x = heap[i];
+      for (;;) {
+        uint32_t c = 2 * i + 1;
+        if (c >= n) break;
+        if (c + 1 < n && less(heap[c + 1], heap[c])) ++c;
+        const uint32_t y = heap[c];
+        if (!less(y, x)) break;
+        heap[i] = y;
+        pos[y] = i + 1;
+        i = c;
+      }
+      heap[i] = x;
+      pos[x] = i + 1;
+    };
+    uint32_t n_heap = 0, order = 0;
+    metric[src] = 0;
+    heap[n_heap++] = src;
+    pos[src] = 1;
+    const uint32_t K = a.ell_k;
+    while (n_heap) {
+      const uint32_t v = heap[0];
+      if (--n_heap) {
+        heap[0] = heap[n_heap];
+        sift_down(0, n_heap);
+      }
+      pos[v] = kRec;  // recorded: final (LinkState.cpp:824)
+      if (rank_out) rank_out[v] = order;
+      ++order;
+      const uint2 r0 = a.recs[static_cast<size_t>(v) * K];
+      if (v != src && (r0.x & ORH_REC_ROW_OVL)) continue;  // no transit (:831-838)
+      const uint64_t dv = metric[v];
+      auto relax = [&](uint32_t q) {
+        const uint2 r = a.recs[q];
+        if (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) return;
+        if (n_ign && ignored(ign, n_ign, a.link[q])) return;
+        const uint32_t u = r.x & ORH_REC_COL_MASK;
+        if (pos[u] == kRec) return;
+        const uint64_t nd = dv + (a.use_link_metric ? static_cast<uint64_t>(r.y) : 1ull);
+        if (pos[u] == 0u) {  // first seen: queued at nd (:853-856)
+          metric[u] = nd;
+          heap[n_heap] = u;
+          sift_up(n_heap++);
+        } else if (metric[u] > nd) {  // strictly better: reset and re-heap (:862-866)
+          metric[u] = nd;
+          for (uint32_t k = 0; k < W; ++k) nh[static_cast<size_t>(u) * W + k] = 0u;
+          sift_up(pos[u] - 1);
+        }
+        if (metric[u] != nd) return;
+        if (v == src) {  // a direct neighbour's own bit (:869-872)
+          const uint32_t b = a.rank_out[q];
+          nh[static_cast<size_t>(u) * W + (b >> 5)] |= 1u << (b & 31u);
+        } else {
+          for (uint32_t k = 0; k < W; ++k)
+            nh[static_cast<size_t>(u) * W + k] |= nh[static_cast<size_t>(v) * W + k];
+        }
+      };
+      for (uint32_t j = 0; j < K; ++j) relax(v * K + j);
+      const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
+      if (last.x & ORH_REC_CONT) {
+        const uint32_t start = last.x & ORH_REC_COL_MASK;
+        for (uint32_t q = 0; q < last.y; ++q) relax(start + q);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t v = lane; v < N; v += 64) {
+    const uint64_t m = metric[v];
+    const bool reached = pos[v] == kRec;
+    if (a.out_dist64) a.out_dist64[static_cast<size_t>(row) * N + v] = reached ? m : kInf64;
+    if (a.out_dist32) a.out_dist32[static_cast<size_t>(row) * N + v] = reached ? static_cast<uint32_t>(m) : kInf;
+    if (rank_out && !reached) rank_out[v] = kInf;
+  }
+  for (uint32_t i = lane; i < N * W; i += 64) {
+    const uint32_t v = i / W;
+    a.out_nh[static_cast<size_t>(row) * N * W + i] = (pos[v] == kRec && v != src) ? nh[i] : 0u;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // phase 2: first-hop masks
 // ---------------------------------------------------------------------------
 // distance of node x in row `row`: the u32 distance row, or (multi-source
@@ -1433,7 +1591,9 @@ template <int K, class M, int J>
 static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   constexpr uint32_t kS = MsMask<M>::kS;
   const uint32_t batches = (n_rows + kS - 1) / kS;
-  return launch(spf_msbfs_kernel<K, M, J>, a, batches, plan.block, plan.lds_bytes, s);
+  if (a.ms_radius)
+    return launch(spf_msbfs_kernel<K, M, J, true>, a, batches, plan.block, plan.lds_bytes, s);
+  return launch(spf_msbfs_kernel<K, M, J, false>, a, batches, plan.block, plan.lds_bytes, s);
 }
 
 template <int K, class M>
@@ -1556,6 +1716,15 @@ hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* va
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_recs_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, recs,
                      pos, vals, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_exact(const ExactArgs& a, size_t lds_limit, hipStream_t s) {
+  if (a.n_rows == 0) return hipSuccess;
+  const size_t bytes = exact_state_bytes(a.n_nodes, a.words);
+  if (bytes <= lds_limit) return launch(spf_exact_kernel<true>, a, a.n_rows, 64, bytes, s);
+  if (!a.scratch) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spf_exact_kernel<false>, dim3(a.n_rows), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
