@@ -140,6 +140,7 @@ int orh_set_spf_mode(orh_ctx* ctx, int mode);
 #define ORH_VARIANT_DIST32 6
 #define ORH_VARIANT_GLOBAL 7    /* HBM frontier kernel, two-phase */
 #define ORH_VARIANT_GLOBAL_NH 8 /* HBM frontier kernel with fused first hops */
+#define ORH_VARIANT_EXACT 9     /* exact Dijkstra in the reference's extraction order */
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */
@@ -201,10 +202,11 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
 
 /* Exact SPF: LinkState::runSpf (LinkState.cpp:808-882) in the reference's own
  * extraction order, with 64-bit path metrics (LinkStateMetric = uint64_t,
- * LinkState.h:22). Needed when a live link has metric 0 (the first hops of a
- * node then depend on which equal-metric neighbour is extracted first) or
- * when path metrics can reach 2^32 (orh_spf_run then returns
- * ORH_E_UNSUPPORTED). d_dist [n_src*N] u64 (~0 = unreachable), d_nh as in
+ * LinkState.h:22). With a zero-metric live link the first hops of a node
+ * depend on which equal-metric neighbour is extracted first; orh_spf_run then
+ * runs this kernel itself (u32 distances). When path metrics can reach
+ * 2^32 - 1, orh_spf_run returns ORH_E_UNSUPPORTED and this entry point is the
+ * one to use. d_dist [n_src*N] u64 (~0 = unreachable), d_nh as in
  * orh_spf_run, d_rank [n_src*N] (nullable): extraction order of every node
  * (the order of NodeSpfResult::pathLinks' predecessors; ~0 = unreachable). */
 int orh_spf_run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint64_t* d_dist,

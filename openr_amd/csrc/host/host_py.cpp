@@ -250,7 +250,7 @@ py::dict rowToDict(const LinkState& ls, const SpfRow& row, bool withPaths) {
     d[py::str(row.srcName)] = py::make_tuple(0, py::list(), py::list());
     return d;
   }
-  for (uint32_t v = 0; v < row.dist.size(); ++v) {
+  for (uint32_t v = 0; v < row.n; ++v) {
     if (!row.reachable(v)) continue;
     std::vector<std::string> nhs;
     row.forEachNextHop(v, [&](uint32_t nb) { nhs.push_back(ls.nodeName(nb)); });
@@ -260,7 +260,7 @@ py::dict rowToDict(const LinkState& ls, const SpfRow& row, bool withPaths) {
       for (const auto& [lid, prev] : ls.pathLinks(row, v))
         pls.append(py::make_tuple(linkDesc(ls.link(lid)), ls.nodeName(prev)));
     }
-    d[py::str(ls.nodeName(v))] = py::make_tuple(static_cast<uint64_t>(row.dist[v]), nhs, pls);
+    d[py::str(ls.nodeName(v))] = py::make_tuple(static_cast<uint64_t>(row.metric(v)), nhs, pls);
   }
   return d;
 }

@@ -20,11 +20,12 @@ void check(orh_ctx* ctx, int rc, const char* what) {
 }
 
 uint32_t toDeviceMetric(Metric m) {
-  // the device keeps 32-bit metrics; thrift adjacency metrics are i32, so
-  // only non-positive values (which widen to 0 or > 2^32) are out of range
-  if (m == 0 || m > 0xFFFFFFFFull) {
+  // the device keeps 32-bit link metrics (path sums are 64-bit on the exact
+  // path); thrift adjacency metrics are i32, so only negative values (which
+  // widen past 2^32) are out of range
+  if (m > 0xFFFFFFFFull) {
     throw std::domain_error("libopenr_hip: link metric " + std::to_string(m) +
-                            " is outside [1, 2^32-1] (zero/negative adjacency metrics are "
+                            " is outside [0, 2^32-1] (negative adjacency metrics are "
                             "not supported by the device SPF)");
   }
   return static_cast<uint32_t>(m);
@@ -387,8 +388,15 @@ void LinkState::flushMirror() const {
     }
     std::vector<uint8_t> ovl(N, 0);
     for (uint32_t v = 0; v < N; ++v) ovl[v] = isNodeOverloaded(names_[v]) ? 1 : 0;
+    // DijkstraQ ties break on the node name (LinkState.h:488-498)
+    std::vector<uint32_t> byName(N), nameRank(N);
+    for (uint32_t v = 0; v < N; ++v) byName[v] = v;
+    std::sort(byName.begin(), byName.end(),
+              [&](uint32_t a, uint32_t b) { return names_[a] < names_[b]; });
+    for (uint32_t r = 0; r < N; ++r) nameRank[byName[r]] = r;
     orh_csr c{};
     c.n_nodes = N;
+    c.name_rank = nameRank.data();
     c.n_edges = static_cast<uint32_t>(col_.size());
     c.n_links = static_cast<uint32_t>(links_.size());
     c.row_ptr = rowPtr_.data();
@@ -442,18 +450,61 @@ orh_graph* LinkState::deviceGraph() const {
   return graph_;
 }
 
+void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric,
+                         const orh_spf_request& req, std::vector<SpfRow>& rows) const {
+  const uint32_t N = static_cast<uint32_t>(names_.size());
+  const uint32_t n = static_cast<uint32_t>(srcIds.size());
+  uint32_t words = 1, flags = 0;
+  check(ctx_, orh_spf_words(graph_, srcIds.data(), n, &words), "orh_spf_words");
+  check(ctx_, orh_graph_flags(graph_, &flags), "orh_graph_flags");
+  const size_t nd = static_cast<size_t>(n) * N;
+  std::vector<uint32_t> dist, nh(nd * words), order;
+  std::vector<uint64_t> dist64;
+  // zero-metric links / 64-bit path metrics: the reference's extraction order
+  // decides the first hops and the pathLinks order (LinkState.cpp:808-882)
+  const bool exact = useLinkMetric && flags != 0;
+  const bool wide = useLinkMetric && (flags & ORH_GRAPH_WIDE_METRIC);
+  if (exact) {
+    dist64.resize(nd);
+    order.resize(nd);
+    check(ctx_, orh_spf_batch_exact(graph_, &req, words, dist64.data(), nh.data(), order.data()),
+          "orh_spf_batch_exact");
+  } else {
+    dist.resize(nd);
+    check(ctx_, orh_spf_batch(graph_, &req, words, dist.data(), nh.data()), "orh_spf_batch");
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    SpfRow& row = rows[i];
+    const uint32_t src = srcIds[i];
+    const size_t b = static_cast<size_t>(i) * N;
+    row.srcName = names_[src];
+    row.src = src;
+    row.known = true;
+    row.useLinkMetric = useLinkMetric;
+    row.words = words;
+    row.n = N;
+    if (!exact) {
+      row.dist.assign(dist.begin() + b, dist.begin() + b + N);
+    } else if (wide) {
+      row.dist64.assign(dist64.begin() + b, dist64.begin() + b + N);
+    } else {  // path metrics < 2^32 - 1: the u32 row (route selection reads it)
+      row.dist.resize(N);
+      for (uint32_t v = 0; v < N; ++v)
+        row.dist[v] = dist64[b + v] == ~0ull ? ORH_UNREACHABLE : static_cast<uint32_t>(dist64[b + v]);
+    }
+    if (exact) row.order.assign(order.begin() + b, order.begin() + b + N);
+    row.nh.assign(nh.begin() + b * words, nh.begin() + (b + N) * words);
+    uint32_t nn = 0;
+    check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &nn), "orh_graph_neighbors");
+    row.nbrs.resize(nn);
+    check(ctx_, orh_graph_neighbors(graph_, src, row.nbrs.data(), nn, &nn), "orh_graph_neighbors");
+  }
+  spfRuns_ += n;
+}
+
 SpfRow LinkState::spfOnDevice(uint32_t src, bool useLinkMetric,
                               const std::vector<uint32_t>* ignore) const {
   flushMirror();
-  SpfRow row;
-  row.srcName = names_[src];
-  row.src = src;
-  row.known = true;
-  row.useLinkMetric = useLinkMetric;
-  check(ctx_, orh_spf_words(graph_, &src, 1, &row.words), "orh_spf_words");
-  const uint32_t N = static_cast<uint32_t>(names_.size());
-  row.dist.resize(N);
-  row.nh.resize(static_cast<size_t>(N) * row.words);
   uint32_t ptr[2] = {0, ignore ? static_cast<uint32_t>(ignore->size()) : 0u};
   orh_spf_request req{};
   req.h_srcs = &src;
@@ -463,14 +514,9 @@ SpfRow LinkState::spfOnDevice(uint32_t src, bool useLinkMetric,
     req.h_ignore_ptr = ptr;
     req.h_ignore_links = ignore->data();
   }
-  check(ctx_, orh_spf_batch(graph_, &req, row.words, row.dist.data(), row.nh.data()),
-        "orh_spf_batch");
-  uint32_t n = 0;
-  check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &n), "orh_graph_neighbors");
-  row.nbrs.resize(n);
-  check(ctx_, orh_graph_neighbors(graph_, src, row.nbrs.data(), n, &n), "orh_graph_neighbors");
-  ++spfRuns_;
-  return row;
+  std::vector<SpfRow> rows(1);
+  fillRows({src}, useLinkMetric, req, rows);
+  return std::move(rows[0]);
 }
 
 std::vector<SpfRow> LinkState::runSpfBatch(
@@ -479,14 +525,10 @@ std::vector<SpfRow> LinkState::runSpfBatch(
   std::vector<SpfRow> rows(srcIds.size());
   if (srcIds.empty()) return rows;
   flushMirror();
-  const uint32_t N = static_cast<uint32_t>(names_.size());
-  const uint32_t n = static_cast<uint32_t>(srcIds.size());
-  uint32_t words = 1;
-  check(ctx_, orh_spf_words(graph_, srcIds.data(), n, &words), "orh_spf_words");
   std::vector<uint32_t> ptr, flat;
   orh_spf_request req{};
   req.h_srcs = srcIds.data();
-  req.n_src = n;
+  req.n_src = static_cast<uint32_t>(srcIds.size());
   req.use_link_metric = useLinkMetric ? 1 : 0;
   if (ignoreSets) {
     if (ignoreSets->size() != srcIds.size())
@@ -499,26 +541,7 @@ std::vector<SpfRow> LinkState::runSpfBatch(
     req.h_ignore_ptr = ptr.data();
     req.h_ignore_links = flat.empty() ? ptr.data() : flat.data();
   }
-  std::vector<uint32_t> dist(static_cast<size_t>(n) * N), nh(static_cast<size_t>(n) * N * words);
-  check(ctx_, orh_spf_batch(graph_, &req, words, dist.data(), nh.data()), "orh_spf_batch");
-  for (uint32_t i = 0; i < n; ++i) {
-    SpfRow& row = rows[i];
-    const uint32_t src = srcIds[i];
-    row.srcName = names_[src];
-    row.src = src;
-    row.known = true;
-    row.useLinkMetric = useLinkMetric;
-    row.words = words;
-    row.dist.assign(dist.begin() + static_cast<size_t>(i) * N,
-                    dist.begin() + static_cast<size_t>(i + 1) * N);
-    row.nh.assign(nh.begin() + static_cast<size_t>(i) * N * words,
-                  nh.begin() + static_cast<size_t>(i + 1) * N * words);
-    uint32_t nn = 0;
-    check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &nn), "orh_graph_neighbors");
-    row.nbrs.resize(nn);
-    check(ctx_, orh_graph_neighbors(graph_, src, row.nbrs.data(), nn, &nn), "orh_graph_neighbors");
-  }
-  spfRuns_ += n;
+  fillRows(srcIds, useLinkMetric, req, rows);
   return rows;
 }
 
@@ -617,8 +640,8 @@ Metric LinkState::getMaxHopsToNode(const std::string& node) const {
   const SpfRow& row = getSpfResult(node, false);  // LinkState.cpp:753-760
   Metric mx = 0;
   if (!row.known) return 0;
-  for (uint32_t d : row.dist)
-    if (d != ORH_UNREACHABLE) mx = std::max<Metric>(mx, d);
+  for (uint32_t v = 0; v < row.n; ++v)
+    if (row.reachable(v)) mx = std::max(mx, row.metric(v));
   return mx;
 }
 
@@ -626,10 +649,12 @@ Metric LinkState::getMaxHopsToNode(const std::string& node) const {
 std::vector<std::pair<uint32_t, uint32_t>> LinkState::pathLinks(
     const SpfRow& row, uint32_t v, const std::unordered_set<uint32_t>* ignore) const {
   // predecessors (link, prev) of v in the order runSpf appends them: by
-  // extraction order of prev = (dist, name) for metrics >= 1, then prev's
-  // LinkSet iteration order (LinkState.cpp:821-873)
+  // extraction order of prev - (dist, name) for metrics >= 1, the recorded
+  // order of exact rows - then prev's LinkSet iteration order
+  // (LinkState.cpp:821-873). A prev extracted after v (possible only over a
+  // zero-metric link) never relaxed v.
   struct Cand {
-    uint32_t dist;
+    Metric dist;
     const std::string* name;
     uint32_t pos;
     uint32_t link;
@@ -644,16 +669,17 @@ std::vector<std::pair<uint32_t, uint32_t>> LinkState::pathLinks(
     if (!row.reachable(u)) continue;
     if (u != row.src && isNodeOverloaded(names_[u])) continue;
     const Metric w = row.useLinkMetric ? l.metricFrom(u) : 1;
-    if (static_cast<Metric>(row.dist[u]) + w != row.dist[v]) continue;
+    if (row.metric(u) + w != row.metric(v)) continue;
+    if (!row.order.empty() && row.order[u] > row.order[v]) continue;
     uint32_t pos = 0;
     for (uint32_t x : *nodeLinks_[u]) {
       if (x == id) break;
       ++pos;
     }
-    cands.push_back({row.dist[u], &names_[u], pos, id, u});
+    cands.push_back({row.order.empty() ? row.metric(u) : row.order[u], &names_[u], pos, id, u});
   }
   std::sort(cands.begin(), cands.end(), [](const Cand& a, const Cand& b) {
-    if (a.dist != b.dist) return a.dist < b.dist;
+    if (a.dist != b.dist) return a.dist < b.dist;  // the order rank for exact rows
     if (*a.name != *b.name) return *a.name < *b.name;
     return a.pos < b.pos;
   });

@@ -99,18 +99,27 @@ using Path = std::vector<uint32_t>;  // link ids, src -> dst
 
 // One source's SPF result as produced by the device: dist row + first-hop
 // bitmask row over the source's distinct neighbours (orh_graph_neighbors).
+// Rows of the exact kernel (zero-metric links, or path metrics that can reach
+// 2^32) also carry the extraction order; their distances are 64-bit when the
+// graph's path metrics can exceed 32 bits.
 struct SpfRow {
   std::string srcName;
   uint32_t src{0};
   bool known{false};  // src has a node id in this area
   bool useLinkMetric{true};
   uint32_t words{1};
-  std::vector<uint32_t> dist;  // ORH_UNREACHABLE when absent
-  std::vector<uint32_t> nh;    // [N * words]
-  std::vector<uint32_t> nbrs;  // bit k <-> node id nbrs[k]
+  uint32_t n{0};                 // nodes in the row
+  std::vector<uint32_t> dist;    // ORH_UNREACHABLE when absent (empty when dist64 is used)
+  std::vector<uint64_t> dist64;  // ~0 when absent (wide-metric graphs only)
+  std::vector<uint32_t> order;   // extraction order (exact rows only, ~0 when absent)
+  std::vector<uint32_t> nh;      // [N * words]
+  std::vector<uint32_t> nbrs;    // bit k <-> node id nbrs[k]
 
-  bool reachable(uint32_t v) const { return known && v < dist.size() && dist[v] != ORH_UNREACHABLE; }
-  Metric metric(uint32_t v) const { return dist[v]; }
+  bool reachable(uint32_t v) const {
+    if (!known || v >= n) return false;
+    return dist64.empty() ? dist[v] != ORH_UNREACHABLE : dist64[v] != ~0ull;
+  }
+  Metric metric(uint32_t v) const { return dist64.empty() ? Metric{dist[v]} : dist64[v]; }
   template <class F>
   void forEachNextHop(uint32_t v, F&& f) const {
     for (uint32_t k = 0; k < words; ++k) {
@@ -205,6 +214,10 @@ class LinkState {
   void flushMirror() const;
   SpfRow spfOnDevice(uint32_t src, bool useLinkMetric,
                      const std::vector<uint32_t>* ignore) const;
+  // rows from the device for sources `srcIds` (the exact kernel when the
+  // graph needs it); rows[i].src etc. filled in
+  void fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric, const orh_spf_request& req,
+                std::vector<SpfRow>& rows) const;
   std::vector<Path> traceKthPaths(const std::string& src, const std::string& dst,
                                   const SpfRow& row,
                                   const std::unordered_set<uint32_t>* ignore) const;

@@ -616,6 +616,9 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   for (const auto& [_, ls] : als)
     if (ls.context() != ctx) return false;
   if (selCtx_ && selCtx_ != ctx) return false;
+  // the kernel reads u32 distance rows: path metrics past 32 bits stay on the host
+  for (const auto& [_, ls] : als)
+    if (ls.getSpfResult(me).known && !ls.getSpfResult(me).dist64.empty()) return false;
   // getNextHopsWithMetric keys nexthops by neighbour name only (:1221): a
   // neighbour name shared by two areas couples their links, keep those
   // topologies on the host path
@@ -656,7 +659,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     const SpfRow& row = ls->getSpfResult(me);
     orh_graph* g = ls->deviceGraph();
     if (!row.known) continue;  // me's SpfResult holds only me: nothing reachable
-    const uint32_t N = static_cast<uint32_t>(row.dist.size());
+    const uint32_t N = row.n;
     // names -> node ids of this area (incremental while both only grow)
     if (w.ls != ls || w.lsNodes != ls->numNodeIds() || w.psNames > nNames) {
       w.ls = ls;

@@ -56,6 +56,12 @@ struct orh_ctx {
   // mirror-patch staging (positions + records of one delta batch)
   uint32_t* d_patch = nullptr;
   size_t d_patch_cap = 0;  // in u32
+  // exact kernel: per-row heap state when it does not fit in LDS, and
+  // orh_spf_batch_exact's device rows
+  uint8_t* d_exact = nullptr;
+  size_t d_exact_cap = 0;  // in bytes
+  uint8_t* d_batch_x = nullptr;
+  size_t d_batch_x_cap = 0;  // in bytes
 };
 
 struct orh_graph {
@@ -74,6 +80,9 @@ struct orh_graph {
   uint32_t max_metric = 0;
   uint32_t min_out = 0, max_out = 0;  // w_out range over up CSR entries
   uint32_t mean_out = 1;               // mean w_out over up CSR entries
+  bool has_zero = false;               // an up CSR entry has w_out == 0
+  std::vector<uint32_t> name_rank;     // orh_csr::name_rank (identity when not given)
+  uint32_t* d_name_rank = nullptr;
   // device layout: ELL slots v*K .. v*K+K-1, the last one a continuation
   // record into the overflow area when deg(v) > K
   uint32_t ell_k = 4;
@@ -121,6 +130,8 @@ void free_graph_device(orh_graph* g) {
   (void)hipFree(g->d_ms_recs);
   (void)hipFree(g->d_ms_dev_of);
   (void)hipFree(g->d_ms_host_of);
+  (void)hipFree(g->d_name_rank);
+  g->d_name_rank = nullptr;
   g->d_ms_recs = nullptr;
   g->d_ms_dev_of = nullptr;
   g->d_ms_host_of = nullptr;
@@ -258,10 +269,13 @@ void build_ms_layout(orh_graph* g, std::vector<uint2>& recs) {
     }
   }
   // a slice (64 consecutive ids) reaches the slices within ceil(bw / 64);
-  // the kernel's dilation handles up to 31 (ORH_MS_SKIP=0 turns it off)
+  // the kernel's dilation handles up to 31. Opt-in (ORH_MS_SKIP=1): on the C2
+  // grid the skip variant measured 1.62 ms per all-sources sweep against
+  // 1.14 ms without it (profiles/r02/e_ab_skip.txt) - its extra registers
+  // (117 vs 74 VGPRs) cost more occupancy than the skipped slices save
   const uint32_t r = (bw + 63) / 64;
   const char* e = getenv("ORH_MS_SKIP");
-  g->ms_radius = (r <= 31 && !(e && atoi(e) == 0)) ? std::max(r, 1u) : 0u;
+  g->ms_radius = (r <= 31 && e && atoi(e) == 1) ? std::max(r, 1u) : 0u;
 }
 
 int sync_ms_layout(orh_graph* g) {
@@ -333,8 +347,10 @@ void recompute_bounds(orh_graph* g) {
   g->max_metric = 0;
   g->min_out = 0xFFFFFFFFu;
   g->max_out = 0;
+  g->has_zero = false;
   for (uint32_t e = 0; e < g->n_edges; ++e) {
     if (g->meta[e] & ORH_META_DOWN) continue;
+    g->has_zero |= g->w_out[e] == 0;
     const uint32_t m = std::max(g->w_out[e], g->w_in[e]);
     g->max_metric = std::max(g->max_metric, m);
     g->sum_max_metric += m;  // each link is counted twice (both CSR entries)
@@ -390,6 +406,22 @@ int ensure_scratch(orh_ctx* ctx, size_t words) {
   ORH_HIP(ctx, hipMalloc(&ctx->d_scratch, words * sizeof(uint32_t)));
   ctx->d_scratch_cap = words;
   return ORH_OK;
+}
+
+int ensure_bytes(orh_ctx* ctx, uint8_t** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return ORH_OK;
+  hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  ORH_HIP(ctx, hipMalloc(p, bytes));
+  *cap = bytes;
+  return ORH_OK;
+}
+
+// path metrics of the graph can reach the 32-bit sentinel (link metrics are
+// summed in 64 bits by the reference, LinkState.h:22)
+bool wide_metrics(const orh_graph* g) {
+  return g->sum_max_metric / 2 + g->max_metric >= 0xFFFFFFFFull;
 }
 
 int ensure_ms_lvl(orh_ctx* ctx, size_t bytes) {
@@ -458,6 +490,8 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_ms_lvl);
   hipFree(ctx->d_batch);
   hipFree(ctx->d_patch);
+  hipFree(ctx->d_exact);
+  hipFree(ctx->d_batch_x);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -555,12 +589,12 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   for (uint32_t v = 0; v < c->n_nodes; ++v)
     if (c->row_ptr[v] > c->row_ptr[v + 1])
       return fail(ctx, ORH_E_INVALID, "orh_graph_load: row_ptr not monotone");
-  for (uint32_t e = 0; e < c->n_edges; ++e) {
+  for (uint32_t e = 0; e < c->n_edges; ++e)
     if (c->col[e] >= c->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_graph_load: col out of range");
-    if (!(c->meta[e] & ORH_META_DOWN) && (c->w_out[e] == 0 || c->w_in[e] == 0))
-      return fail(ctx, ORH_E_UNSUPPORTED,
-                  "orh_graph_load: metric 0 on an up link (closed-form SPF needs metrics >= 1)");
-  }
+  if (c->name_rank)
+    for (uint32_t v = 0; v < c->n_nodes; ++v)
+      if (c->name_rank[v] >= c->n_nodes)
+        return fail(ctx, ORH_E_INVALID, "orh_graph_load: name_rank out of range");
   ORH_HIP(ctx, hipSetDevice(ctx->device));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   free_graph_device(g);
@@ -574,6 +608,8 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   g->meta.assign(c->meta, c->meta + c->n_edges);
   g->overloaded.assign(c->node_overloaded, c->node_overloaded + c->n_nodes);
   for (auto& o : g->overloaded) o = o ? 1 : 0;
+  g->name_rank.resize(c->n_nodes);
+  for (uint32_t v = 0; v < c->n_nodes; ++v) g->name_rank[v] = c->name_rank ? c->name_rank[v] : v;
   g->gen = next_graph_gen();
   g->row_of.assign(g->n_nodes, -1);
   recompute_bounds(g);
@@ -591,7 +627,8 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   if (hipMalloc(&g->d_recs, recs.size() * sizeof(uint2)) != hipSuccess ||
       hipMalloc(&g->d_link, link.size() * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&g->d_rank_out, rank.size() * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&g->d_ovl, nn) != hipSuccess) {
+      hipMalloc(&g->d_ovl, nn) != hipSuccess ||
+      hipMalloc(&g->d_name_rank, nn * sizeof(uint32_t)) != hipSuccess) {
     free_graph_device(g);
     return fail(ctx, ORH_E_NOMEM, "orh_graph_load: device allocation failed");
   }
@@ -601,9 +638,12 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
                               hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipMemcpyAsync(g->d_rank_out, rank.data(), rank.size() * sizeof(uint16_t),
                               hipMemcpyHostToDevice, ctx->stream));
-  if (g->n_nodes)
+  if (g->n_nodes) {
     ORH_HIP(ctx, hipMemcpyAsync(g->d_ovl, g->overloaded.data(), g->n_nodes, hipMemcpyHostToDevice,
                                 ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_name_rank, g->name_rank.data(), g->n_nodes * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, ctx->stream));
+  }
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
@@ -618,8 +658,6 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
     if (e >= g->n_edges) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: bad edge index");
     if ((meta[i] & ORH_META_LINK_MASK) != (g->meta[e] & ORH_META_LINK_MASK))
       return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: link id changed (use load)");
-    if (!(meta[i] & ORH_META_DOWN) && (w_out[i] == 0 || w_in[i] == 0))
-      return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_patch_edges: metric 0 on an up link");
   }
   ORH_HIP(ctx, hipSetDevice(ctx->device));
   std::vector<std::pair<uint32_t, uint32_t>> edges;
@@ -671,6 +709,12 @@ int orh_graph_device_flags(const orh_graph* g, const uint8_t** d_overloaded) {
   return ORH_OK;
 }
 
+int orh_graph_flags(const orh_graph* g, uint32_t* flags) {
+  if (!g || !flags) return ORH_E_INVALID;
+  *flags = (g->has_zero ? ORH_GRAPH_ZERO_METRIC : 0u) | (wide_metrics(g) ? ORH_GRAPH_WIDE_METRIC : 0u);
+  return ORH_OK;
+}
+
 int orh_graph_info(const orh_graph* g, uint32_t* n_nodes, uint32_t* n_edges) {
   if (!g) return ORH_E_INVALID;
   if (n_nodes) *n_nodes = g->n_nodes;
@@ -699,6 +743,87 @@ int orh_spf_words(const orh_graph* g, const uint32_t* srcs, uint32_t n, uint32_t
   return ORH_OK;
 }
 
+// The exact kernel (LinkState::runSpf's own extraction order): one wave per
+// requested row, nothing shared between rows. Rows run in chunks whose heap
+// state fits a bounded scratch when it is too large for LDS.
+static int run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32_t* d_dist32,
+                     uint64_t* d_dist64, uint32_t* d_nh, uint32_t* d_rank) {
+  orh_ctx* ctx = g->ctx;
+  const uint32_t n_src = req->n_src, N = g->n_nodes;
+  uint32_t max_nbr = 1;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    if (req->h_srcs[i] >= N) return fail(ctx, ORH_E_INVALID, "exact SPF: source out of range");
+    max_nbr = std::max(max_nbr, n_distinct(g, req->h_srcs[i]));
+  }
+  if (words < (max_nbr + 31) / 32) return fail(ctx, ORH_E_INVALID, "exact SPF: words too small");
+  hipSetDevice(ctx->device);
+  // staging: srcs[n_src] | ign_ptr[n_src + 1] ign[..] (ignore sets sorted for
+  // the device binary search)
+  const bool has_ign = req->h_ignore_ptr != nullptr;
+  std::vector<uint32_t> staging(req->h_srcs, req->h_srcs + n_src);
+  const size_t off_ign_ptr = staging.size();
+  if (has_ign) {
+    const size_t off_ign = off_ign_ptr + n_src + 1;
+    staging.resize(off_ign);
+    staging[off_ign_ptr] = 0;
+    for (uint32_t i = 0; i < n_src; ++i) {
+      std::vector<uint32_t> set(req->h_ignore_links + req->h_ignore_ptr[i],
+                                req->h_ignore_links + req->h_ignore_ptr[i + 1]);
+      std::sort(set.begin(), set.end());
+      staging.insert(staging.end(), set.begin(), set.end());
+      staging[off_ign_ptr + i + 1] = static_cast<uint32_t>(staging.size() - off_ign);
+    }
+  }
+  int rc = ensure_req(ctx, staging.size());
+  if (rc) return rc;
+  ctx->req_key.clear();  // the staged request of orh_spf_run is overwritten
+  ORH_HIP(ctx, hipMemcpyAsync(ctx->d_req, staging.data(), staging.size() * 4, hipMemcpyHostToDevice,
+                              ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
+  orh::ExactArgs a{};
+  a.n_nodes = N;
+  a.words = words;
+  a.use_link_metric = req->use_link_metric;
+  a.ell_k = g->ell_k;
+  a.recs = g->d_recs;
+  a.link = g->d_link;
+  a.rank_out = g->d_rank_out;
+  a.name_rank = g->d_name_rank;
+  a.ignore_links = has_ign ? ctx->d_req + off_ign_ptr + n_src + 1 : nullptr;
+  const size_t state = orh::exact_state_bytes(N, words);
+  uint32_t chunk = n_src;
+  if (state > ctx->lds_limit) {  // per-row global heap state, at most 1 GiB at a time
+    chunk = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(n_src, (size_t{1} << 30) / state)));
+    rc = ensure_bytes(ctx, &ctx->d_exact, &ctx->d_exact_cap, state * chunk);
+    if (rc) return rc;
+    a.scratch = ctx->d_exact;
+    a.scratch_stride = state;
+  }
+  ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  for (uint32_t r0 = 0; r0 < n_src; r0 += chunk) {
+    const size_t base = static_cast<size_t>(r0) * N;
+    a.n_rows = std::min(chunk, n_src - r0);
+    a.srcs = ctx->d_req + r0;
+    a.ignore_ptr = has_ign ? ctx->d_req + off_ign_ptr + r0 : nullptr;
+    a.out_dist32 = d_dist32 ? d_dist32 + base : nullptr;
+    a.out_dist64 = d_dist64 ? d_dist64 + base : nullptr;
+    a.out_nh = d_nh + base * words;
+    a.out_rank = d_rank ? d_rank + base : nullptr;
+    hipError_t e = orh::launch_exact(a, ctx->lds_limit, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "exact SPF kernel launch");
+  }
+  ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
+  ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  orh_spf_info info{};
+  info.variant = static_cast<int32_t>(orh::SpfVariant::kExact);
+  info.rows = n_src;
+  ctx->last_info = info;
+  ctx->counters.spf_runs += n_src;
+  ctx->counters.spf_launches += 1;
+  ctx->counters.last_kernel_ms = -1.0;
+  return ORH_OK;
+}
+
 // Phase 1 computes a distance row for every requested source and for every
 // distinct neighbour of one (the first-hop phase reads them). Without ignore
 // sets rows are shared by node: a neighbour that is itself requested reuses
@@ -718,6 +843,14 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     max_nbr = std::max(max_nbr, n_distinct(g, req->h_srcs[i]));
   }
   if (words < (max_nbr + 31) / 32) return fail(ctx, ORH_E_INVALID, "orh_spf_run: words too small");
+  // zero link metrics: the first hops depend on the extraction order among
+  // equal-metric nodes, which only the exact kernel follows
+  if (ctx->spf_mode == orh::SpfMode::kExact || (req->use_link_metric && g->has_zero)) {
+    if (req->use_link_metric && wide_metrics(g))
+      return fail(ctx, ORH_E_UNSUPPORTED,
+                  "orh_spf_run: path metrics may reach 2^32 - 1 (use orh_spf_run_exact)");
+    return run_exact(g, req, words, d_dist, nullptr, d_nh, nullptr);
+  }
   const bool uniform = !req->use_link_metric || g->min_out == g->max_out;
   const uint32_t w0 = req->use_link_metric ? g->max_out : 1u;
   // any tentative value is at most (sum of link metrics) + max metric; BFS
@@ -731,7 +864,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   if (plan.variant == orh::SpfVariant::kUnsupported)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: no distance kernel for this graph (N=" +
                                             std::to_string(N) + ", path bound " +
-                                            std::to_string(bound) + ")");
+                                            std::to_string(bound) + "; orh_spf_run_exact covers it)");
   if (orh::hop_lds_bytes(max_nbr) > ctx->lds_limit)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_spf_run: too many neighbours for the first-hop phase");
   hipSetDevice(ctx->device);
@@ -1004,6 +1137,48 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
       e = hipMemcpyAsync(h_nh, d_nh, nd * words * 4, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) rc = hip_fail(ctx, e, "orh_spf_batch: copy-out");
+    float ms = 0.f;
+    if (rc == ORH_OK && hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) {
+      ctx->counters.last_kernel_ms = ms;
+      ctx->counters.total_kernel_ms += ms;
+    }
+  }
+  return rc;
+}
+
+int orh_spf_run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint64_t* d_dist,
+                      uint32_t* d_nh, uint32_t* d_rank) {
+  if (!g || !req || (req->n_src && (!req->h_srcs || !d_dist || !d_nh)))
+    return g ? fail(g->ctx, ORH_E_INVALID, "orh_spf_run_exact: null argument") : ORH_E_INVALID;
+  if (req->n_src == 0) return ORH_OK;
+  if (!g->d_recs || g->n_nodes == 0)
+    return fail(g->ctx, ORH_E_STATE, "orh_spf_run_exact: no graph loaded");
+  return run_exact(g, req, words, nullptr, d_dist, d_nh, d_rank);
+}
+
+int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint64_t* h_dist,
+                        uint32_t* h_nh, uint32_t* h_rank) {
+  if (!g || !req) return ORH_E_INVALID;
+  orh_ctx* ctx = g->ctx;
+  if (req->n_src == 0) return ORH_OK;
+  if (!h_dist || !h_nh) return fail(ctx, ORH_E_INVALID, "orh_spf_batch_exact: null output");
+  const size_t nd = static_cast<size_t>(req->n_src) * g->n_nodes;
+  const size_t bytes = nd * 8 + nd * words * 4 + nd * 4;
+  hipSetDevice(ctx->device);
+  int rc = ensure_bytes(ctx, &ctx->d_batch_x, &ctx->d_batch_x_cap, bytes);
+  if (rc) return fail(ctx, ORH_E_NOMEM, "orh_spf_batch_exact: device allocation failed");
+  uint64_t* d_dist = reinterpret_cast<uint64_t*>(ctx->d_batch_x);
+  uint32_t* d_nh = reinterpret_cast<uint32_t*>(d_dist + nd);
+  uint32_t* d_rank = d_nh + nd * words;
+  rc = orh_spf_run_exact(g, req, words, d_dist, d_nh, h_rank ? d_rank : nullptr);
+  if (rc == ORH_OK) {
+    hipError_t e = hipMemcpyAsync(h_dist, d_dist, nd * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h_nh, d_nh, nd * words * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && h_rank)
+      e = hipMemcpyAsync(h_rank, d_rank, nd * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = hip_fail(ctx, e, "orh_spf_batch_exact: copy-out");
     float ms = 0.f;
     if (rc == ORH_OK && hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) {
       ctx->counters.last_kernel_ms = ms;

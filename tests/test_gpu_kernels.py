@@ -20,7 +20,7 @@ from test_gpu_parity import random_topology, spf_view
 
 pytestmark = pytest.mark.gpu
 A = K_TESTING_AREA
-MODES = {"auto": 0, "per_source": 1, "global": 2, "global_two_phase": 3}
+MODES = {"auto": 0, "per_source": 1, "global": 2, "global_two_phase": 3, "exact": 4}
 
 
 @pytest.fixture(params=list(MODES))

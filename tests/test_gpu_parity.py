@@ -19,7 +19,7 @@ A = K_TESTING_AREA
 
 
 def random_topology(seed, n=24, extra=30, max_metric=20, parallel=0.15, overload=0.1,
-                    link_overload=0.05):
+                    link_overload=0.05, min_metric=1):
     """Seeded graph with parallel links, directional metrics, drained nodes
     and drained adjacencies (both link-down and node-overload semantics)."""
     rng = random.Random(seed)
@@ -37,7 +37,7 @@ def random_topology(seed, n=24, extra=30, max_metric=20, parallel=0.15, overload
         for _ in range(reps):
             k = count.get((a, b), 0) + count.get((b, a), 0)
             count[(a, b)] = count.get((a, b), 0) + 1
-            m_ab, m_ba = rng.randint(1, max_metric), rng.randint(1, max_metric)
+            m_ab, m_ba = rng.randint(min_metric, max_metric), rng.randint(min_metric, max_metric)
             # adjacency labels unique per node (the reference CHECKs duplicates)
             ab = create_adjacency(f"n{b}", f"{a}-{b}-{k}", f"{b}-{a}-{k}", f"fe80::{a}:{b}:{k}",
                                   f"10.{a}.{b}.{k}", m_ab, 10000 + a * 256 + len(adjs[a]))
