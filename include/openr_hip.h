@@ -144,10 +144,11 @@ int orh_set_spf_mode(orh_ctx* ctx, int mode);
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */
-  uint32_t mask_bits;  /* MS-BFS: sources per workgroup (32 or 16), else 0 */
+  uint32_t mask_bits;  /* MS-BFS: source-mask width (64, 32 or 16), else 0 */
   uint32_t hop_nodes;  /* first-hop phase: nodes per thread over u8 level rows
                           (16 or 4), 1 for the u32-row kernel, 0 when fused */
   uint32_t hop_split;  /* first-hop phase: workgroups per source */
+  uint32_t batch_sources; /* MS-BFS: sources per workgroup (<= mask_bits), else 0 */
 } orh_spf_info;
 int orh_last_spf_info(const orh_ctx* ctx, orh_spf_info* out);
 /* device time (HIP events on the context stream) of the last orh_spf_run;

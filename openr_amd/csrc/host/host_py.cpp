@@ -341,6 +341,7 @@ class SpfSweep {
     d["variant"] = i.variant;
     d["rows"] = i.rows;
     d["mask_bits"] = i.mask_bits;
+    d["batch_sources"] = i.batch_sources;
     d["hop_nodes"] = i.hop_nodes;
     d["hop_split"] = i.hop_split;
     return d;

@@ -26,7 +26,8 @@ struct SpfArgs {
   uint8_t* ms_lvl;            // multi-source BFS: node-major level bytes [batches][N][S]
   uint32_t ms_pitch;          // multi-source BFS: frontier-array entries (> N)
   uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
-  uint32_t ms_radius;         // multi-source BFS: neighbour reach in 64-node slices (0: no skip)
+  uint32_t ms_bw;             // multi-source BFS: layout bandwidth for the interval skip (0: no skip)
+  uint32_t ms_width;          // multi-source BFS: sources per batch (<= mask bits)
   const uint2* recs;       // ELL slots [N * K] then overflow records
   const uint32_t* link;    // per record: link id (ignore sets)
   const uint32_t* srcs;    // [n_rows]
@@ -126,7 +127,8 @@ struct SpfPlan {
   SpfVariant variant;
   uint32_t ell_k;
   uint32_t block;
-  uint32_t mask_bytes;  // multi-source BFS: source-mask width (S = 8 * mask_bytes)
+  uint32_t mask_bytes;  // multi-source BFS: source-mask width (up to 8 * mask_bytes sources)
+  uint32_t ms_width;    // multi-source BFS: sources per batch (ms_set_width)
   uint32_t ms_j;        // multi-source BFS: nodes owned per thread (template)
   uint32_t ms_pitch;    // multi-source BFS: frontier-array entries
   size_t pend_off;
@@ -139,6 +141,9 @@ struct SpfPlan {
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
                  size_t lds_limit, bool multi_source, SpfMode mode);
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
+// multi-source plans, once the row count is known: sources per batch, and
+// u64 masks when u32 ones would put more than one batch on a CU
+void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit);
 // bytes of node-major level scratch a multi-source plan needs for n_rows rows
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
 

@@ -290,17 +290,17 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_kernel(SpfArgs a) {
 // >= 254 are written to the output row directly (marker 254), so any depth is
 // exact; 255 = unreached.
 //
-// Activity skip: nodes are numbered in Cuthill-McKee order, so every live
-// record v -> u has |u - v| <= bandwidth. A 64-node slice (one wave's nodes
-// of one j) can only gain bits at level L if some slice within
-// ms_radius = ceil(bandwidth / 64) had a new bit at level L-1; every other
-// slice is skipped without reading its neighbours' frontier entries (their
-// stale entries only repeat visited bits, see below). Slice activity lives in
-// three rotating LDS bitmaps; each wave dilates the previous level's bitmap
-// by the radius in registers (lanes 0..15 hold one 32-slice word each) and
-// reads its slices' bits with readlane. On the 10k grid this skips the
-// unreached and settled bands around the frontier: ~30-70 % of the wave
-// groups of a batch, most for the corner batches that set the sweep time.
+// Interval skip (kSkip): nodes are numbered in Cuthill-McKee order, so every
+// live record v -> u has |u - v| <= bw (the layout's bandwidth). If the nodes
+// that gained a bit at level L-1 span the ids [lo, hi], only nodes in
+// [lo - bw, hi + bw] can gain one at level L; a 64-node slice (one wave's
+// nodes of one j) outside it is skipped without reading its neighbours'
+// frontier entries. The interval is two LDS words per level (wave min / max
+// reductions); the per-slice test is scalar, so the variant costs no VGPRs
+// beyond the two running bounds (a slice-bitmap form of the same skip needed
+// 117 VGPRs, one workgroup per CU, and ran 1.4x slower). A skipped node keeps
+// a stale f_nxt entry from two levels back: its bits reached every neighbour
+// by the previous level, so it only repeats visited bits (see below).
 //
 // The search is latency-bound, not LDS-bound: on the 10k grid one workgroup
 // takes ~0.7 ms whether 32 or 313 of them run (two fit per CU), ~165 levels
@@ -313,13 +313,24 @@ constexpr uint32_t kLvlDirect = 254u, kLvlNone = 255u;
 
 template <class M>
 struct MsMask;
+// V: the register type of a node's visited / new bits
+template <>
+struct MsMask<uint64_t> {
+  static constexpr uint32_t kS = 64;
+  typedef uint64_t V;
+  __device__ static uint32_t ctz(uint64_t x) { return static_cast<uint32_t>(__builtin_ctzll(x)); }
+};
 template <>
 struct MsMask<uint32_t> {
   static constexpr uint32_t kS = 32;
+  typedef uint32_t V;
+  __device__ static uint32_t ctz(uint32_t x) { return static_cast<uint32_t>(__builtin_ctz(x)); }
 };
 template <>
 struct MsMask<uint16_t> {
   static constexpr uint32_t kS = 16;
+  typedef uint32_t V;
+  __device__ static uint32_t ctz(uint32_t x) { return static_cast<uint32_t>(__builtin_ctz(x)); }
 };
 
 __device__ inline uint32_t ms_col(const uint2& r, uint32_t zero) {
@@ -350,22 +361,29 @@ template <int K, class M, int J, bool kSkip>
 __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t kS = MsMask<M>::kS;
+  typedef typename MsMask<M>::V V;
   constexpr int KH = (K + 1) / 2;
   const uint32_t N = a.n_nodes;
   const uint32_t NZ = a.ms_zero;  // index of the always-zero frontier entry
   const uint32_t tid = threadIdx.x, B = blockDim.x;
-  const uint32_t b0 = blockIdx.x * kS;
-  const uint32_t S = min(kS, a.n_rows - b0);
-  const uint32_t full = S == 32u ? 0xFFFFFFFFu : (1u << S) - 1u;
+  const uint32_t b0 = blockIdx.x * a.ms_width;  // a batch: ms_width <= kS sources
+  const uint32_t S = min(a.ms_width, a.n_rows - b0);
+  const V full = S >= 8 * sizeof(V) ? ~V(0) : (V(1) << S) - V(1);
   __shared__ uint32_t s_prog[3];
-  __shared__ uint32_t s_act[3][16];  // slice activity (<= 512 slices of 64 nodes)
+  __shared__ uint32_t s_lo[3], s_hin[3];  // per level: min / ~max id with a new frontier bit
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
   uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
+#ifdef ORH_DIAG_STAMPS
+  const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
 
   for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
-  if (tid < 3) s_prog[tid] = 0u;
-  if (tid < 48) (&s_act[0][0])[tid] = 0u;
+  if (tid < 3) {
+    s_prog[tid] = 0u;
+    s_lo[tid] = ~0u;
+    s_hin[tid] = ~0u;
+  }
   {  // every level byte starts as "unreached"
     uint4* l4 = reinterpret_cast<uint4*>(lvl);
     for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -373,19 +391,18 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   __syncthreads();
   if (tid < S) {  // sources may repeat: OR the bits in
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
-    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f_cur + src) & ~uintptr_t(3));
-    const uint32_t sh = (reinterpret_cast<uintptr_t>(f_cur + src) & 3u) * 8u;
-    atomicOr(w, (1u << tid) << sh);
+    const uintptr_t byte = reinterpret_cast<uintptr_t>(f_cur + src) + tid / 8u;
+    atomicOr(reinterpret_cast<uint32_t*>(byte & ~uintptr_t(3)), 1u << ((byte & 3u) * 8u + (tid & 7u)));
     lvl[static_cast<size_t>(src) * kS + tid] = 0;
   }
-  __syncthreads();  // s_act zeroed before the sources mark their slices
-  if (tid < S) {
-    const uint32_t k = a.dev_of[a.srcs[a.order[b0 + tid]]] >> 6;
-    atomicOr(&s_act[0][k >> 5], 1u << (k & 31u));
+  if (kSkip && tid < S) {  // level 0's frontier: the sources
+    const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
+    atomicMin(&s_lo[0], src);
+    atomicMin(&s_hin[0], ~src);
   }
 
   uint32_t col[J][KH];
-  uint32_t vis[J];
+  V vis[J];
   uint32_t ovlm = 0u, ovfm = 0u;  // bit j: owned node j overloaded / has an overflow list
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -418,8 +435,8 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
   uint64_t t_bar = 0, t_store = 0;
   uint32_t n_levels = 0;
 #endif
-  const uint32_t R = a.ms_radius;
-  const uint32_t lane = tid & 63u, wave = tid >> 6, nwaves = B >> 6;
+  const uint32_t bw = a.ms_bw;
+  const uint32_t wave_base = __builtin_amdgcn_readfirstlane(tid & ~63u);
   for (uint32_t level = 1;; ++level) {
     int prog = 0;
     // opaque per level: keeps the compiler from hoisting J * K unpacked LDS
@@ -427,43 +444,41 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
-    // slices of this wave (j, wave) whose neighbourhood had a new bit at the
-    // previous level: bit j of amask (all ones without the skip)
-    uint32_t amask = 0xFFFFFFFFu, jm = 0u;
+    // ids that can gain a bit at this level: within bw of the previous
+    // level's new frontier (scalar; empty when the frontier was)
+    uint32_t reach_lo = 0u, reach_hi = ~0u, jm = 0u;  // jm: this wave's slices with a new frontier bit
+    // first id of this wave's slice j0 (advanced by B per slice; opaque per
+    // level so the 16 slice bases are not hoisted into SGPRs that spill)
+    uint32_t slice = wave_base;
+    if constexpr (kSkip) asm volatile("" : "+s"(slice));
     if constexpr (kSkip) {
-      if (tid < 16) s_act[(level + 1u) % 3u][tid] = 0u;  // read at level - 1, written at level + 1
-      // previous level's active slices dilated by R: lane l < 16 holds word l
-      const uint32_t* prev = s_act[(level + 2u) % 3u];
-      uint32_t dil = 0u;
-      if (lane < 16) {
-        const uint64_t p = lane ? prev[lane - 1] : 0u, c = prev[lane], n = lane < 15 ? prev[lane + 1] : 0u;
-        const uint64_t lo = (c << 32) | p, hi = (n << 32) | c;
-        for (uint32_t d = 0; d <= R; ++d)
-          dil |= static_cast<uint32_t>((lo << d) >> 32) | static_cast<uint32_t>(hi >> d);
-      }
-      amask = 0u;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const uint32_t k = j * nwaves + wave;
-        const uint32_t wd = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dil), k >> 5));
-        amask |= ((wd >> (k & 31u)) & 1u) << j;
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(s_lo[(level + 2u) % 3u]);
+      const uint32_t hi = ~__builtin_amdgcn_readfirstlane(s_hin[(level + 2u) % 3u]);
+      reach_lo = lo > bw ? lo - bw : 0u;
+      reach_hi = hi + bw;
+      if (tid < 1) {  // read at level - 1, written at level + 1
+        s_lo[(level + 1u) % 3u] = ~0u;
+        s_hin[(level + 1u) % 3u] = ~0u;
       }
     }
     // groups of G owned nodes: a group is skipped when every lane holds all
     // bits for all G nodes (wave-uniform branch); otherwise all G * K
-    // frontier reads go out back to back before any is consumed
-    constexpr int G = 4;
+    // frontier reads go out back to back before any is consumed. The skip
+    // variant tests single slices (G = 1): its active band is a slice or two
+    // per wave, and a group of 4 would do 2-4x the reads the band needs
+    constexpr int G = kSkip ? 1 : 4;
 #pragma unroll
     for (int j0 = 0; j0 < J; j0 += G) {
+      const uint32_t sl = slice;
+      if constexpr (kSkip) slice += B;
       bool open = false;
 #pragma unroll
       for (int g = 0; g < G; ++g) open |= vis[j0 + g] != full;
       if (!__builtin_amdgcn_ballot_w64(open)) continue;
-      // no frontier within reach of any of the G slices: nothing can arrive,
-      // and the group's f_nxt entries stay stale (harmless, see above); an
-      // active group processes all G nodes (branch-free loads)
-      if (kSkip && !((amask >> j0) & ((1u << G) - 1u))) continue;
-      uint32_t acc[G];
+      // no new frontier within reach of the slice: nothing can arrive, and
+      // its f_nxt entries stay stale (harmless, see above)
+      if (kSkip && (sl > reach_hi || sl + 63u < reach_lo)) continue;
+      V acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -481,7 +496,7 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
       for (int g = 0; g < G; ++g) {
         const int j = j0 + g;
         const uint32_t v = j * B + me;
-        uint32_t nx = 0u;
+        V nx = 0u;
         if (vis[j] != full) {  // also every v >= N
           if ((ovfm >> j) & 1u) {
             const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
@@ -503,11 +518,11 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
           {
           uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
           if (level < kLvlDirect) {
-            for (uint32_t q = nx; q; q &= q - 1) lb[__builtin_ctz(q)] = static_cast<uint8_t>(level);
+            for (V q = nx; q; q &= q - 1) lb[MsMask<M>::ctz(q)] = static_cast<uint8_t>(level);
           } else {
             const uint32_t vh = a.host_of[v];
-            for (uint32_t q = nx; q; q &= q - 1) {
-              const uint32_t b = __builtin_ctz(q);
+            for (V q = nx; q; q &= q - 1) {
+              const uint32_t b = MsMask<M>::ctz(q);
               lb[b] = kLvlDirect;
               dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
             }
@@ -522,17 +537,16 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
           if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
           f_nxt[v] = static_cast<M>(nx);
         }
-        if constexpr (kSkip) jm |= (nx != 0u ? 1u : 0u) << j;
+        if constexpr (kSkip) jm |= (__builtin_amdgcn_ballot_w64(nx != 0u) != 0u ? 1u : 0u) << j;
       }
     }
-    if constexpr (kSkip) {  // this wave's slices with a new bit, into the level's bitmap
-      uint32_t* act_now = s_act[level % 3u];
-      uint32_t wm = wave_or(jm);
-      if (lane == 0)
-        for (; wm; wm &= wm - 1) {
-          const uint32_t k = static_cast<uint32_t>(__builtin_ctz(wm)) * nwaves + wave;
-          atomicOr(&act_now[k >> 5], 1u << (k & 31u));
-        }
+    if constexpr (kSkip) {  // this wave's new-frontier slices into the level's interval
+      if (jm && (tid & 63u) == 0) {
+        const uint32_t jl = static_cast<uint32_t>(__builtin_ctz(jm));
+        const uint32_t jh = 31u - static_cast<uint32_t>(__builtin_clz(jm));
+        atomicMin(&s_lo[level % 3u], jl * B + wave_base);
+        atomicMin(&s_hin[level % 3u], ~(jh * B + wave_base + 63u));
+      }
     }
     // every level that makes progress adds >= 1 visited bit: at most S * N
     // levels. The barrier waits for LDS traffic only: the level bytes on
@@ -554,6 +568,14 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     f_nxt = t;
   }
 #ifdef ORH_DIAG_STAMPS
+  if (tid == 0 && blockIdx.x < 4096) {  // per workgroup: entry, exit, hardware id, levels
+    uint64_t* w = a.diag + 16 + 4 * static_cast<size_t>(blockIdx.x);
+    w[0] = t_entry;
+    w[1] = __builtin_amdgcn_s_memtime();
+    w[2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF804)) |
+           (static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32);
+    w[3] = n_levels;
+  }
   if ((tid & 63u) == 0) {  // per wave: total, barrier and store-block cycles, levels
     const uint64_t tot = __builtin_amdgcn_s_memtime() - t_begin;
     atomicAdd(reinterpret_cast<unsigned long long*>(&a.diag[0]), tot);
@@ -578,8 +600,8 @@ __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t ti
   const uint32_t N = a.n_nodes;
   const uint32_t batch = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const uint32_t i = tile * 256 + threadIdx.x;
-  const uint32_t b0 = batch * kS;
-  const uint32_t S = min(kS, a.n_rows - b0);
+  const uint32_t b0 = batch * a.ms_width;
+  const uint32_t S = min(a.ms_width, a.n_rows - b0);
   if (threadIdx.x < S) {
     s_row[threadIdx.x] = a.order[b0 + threadIdx.x];
     s_out[threadIdx.x] = dist_row(a.out_dist, a.scratch, a.n_out, N, s_row[threadIdx.x]);
@@ -1589,9 +1611,9 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
 
 template <int K, class M, int J>
 static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
-  constexpr uint32_t kS = MsMask<M>::kS;
-  const uint32_t batches = (n_rows + kS - 1) / kS;
-  if (a.ms_radius)
+  if (a.ms_width == 0 || a.ms_width > MsMask<M>::kS) return hipErrorInvalidValue;
+  const uint32_t batches = (n_rows + a.ms_width - 1) / a.ms_width;
+  if (a.ms_bw)
     return launch(spf_msbfs_kernel<K, M, J, true>, a, batches, plan.block, plan.lds_bytes, s);
   return launch(spf_msbfs_kernel<K, M, J, false>, a, batches, plan.block, plan.lds_bytes, s);
 }
@@ -1616,14 +1638,36 @@ static hipError_t launch_ms(const SpfPlan& plan, const SpfArgs& a, uint32_t n_ro
   switch (plan.mask_bytes) {
     case 2: return launch_ms_m<K, uint16_t>(plan, a, n_rows, s);
     case 4: return launch_ms_m<K, uint32_t>(plan, a, n_rows, s);
+    case 8: return launch_ms_m<K, uint64_t>(plan, a, n_rows, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows) {
-  if (plan.variant != SpfVariant::kMsBfs) return 0;
-  const uint32_t s = plan.mask_bytes * 8;
-  return static_cast<size_t>((n_rows + s - 1) / s) * n_nodes * s;
+  if (plan.variant != SpfVariant::kMsBfs || plan.ms_width == 0) return 0;
+  const uint32_t w = plan.ms_width;
+  return static_cast<size_t>((n_rows + w - 1) / w) * n_nodes * (plan.mask_bytes * 8);
+}
+
+void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit) {
+  if (plan.variant != SpfVariant::kMsBfs) return;
+  plan.ms_width = plan.mask_bytes * 8;
+  // ORH_MS_WIDE=1 (opt-in): when u32 masks need more than one batch per CU
+  // and u64 frontier arrays fit in LDS, widen the masks and spread the rows
+  // over at most n_cu batches of ceil(n_rows / n_cu) sources. On C2 (250
+  // batches of 40) this swept in 0.86-0.92 ms against 0.75 for 313 u32
+  // batches: the batches that share a CU are not the slow ones
+  // (per-workgroup stamps, profiles/r02/msbfs_ab.md), and u64 masks cost more
+  // per level than they save
+  const size_t bytes64 = 2 * 8 * static_cast<size_t>(plan.ms_pitch);
+  const char* e = getenv("ORH_MS_WIDE");
+  const bool allow = e && atoi(e) == 1;
+  if (allow && plan.mask_bytes == 4 && n_cu && n_rows > 32ull * n_cu && bytes64 <= lds_limit) {
+    plan.mask_bytes = 8;
+    plan.lds_bytes = bytes64;
+    plan.ms_width = std::min<uint32_t>(64, (n_rows + n_cu - 1) / n_cu);
+  }
+  (void)n_nodes;
 }
 
 template <int K>
@@ -1694,13 +1738,15 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
 hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {
   if (plan.variant != SpfVariant::kMsBfs || n_rows == 0) return hipErrorInvalidValue;
   a.n_rows = n_rows;
-  const uint32_t kS = plan.mask_bytes * 8;
-  const uint32_t batches = (n_rows + kS - 1) / kS;
+  if (a.ms_width == 0 || a.ms_width > plan.mask_bytes * 8) return hipErrorInvalidValue;
+  const uint32_t batches = (n_rows + a.ms_width - 1) / a.ms_width;
   const uint32_t tiles = (a.n_nodes + 255) / 256;
   if (plan.mask_bytes == 2)
     hipLaunchKernelGGL(ms_finalize_kernel<uint16_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
-  else
+  else if (plan.mask_bytes == 4)
     hipLaunchKernelGGL(ms_finalize_kernel<uint32_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
+  else
+    hipLaunchKernelGGL(ms_finalize_kernel<uint64_t>, dim3(batches * tiles), dim3(256), 0, s, a, tiles);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ struct orh_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;  // around phase 1 | phase 2
   size_t lds_limit = 160 * 1024;
+  uint32_t n_cu = 256;  // compute units (multi-source batch sizing)
   orh::SpfMode spf_mode = orh::SpfMode::kAuto;  // orh_set_spf_mode
   // ORH_DELTA_PCT: HBM-kernel near/far width in % of the mean live metric;
   // 50 measured best on the C4 WAN what-if batch (25: 12.4, 50: 11.9,
@@ -98,7 +99,7 @@ struct orh_graph {
   // after attribute patches. Rows in HBM are always indexed by host id.
   std::vector<uint32_t> ms_dev_of, ms_host_of;  // host -> CM id, CM id -> host
   bool ms_dirty = true;
-  uint32_t ms_radius = 0;  // ceil(CM bandwidth / 64) over live records, 0 if > 31
+  uint32_t ms_bw = 0;  // CM bandwidth over live records when the interval skip is on, else 0
   uint2* d_ms_recs = nullptr;
   uint32_t* d_ms_dev_of = nullptr;
   uint32_t* d_ms_host_of = nullptr;
@@ -268,14 +269,14 @@ void build_ms_layout(orh_graph* g, std::vector<uint2>& recs) {
       for (uint32_t j = inl; j < d; ++j) put(ovf++, dv, v, e0 + j);
     }
   }
-  // a slice (64 consecutive ids) reaches the slices within ceil(bw / 64);
-  // the kernel's dilation handles up to 31. Opt-in (ORH_MS_SKIP=1): on the C2
-  // grid the skip variant measured 1.62 ms per all-sources sweep against
-  // 1.14 ms without it (profiles/r02/e_ab_skip.txt) - its extra registers
-  // (117 vs 74 VGPRs) cost more occupancy than the skipped slices save
-  const uint32_t r = (bw + 63) / 64;
+  // interval skip (spf_msbfs_kernel<..., true>), opt-in with ORH_MS_SKIP=1:
+  // it cuts a lone corner batch of the C2 grid from 0.48 to 0.32 ms, but the
+  // all-sources sweep stays at 0.75-0.77 ms either way (profiles/r02/
+  // msbfs_ab.md: with every CU busy the level-byte stores, not the skipped
+  // slices, set the time)
   const char* e = getenv("ORH_MS_SKIP");
-  g->ms_radius = (r <= 31 && e && atoi(e) == 1) ? std::max(r, 1u) : 0u;
+  const bool on = e && atoi(e) == 1;
+  g->ms_bw = on ? std::max(bw, 1u) : 0u;
 }
 
 int sync_ms_layout(orh_graph* g) {
@@ -468,6 +469,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
+    if (prop.multiProcessorCount > 0) ctx->n_cu = static_cast<uint32_t>(prop.multiProcessorCount);
   }
   *out = ctx;
   return ORH_OK;
@@ -952,8 +954,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     staging.insert(staging.end(), nbr_ptr.begin(), nbr_ptr.end());
     off_nbr_row = staging.size();
     staging.insert(staging.end(), nbr_row.begin(), nbr_row.end());
-    // multi-source batches: rows in ascending device id of their source, so
-    // a batch's sources are neighbours in the Cuthill-McKee order
+    // multi-source batches (consecutive runs of ms_width rows): rows in
+    // ascending Cuthill-McKee id of their source, so a batch's sources are
+    // neighbours. (Measured alternatives on C2: BFS balls of 32 rows - 10.6
+    // arrival levels per node and batch against 16.4 - swept in 0.92 ms
+    // against 0.77; dispatching the batches middle-out changed nothing.)
     off_order = staging.size();
     {
       std::vector<uint32_t> order(n_rows);
@@ -990,6 +995,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // when one mask word covers every source and the two-phase scheme would
   // need extra neighbour rows (or the HBM kernel is forced)
   orh::SpfPlan run_plan = plan;
+  orh::ms_set_width(run_plan, N, n_rows, ctx->n_cu, ctx->lds_limit);
   if (plan.variant == orh::SpfVariant::kGlobal && max_nbr <= 32 &&
       ctx->spf_mode != orh::SpfMode::kGlobalTwoPhase &&
       (ctx->spf_mode == orh::SpfMode::kGlobal || n_rows > n_src)) {
@@ -1013,8 +1019,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   if (plan.variant == orh::SpfVariant::kMsBfs) {
     int rc = sync_ms_layout(g);
     if (rc) return rc;
-    a.ms_radius = g->ms_radius;
-    rc = ensure_ms_lvl(ctx, orh::ms_scratch_bytes(plan, N, n_rows));
+    a.ms_bw = g->ms_bw;
+    a.ms_width = run_plan.ms_width;
+    rc = ensure_ms_lvl(ctx, orh::ms_scratch_bytes(run_plan, N, n_rows));
     if (rc) return rc;
     a.recs = g->d_ms_recs;
     a.dev_of = g->d_ms_dev_of;
@@ -1069,8 +1076,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
 #ifdef ORH_DIAG_STAMPS
   static uint64_t* d_diag = nullptr;
-  if (!d_diag) hipMalloc(&d_diag, 128);
-  hipMemsetAsync(d_diag, 0, 128, ctx->stream);
+  constexpr size_t kDiagWords = 16 + 4 * 4096;
+  if (!d_diag) hipMalloc(&d_diag, kDiagWords * 8);
+  hipMemsetAsync(d_diag, 0, kDiagWords * 8, ctx->stream);
   a.diag = d_diag;
 #endif
   {
@@ -1081,13 +1089,44 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   if (e != hipSuccess) { std::string m = "spf kernel launch variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + " lds " + std::to_string(run_plan.lds_bytes) + " block " + std::to_string(run_plan.block) + " j " + std::to_string(run_plan.ms_j); return hip_fail(ctx, e, m.c_str()); }
 #ifdef ORH_DIAG_STAMPS
   {
-    uint64_t h[16] = {};
-    hipMemcpyAsync(h, d_diag, 128, hipMemcpyDeviceToHost, ctx->stream);
+    std::vector<uint64_t> h(kDiagWords);
+    hipMemcpyAsync(h.data(), d_diag, kDiagWords * 8, hipMemcpyDeviceToHost, ctx->stream);
     hipStreamSynchronize(ctx->stream);
     if (h[4])
       fprintf(stderr, "diag: waves %llu avg cycles %.0f barrier %.0f groups/wave %.1f levels %.1f max cycles %llu max levels %llu read %.0f proc %.0f\n",
               (unsigned long long)h[4], double(h[0]) / h[4], double(h[1]) / h[4],
               double(h[2]) / h[4], double(h[3]) / h[4], (unsigned long long)h[5], (unsigned long long)h[6], double(h[7]) / h[4], double(h[8]) / h[4]);
+    // per workgroup: duration, and how many workgroups shared its CU at any time
+    struct Wg { uint64_t t0, t1, cu; uint32_t lv, b; };
+    std::vector<Wg> wg;
+    for (uint32_t b = 0; b < 4096; ++b) {
+      const uint64_t* w = &h[16 + 4 * b];
+      if (!w[1]) continue;
+      const uint64_t hw = w[2];
+      // HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]; XCC_ID in the high word
+      const uint64_t cu = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 7) << 5) | ((hw >> 32) & 0xF) << 8;
+      wg.push_back({w[0], w[1], cu, static_cast<uint32_t>(w[3]), b});
+    }
+    if (!wg.empty()) {
+      uint64_t t_min = ~0ull, t_max = 0;
+      for (auto& x : wg) { t_min = std::min(t_min, x.t0); t_max = std::max(t_max, x.t1); }
+      std::vector<uint64_t> dur_solo, dur_shared;
+      uint64_t worst = 0; uint32_t worst_b = 0, worst_lv = 0; int worst_share = 0;
+      for (auto& x : wg) {
+        int share = 0;
+        for (auto& y : wg) if (&y != &x && y.cu == x.cu && y.t0 < x.t1 && x.t0 < y.t1) ++share;
+        (share ? dur_shared : dur_solo).push_back(x.t1 - x.t0);
+        if (x.t1 - x.t0 > worst) { worst = x.t1 - x.t0; worst_b = x.b; worst_lv = x.lv; worst_share = share; }
+      }
+      auto med = [](std::vector<uint64_t> v) { if (v.empty()) return 0.0; std::sort(v.begin(), v.end()); return double(v[v.size() / 2]); };
+      auto mx = [](const std::vector<uint64_t>& v) { uint64_t m = 0; for (auto x : v) m = std::max(m, x); return double(m); };
+      uint64_t last_start = 0;
+      for (auto& x : wg) last_start = std::max(last_start, x.t0 - t_min);
+      fprintf(stderr, "diag-wg: %zu wgs span %llu; solo %zu med %.0f max %.0f; shared %zu med %.0f max %.0f; worst wg %u (%u levels, %d partners) %llu; last start %llu\n",
+              wg.size(), (unsigned long long)(t_max - t_min), dur_solo.size(), med(dur_solo), mx(dur_solo),
+              dur_shared.size(), med(dur_shared), mx(dur_shared), worst_b, worst_lv, worst_share,
+              (unsigned long long)worst, (unsigned long long)last_start);
+    }
   }
 #endif
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
@@ -1095,6 +1134,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   info.variant = static_cast<int32_t>(run_plan.variant);
   info.rows = n_rows;
   info.mask_bits = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.mask_bytes * 8 : 0;
+  info.batch_sources = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.ms_width : 0;
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
     e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");

@@ -4,7 +4,8 @@ oracle (``-m gpu``).
 Each sweep test asserts which kernel plan ran (orh_last_spf_info), so the
 variant the bench times is the variant that is checked:
 
-  C2 100x100 grid, all 10,000 sources   MS-BFS u32 masks + first_hop_lvl<16>
+  C2 100x100 grid, all 10,000 sources   MS-BFS u32 masks + first_hop_lvl<16>;
+                                        opt-in u64 masks and interval skip
   ladder 2 x 4,100 (BFS depth > 254)    MS-BFS levels >= 254 written directly
                                         (kLvlDirect) + first_hop_lvl<16>
   ladder 2 x 300, all sources           kLvlDirect + first_hop_lvl<4>
@@ -75,7 +76,27 @@ def test_c2_sweep_first_hops_exact(hip, oracle):
     check = special + rng.sample([i for i in range(n * n) if i not in special], 291)
     info = _sweep_tables(als_h[A], als_o[A], names, check)
     assert info["variant"] == MSBFS and info["mask_bits"] == 32, info
+    assert info["batch_sources"] == 32, info
     assert info["hop_nodes"] == 16, info  # first_hop_lvl_kernel<16>, as benched
+
+
+@pytest.mark.parametrize("env", [{"ORH_MS_WIDE": "1"}, {"ORH_MS_SKIP": "1"}])
+def test_c2_sweep_opt_in_variants(hip, oracle, monkeypatch, env):
+    """The opt-in MS-BFS variants on the same sweep, 64 sources compared in
+    full: u64 masks (250 batches of 40 sources) and the interval skip."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n = 100
+    adj_dbs, _ = bench_grid(n)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    names = [str(i) for i in range(n * n)]
+    rng = random.Random(32)
+    check = [0, n * n - 1] + rng.sample(range(1, n * n - 1), 62)
+    info = _sweep_tables(als_h[A], als_o[A], names, check)
+    wide = "ORH_MS_WIDE" in env
+    assert info["variant"] == MSBFS and info["mask_bits"] == (64 if wide else 32), info
+    assert info["batch_sources"] == (40 if wide else 32), info
 
 
 @pytest.mark.parametrize("length,metric,hop_nodes", [(4100, 3, 16), (300, 1, 4)])
