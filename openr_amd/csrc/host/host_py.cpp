@@ -18,6 +18,8 @@ using namespace openr_amd;
 
 namespace {
 
+py::bytes pyBytes(const AddrBytes& a) { return py::bytes(a.data(), a.size()); }
+
 std::string str(const py::handle& h) { return h.cast<std::string>(); }
 
 Adjacency adjFromWire(const py::tuple& t) {
@@ -88,7 +90,7 @@ py::object entryToWire(const PrefixEntry& e) {
                                  py::tuple(py::cast(me.metric))));
     mv = py::make_tuple(e.mv->version, ents);
   }
-  return py::make_tuple(py::bytes(e.addr), e.len, e.type, e.forwardingType, e.forwardingAlgorithm,
+  return py::make_tuple(pyBytes(e.addr), e.len, e.type, e.forwardingType, e.forwardingAlgorithm,
                         py::cast(e.minNexthop), py::cast(e.prependLabel),
                         py::make_tuple(e.pathPreference, e.sourcePreference, e.distance), mv,
                         e.data ? py::object(py::bytes(*e.data)) : py::none(),
@@ -122,7 +124,7 @@ py::tuple nhToWire(const NextHopThrift& nh) {
                              ? py::object(py::tuple(py::cast(*nh.mplsAction->pushLabels)))
                              : py::none());
   }
-  return py::make_tuple(py::bytes(nh.address.addr), py::cast(nh.address.ifName), nh.weight, act,
+  return py::make_tuple(pyBytes(nh.address.addr), py::cast(nh.address.ifName), nh.weight, act,
                         nh.metric, py::cast(nh.area), py::cast(nh.neighborNodeName));
 }
 
@@ -133,7 +135,7 @@ py::list nhsToWire(const NextHopSet& s) {
 }
 
 py::tuple unicastToWire(const RibUnicastEntry& e) {
-  return py::make_tuple(py::bytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
+  return py::make_tuple(pyBytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
                         e.doNotInstall, e.bestArea,
                         e.bestPrefixEntry ? entryToWire(*e.bestPrefixEntry) : py::none());
 }
@@ -200,7 +202,7 @@ DecisionRouteDb routeDbFromWire(const py::tuple& w) {
 py::tuple deltaToWire(const DecisionRouteUpdate& d) {
   py::list uu, ud, mu;
   for (const auto& [_, e] : d.unicastRoutesToUpdate) uu.append(unicastToWire(e));
-  for (const auto& p : d.unicastRoutesToDelete) ud.append(py::make_tuple(py::bytes(p.first), p.second));
+  for (const auto& p : d.unicastRoutesToDelete) ud.append(py::make_tuple(pyBytes(p.first), p.second));
   for (const auto& e : d.mplsRoutesToUpdate) mu.append(py::make_tuple(e.label, nhsToWire(e.nexthops)));
   return py::make_tuple(uu, ud, mu, py::cast(d.mplsRoutesToDelete));
 }
@@ -418,7 +420,7 @@ uint64_t fnv1a(const std::string& s) {
 
 std::string nexthopBytes(const NextHopThrift& nh) {
   DigestWriter w;
-  w.str(nh.address.addr);
+  w.str(nh.address.addr.str());
   w.optStr(nh.address.ifName);
   w.i32(nh.weight);
   w.u8(nh.mplsAction ? 1 : 0);
@@ -447,7 +449,7 @@ void writeNexthops(DigestWriter& w, const NextHopSet& nhs) {
 }
 
 void writeEntry(DigestWriter& w, const PrefixEntry& e) {
-  w.str(e.addr);
+  w.str(e.addr.str());
   w.i32(e.len);
   w.i32(e.type);
   w.i32(e.forwardingType);
@@ -493,7 +495,7 @@ py::tuple routeDbDigest(const DecisionRouteDb& db) {
   pool.parallelFor(uc.size(), [&](size_t, size_t b, size_t e) {
     for (size_t i = b; i < e; ++i) {
       DigestWriter w;
-      w.str(uc[i]->prefix.first);
+      w.str(uc[i]->prefix.first.str());
       w.i32(uc[i]->prefix.second);
       w.u8(uc[i]->doNotInstall ? 1 : 0);
       w.str(uc[i]->bestArea);
@@ -717,7 +719,7 @@ PYBIND11_MODULE(_openr_host, m) {
            [](PrefixState& s, const std::string& node, const std::string& area, py::tuple e) {
              py::list out;
              for (const auto& c : s.updatePrefix(node, area, entryFromWire(e)))
-               out.append(py::make_tuple(py::bytes(c.first), c.second));
+               out.append(py::make_tuple(pyBytes(c.first), c.second));
              return out;
            })
       .def("update_prefixes",
@@ -734,7 +736,7 @@ PYBIND11_MODULE(_openr_host, m) {
               int32_t len) {
              py::list out;
              for (const auto& c : s.deletePrefix(node, area, Cidr{std::string(addr), len}))
-               out.append(py::make_tuple(py::bytes(c.first), c.second));
+               out.append(py::make_tuple(pyBytes(c.first), c.second));
              return out;
            })
       .def("num_prefixes", [](const PrefixState& s) { return s.prefixes().size(); });
@@ -846,8 +848,8 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              auto ch = p.applyPolicy(m);
              py::list up, del, out;
-             for (const auto& c : ch.updatedRoutes) up.append(py::make_tuple(py::bytes(c.first), c.second));
-             for (const auto& c : ch.deletedRoutes) del.append(py::make_tuple(py::bytes(c.first), c.second));
+             for (const auto& c : ch.updatedRoutes) up.append(py::make_tuple(pyBytes(c.first), c.second));
+             for (const auto& c : ch.deletedRoutes) del.append(py::make_tuple(pyBytes(c.first), c.second));
              for (const auto& [_, e] : m) out.append(unicastToWire(e));
              return py::make_tuple(up, del, out);
            })

@@ -8,10 +8,12 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <optional>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <utility>
@@ -24,8 +26,58 @@ namespace openr_amd {
 using Metric = uint64_t;  // LinkStateMetric (LinkState.h:22)
 using NodeAndArea = std::pair<std::string, std::string>;
 
+// Raw address bytes (IPv4: 4, IPv6: 16) held inline. A 16-byte std::string
+// is one heap allocation per copy (libstdc++ keeps 15 bytes inline), and a
+// route carries three of them (prefix, best entry, each nexthop): the
+// allocator, not the selection, set the materialisation time. Compares like
+// std::string (unsigned bytes, then length) and hashes to the same value.
+class AddrBytes {
+ public:
+  static constexpr size_t kMax = 16;
+  AddrBytes() = default;
+  AddrBytes(const std::string& s) { assign(s.data(), s.size()); }  // NOLINT: thrift binary field
+  AddrBytes(const char* p, size_t n) { assign(p, n); }
+  AddrBytes(size_t n, char c) {
+    check(n);
+    len_ = static_cast<uint8_t>(n);
+    std::memset(b_, c, n);
+  }
+  void assign(const char* p, size_t n) {
+    check(n);
+    len_ = static_cast<uint8_t>(n);
+    if (n) std::memcpy(b_, p, n);
+  }
+  size_t size() const { return len_; }
+  bool empty() const { return len_ == 0; }
+  const char* data() const { return b_; }
+  char* data() { return b_; }
+  char& operator[](size_t i) { return b_[i]; }
+  const char& operator[](size_t i) const { return b_[i]; }
+  const char* begin() const { return b_; }
+  const char* end() const { return b_ + len_; }
+  std::string str() const { return std::string(b_, len_); }
+  std::string_view view() const { return std::string_view(b_, len_); }
+  bool operator==(const AddrBytes& o) const {
+    return len_ == o.len_ && std::memcmp(b_, o.b_, len_) == 0;
+  }
+  bool operator!=(const AddrBytes& o) const { return !(*this == o); }
+  bool operator<(const AddrBytes& o) const { return view() < o.view(); }
+  bool operator>(const AddrBytes& o) const { return o < *this; }
+  bool operator<=(const AddrBytes& o) const { return !(o < *this); }
+  bool operator>=(const AddrBytes& o) const { return !(*this < o); }
+
+ private:
+  static void check(size_t n) {
+    if (n > kMax) throw std::length_error("address of " + std::to_string(n) + " bytes (at most 16)");
+  }
+  char b_[kMax] = {};
+  uint8_t len_ = 0;
+};
+
+inline size_t strHash(const AddrBytes& s) { return std::hash<std::string_view>{}(s.view()); }
+
 struct BinaryAddress {
-  std::string addr;  // 4 or 16 raw bytes
+  AddrBytes addr;  // 4 or 16 raw bytes
   std::optional<std::string> ifName;
   bool operator==(const BinaryAddress& o) const { return addr == o.addr && ifName == o.ifName; }
   bool operator!=(const BinaryAddress& o) const { return !(*this == o); }
@@ -74,7 +126,7 @@ enum : int32_t { kAlgoSpEcmp = 0, kAlgoKsp2EdEcmp = 1 };
 enum : int32_t { kPush = 0, kSwap = 1, kPhp = 2, kPopAndLookup = 3 };
 
 struct PrefixEntry {
-  std::string addr;  // masked network bytes
+  AddrBytes addr;  // masked network bytes
   int32_t len{0};
   int32_t type{1};
   int32_t forwardingType{kFwdIp};
@@ -131,7 +183,7 @@ struct NextHopHash {
 };
 
 using NextHopSet = std::unordered_set<NextHopThrift, NextHopHash>;
-using Cidr = std::pair<std::string, int32_t>;  // (masked address bytes, length)
+using Cidr = std::pair<AddrBytes, int32_t>;  // (masked address bytes, length)
 
 struct CidrHash {
   size_t operator()(const Cidr& c) const {
