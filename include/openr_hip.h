@@ -141,6 +141,7 @@ int orh_set_spf_mode(orh_ctx* ctx, int mode);
 #define ORH_VARIANT_GLOBAL 7    /* HBM frontier kernel, two-phase */
 #define ORH_VARIANT_GLOBAL_NH 8 /* HBM frontier kernel with fused first hops */
 #define ORH_VARIANT_EXACT 9     /* exact Dijkstra in the reference's extraction order */
+#define ORH_VARIANT_BFS_NH 10   /* BFS with fused first hops, one workgroup per source */
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */

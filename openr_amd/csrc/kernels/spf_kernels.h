@@ -85,8 +85,14 @@ struct HopArgs {
 enum class SpfVariant {
   kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal,
   kGlobalNh,  // HBM frontier kernel that also derives the first hops (no phase 2)
-  kExact      // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
+  kExact,     // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
+  kBfsNh      // uniform metric, few sources: BFS with the first hops fused (no phase 2)
 };
+// fused BFS + first hops (spf_bfs_nh_kernel): workgroup size, nodes per
+// thread and LDS bytes for N nodes and `words` first-hop words per node;
+// false when the graph does not fit (N > 32768 or LDS)
+bool bfs_nh_shape(uint32_t n_nodes, uint32_t words, size_t lds_limit, uint32_t* block,
+                  uint32_t* j, size_t* lds);
 
 // exact Dijkstra (spf_exact_kernel): one wave per source row; heap, 64-bit
 // metrics and first-hop masks in LDS (or per-row global scratch when the

@@ -638,6 +638,170 @@ __global__ __launch_bounds__(256) void ms_finalize_kernel(SpfArgs a, uint32_t ti
 }
 
 // ---------------------------------------------------------------------------
+// fused BFS + first hops, one workgroup per source (kBfsNh)
+// ---------------------------------------------------------------------------
+// For a few sources (a route build's own SPF, small what-if batches) the
+// two-phase plans search the source AND each of its neighbours (the
+// closed-form first hops read the neighbours' rows), 5x the rows on a grid,
+// then launch the first-hop phase. Here the first hops ride along the
+// search, as in runSpf itself (LinkState.cpp:857-873): a level-L node pushes
+// to its neighbours, claims the unvisited ones for level L+1 (LDS CAS) and
+// ORs its first-hop mask into every neighbour at level L+1 - all of them
+// tight, the metric being uniform. The source's neighbours start with their
+// own bit. Overloaded nodes are reached but do not push (no transit).
+// Thread t owns nodes t, t + B, ...: their ELL columns (dead, down and
+// ignored records folded to a never-claimable dummy slot) sit in registers,
+// so a level is one batch of LDS reads (the owned unsettled nodes' levels),
+// then per frontier node one batch of neighbour-level reads and
+// fire-and-forget claims / ORs (no return-value round trips); no global
+// memory is touched until the rows are written out, coalesced.
+// LDS: level u32 [N + 1] | first hops u32 [N * words].
+template <int K, int J>
+__global__ __launch_bounds__(kMaxBlock) void spf_bfs_nh_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr int KH = (K + 1) / 2;
+  const uint32_t N = a.n_nodes, W = a.words, B = blockDim.x, tid = threadIdx.x;
+  const uint32_t row = blockIdx.x;
+  const uint32_t NZ = N;  // dummy slot: level 0, never claimed, never expanded
+  uint32_t* lvl = lds;
+  uint32_t* nh = lds + ((N + 4u) & ~3u);
+  __shared__ uint32_t s_prog[3];
+  const uint32_t src = a.srcs[row];
+  const uint32_t* ign = nullptr;
+  uint32_t n_ign = 0;
+  if (a.ignore_ptr) {
+    ign = a.ignore_links + a.ignore_ptr[row];
+    n_ign = a.ignore_ptr[row + 1] - a.ignore_ptr[row];
+  }
+  for (uint32_t i = tid; i < N; i += B) lvl[i] = kInf;
+  if (tid == 0) lvl[NZ] = 0u;
+  for (uint32_t i = tid; i < N * W; i += B) nh[i] = 0u;
+  if (tid < 3) s_prog[tid] = 0u;
+  auto live = [&](const uint2& r, size_t q) {
+    return !(r.x & (ORH_REC_SKIP | ORH_REC_CONT)) && !(n_ign && ignored(ign, n_ign, a.link[q]));
+  };
+  uint32_t col[J][KH];
+  uint32_t ovlm = 0u, ovfm = 0u, open = 0u;  // bit j: overloaded / overflow list / not yet expanded
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = j * B + tid;
+#pragma unroll
+    for (int h = 0; h < KH; ++h) col[j][h] = NZ | (NZ << 16);
+    if (v < N) {
+      open |= 1u << j;
+      const size_t q0 = static_cast<size_t>(v) * K;
+      uint32_t c[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const uint2 r = a.recs[q0 + k];
+        c[k] = live(r, q0 + k) ? (r.x & ORH_REC_COL_MASK) : NZ;
+        if (k == 0 && (r.x & ORH_REC_ROW_OVL)) ovlm |= 1u << j;
+        if (k == K - 1 && (r.x & ORH_REC_CONT)) ovfm |= 1u << j;
+      }
+#pragma unroll
+      for (int h = 0; h < KH; ++h) col[j][h] = c[2 * h] | ((2 * h + 1 < K ? c[2 * h + 1] : NZ) << 16);
+    }
+  }
+  __syncthreads();
+  // level 1: the source's live neighbours, each with its own first-hop bit
+  // (its rank among the source's distinct neighbours, LinkState.cpp:869-872)
+  if (tid == 0) lvl[src] = 0u;
+  {
+    const size_t q0 = static_cast<size_t>(src) * K;
+    const uint2 last = a.recs[q0 + K - 1];
+    const uint32_t n_ovf = (last.x & ORH_REC_CONT) ? last.y : 0u;
+    const size_t ovf0 = last.x & ORH_REC_COL_MASK;
+    for (uint32_t k = tid; k < K + n_ovf; k += B) {
+      const size_t q = k < K ? q0 + k : ovf0 + (k - K);
+      const uint2 r = a.recs[q];
+      if (!live(r, q)) continue;
+      const uint32_t u = r.x & ORH_REC_COL_MASK;
+      if (u == src) continue;
+      atomicCAS(&lvl[u], kInf, 1u);
+      const uint32_t b = a.rank_out[q];
+      atomicOr(&nh[static_cast<size_t>(u) * W + (b >> 5)], 1u << (b & 31u));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < J; ++j)  // the source itself is settled: it pushed above
+    if (j * B + tid == src) open &= ~(1u << j);
+  for (uint32_t level = 1;; ++level) {
+    int prog = 0;
+    uint32_t me = tid;
+    asm volatile("" : "+v"(me));
+    // every owned unsettled node's level in one batch of independent reads
+    uint32_t lv[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) lv[j] = ((open >> j) & 1u) ? lvl[j * B + me] : 0u;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      if (lv[j] != level) continue;  // settled, unreached, or claimed for the next level
+      open &= ~(1u << j);
+      if ((ovlm >> j) & 1u) continue;  // reached, no transit
+      const uint32_t v = j * B + me;
+      // the neighbours' levels, then fire-and-forget claims and ORs: only
+      // level + 1 claims happen during this level, so a neighbour read as
+      // unreached or level + 1 ends the level at level + 1
+      uint32_t u[2 * KH], lu[2 * KH];
+#pragma unroll
+      for (int h = 0; h < KH; ++h) {
+        u[2 * h] = col[j][h] & 0xFFFFu;
+        u[2 * h + 1] = col[j][h] >> 16;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) lu[k] = lvl[u[k]];
+      uint32_t m0 = nh[static_cast<size_t>(v) * W];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (lu[k] != kInf && lu[k] != level + 1u) continue;
+        if (lu[k] == kInf) {
+          prog = 1;
+          atomicMin(&lvl[u[k]], level + 1u);
+        }
+        if (m0) atomicOr(&nh[static_cast<size_t>(u[k]) * W], m0);
+        for (uint32_t w = 1; w < W; ++w) {
+          const uint32_t m = nh[static_cast<size_t>(v) * W + w];
+          if (m) atomicOr(&nh[static_cast<size_t>(u[k]) * W + w], m);
+        }
+      }
+      if ((ovfm >> j) & 1u) {
+        const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
+        const size_t ovf0 = last.x & ORH_REC_COL_MASK;
+        for (uint32_t q = 0; q < last.y; ++q) {
+          const uint2 r = a.recs[ovf0 + q];
+          if (!live(r, ovf0 + q)) continue;
+          const uint32_t x = r.x & ORH_REC_COL_MASK;
+          const uint32_t lx = lvl[x];
+          if (lx != kInf && lx != level + 1u) continue;
+          if (lx == kInf) {
+            prog = 1;
+            atomicMin(&lvl[x], level + 1u);
+          }
+          for (uint32_t w = 0; w < W; ++w) {
+            const uint32_t m = nh[static_cast<size_t>(v) * W + w];
+            if (m) atomicOr(&nh[static_cast<size_t>(x) * W + w], m);
+          }
+        }
+      }
+    }
+    // levels are < N, so the loop ends; a level that claims nothing is the last
+    if (prog) s_prog[level % 3u] = 1u;
+    __syncthreads();
+    if (!s_prog[level % 3u]) break;
+    if (tid == 0) s_prog[(level + 2u) % 3u] = 0u;
+  }
+  uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
+  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * W;
+  const uint32_t w0 = a.w0;
+  for (uint32_t i = tid; i < N; i += B) {
+    const uint32_t l = lvl[i];
+    __builtin_nontemporal_store(l == kInf ? kInf : l * w0, &od[i]);
+  }
+  for (uint32_t i = tid; i < N * W; i += B) __builtin_nontemporal_store(nh[i], &on[i]);
+}
+
+// ---------------------------------------------------------------------------
 // phase 1b: level-synchronous Dijkstra on a u16 / u32 distance per node
 // ---------------------------------------------------------------------------
 template <class T>
@@ -1694,12 +1858,48 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
   }
 }
 
+bool bfs_nh_shape(uint32_t n_nodes, uint32_t words, size_t lds_limit, uint32_t* block,
+                  uint32_t* j, size_t* lds) {
+  if (n_nodes == 0 || n_nodes > 32768u) return false;  // 16-bit packed columns, J <= 32
+  const uint32_t b = std::min<uint32_t>(kMaxBlock, std::max<uint32_t>(64, ((n_nodes + 3) / 4 + 63) / 64 * 64));
+  const uint32_t jj = ((n_nodes + b - 1) / b + 3) & ~3u;
+  const size_t bytes = 4 * static_cast<size_t>((n_nodes + 4u) & ~3u) + 4 * static_cast<size_t>(n_nodes) * words;
+  if (jj > 32 || bytes > lds_limit) return false;
+  *block = b;
+  *j = jj;
+  *lds = bytes;
+  return true;
+}
+
+template <int K>
+static hipError_t launch_bfs_nh(const SpfArgs& a, uint32_t n_rows, uint32_t block, uint32_t j,
+                                size_t lds, hipStream_t s) {
+  switch (j) {
+    case 4: return launch(spf_bfs_nh_kernel<K, 4>, a, n_rows, block, lds, s);
+    case 8: return launch(spf_bfs_nh_kernel<K, 8>, a, n_rows, block, lds, s);
+    case 12: return launch(spf_bfs_nh_kernel<K, 12>, a, n_rows, block, lds, s);
+    case 16: return launch(spf_bfs_nh_kernel<K, 16>, a, n_rows, block, lds, s);
+    case 20: return launch(spf_bfs_nh_kernel<K, 20>, a, n_rows, block, lds, s);
+    case 24: return launch(spf_bfs_nh_kernel<K, 24>, a, n_rows, block, lds, s);
+    case 28: return launch(spf_bfs_nh_kernel<K, 28>, a, n_rows, block, lds, s);
+    case 32: return launch(spf_bfs_nh_kernel<K, 32>, a, n_rows, block, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
   a.lds_pend_off = static_cast<uint32_t>(plan.pend_off);
   a.n_rows = n_rows;
   a.ms_pitch = plan.ms_pitch;
   a.ms_zero = a.n_nodes;
+  if (plan.variant == SpfVariant::kBfsNh) {
+    uint32_t block = 0, j = 0;
+    size_t lds = 0;
+    if (!bfs_nh_shape(a.n_nodes, a.words, SIZE_MAX, &block, &j, &lds)) return hipErrorInvalidValue;
+    return plan.ell_k == 8 ? launch_bfs_nh<8>(a, n_rows, block, j, lds, s)
+                           : launch_bfs_nh<4>(a, n_rows, block, j, lds, s);
+  }
   return plan.ell_k == 8 ? launch_k<8>(plan, a, n_rows, s) : launch_k<4>(plan, a, n_rows, s);
 }
 

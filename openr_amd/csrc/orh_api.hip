@@ -996,6 +996,24 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // need extra neighbour rows (or the HBM kernel is forced)
   orh::SpfPlan run_plan = plan;
   orh::ms_set_width(run_plan, N, n_rows, ctx->n_cu, ctx->lds_limit);
+  // uniform metric, at most ORH_BFS_NH_MAX sources (default: one per CU):
+  // one fused BFS + first-hop workgroup per source instead of searching
+  // every neighbour row too (ORH_BFS_NH_MAX=0 turns it off)
+  {
+    const bool bfs_plan = plan.variant == orh::SpfVariant::kMsBfs || plan.variant == orh::SpfVariant::kBfs8 ||
+                          plan.variant == orh::SpfVariant::kBfs16 || plan.variant == orh::SpfVariant::kBfs32;
+    uint32_t fused_max = ctx->n_cu;
+    if (const char* e = getenv("ORH_BFS_NH_MAX")) fused_max = static_cast<uint32_t>(atoi(e));
+    uint32_t blk = 0, jj = 0;
+    size_t lds = 0;
+    if (bfs_plan && ctx->spf_mode == orh::SpfMode::kAuto && n_src <= fused_max &&
+        orh::bfs_nh_shape(N, words, ctx->lds_limit, &blk, &jj, &lds)) {
+      run_plan.variant = orh::SpfVariant::kBfsNh;
+      run_plan.block = blk;
+      run_plan.lds_bytes = lds;
+      n_rows = n_src;
+    }
+  }
   if (plan.variant == orh::SpfVariant::kGlobal && max_nbr <= 32 &&
       ctx->spf_mode != orh::SpfMode::kGlobalTwoPhase &&
       (ctx->spf_mode == orh::SpfMode::kGlobal || n_rows > n_src)) {
@@ -1004,7 +1022,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     int rc = ensure_labels(ctx, static_cast<size_t>(n_src) * N);
     if (rc) return rc;
   }
-  const bool fused = run_plan.variant == orh::SpfVariant::kGlobalNh;
+  const bool fused = run_plan.variant == orh::SpfVariant::kGlobalNh ||
+                     run_plan.variant == orh::SpfVariant::kBfsNh;
   const size_t n_extra = n_rows - n_src;
   if (n_extra) {
     int rc = ensure_scratch(ctx, n_extra * N);
@@ -1016,7 +1035,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.n_out = n_src;
   a.recs = g->d_recs;
   a.link = g->d_link;
-  if (plan.variant == orh::SpfVariant::kMsBfs) {
+  if (run_plan.variant == orh::SpfVariant::kMsBfs) {
     int rc = sync_ms_layout(g);
     if (rc) return rc;
     a.ms_bw = g->ms_bw;

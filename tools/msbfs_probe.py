@@ -46,6 +46,8 @@ def main():
         "center32": center,
         # the corner batch repeated: 256 identical workgroups, one per CU
         "corner256x32": corner * 256,
+        "one": [node(1, 0)],
+        "one_center": [node(c, c)],
     }
     for name in args.cases.split(","):
         srcs = cases[name]
