@@ -840,7 +840,7 @@ PYBIND11_MODULE(_openr_host, m) {
            })
       .def("apply_policy",  // (updated prefixes, deleted prefixes, transformed unicast routes)
            [](RibPolicy& p, py::list routes) {
-             std::unordered_map<Cidr, RibUnicastEntry, CidrHash> m;
+             UnicastRouteMap m;
              for (auto r : routes) {
                RibUnicastEntry e = unicastFromWire(r.cast<py::tuple>());
                Cidr k = e.prefix;

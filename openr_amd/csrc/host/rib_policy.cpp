@@ -1,6 +1,8 @@
 // Drop-in RibPolicy (see rib_policy.h).
 #include "rib_policy.h"
 
+#include "parallel.h"
+
 #include <stdexcept>
 
 namespace openr_amd {
@@ -78,18 +80,38 @@ bool RibPolicy::match(const RibUnicastEntry& route) const {
   return false;
 }
 
-bool RibPolicy::applyAction(RibUnicastEntry& route) {
+bool RibPolicy::applyAction(RibUnicastEntry& route) { return applyAction(route, &invalidated_); }
+
+bool RibPolicy::applyAction(RibUnicastEntry& route, uint64_t* invalidated) const {
   for (const auto& s : statements_)
-    if (s.applyAction(route, &invalidated_)) return true;
+    if (s.applyAction(route, invalidated)) return true;
   return false;
 }
 
-RibPolicy::PolicyChange RibPolicy::applyPolicy(
-    std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes) {
+RibPolicy::PolicyChange RibPolicy::applyPolicy(UnicastRouteMap& routes) {
   PolicyChange change;  // RibPolicy.cpp:229-247
   if (!isActive()) return change;
-  for (auto& [prefix, route] : routes)
-    if (applyAction(route)) change.updatedRoutes.push_back(route.prefix);
+  // shard by shard (on the worker pool for large databases: C5 applies the
+  // policy to 1M routes); updated prefixes in the map's iteration order
+  constexpr size_t kS = UnicastRouteMap::kShards;
+  std::vector<std::vector<Cidr>> updated(kS);
+  std::vector<uint64_t> invalidated(kS, 0);
+  auto shard = [&](size_t s) {
+    for (auto& [prefix, route] : routes.shard(s))
+      if (applyAction(route, &invalidated[s])) updated[s].push_back(route.prefix);
+  };
+  auto& pool = WorkerPool::instance();
+  if (routes.size() >= 4096 && pool.size() > 1) {
+    pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
+      for (size_t s = b; s < e; ++s) shard(s);
+    });
+  } else {
+    for (size_t s = 0; s < kS; ++s) shard(s);
+  }
+  for (size_t s = 0; s < kS; ++s) {
+    change.updatedRoutes.insert(change.updatedRoutes.end(), updated[s].begin(), updated[s].end());
+    invalidated_ += invalidated[s];
+  }
   return change;
 }
 

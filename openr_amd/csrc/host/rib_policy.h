@@ -60,7 +60,10 @@ class RibPolicy {
   std::chrono::milliseconds getTtlDuration() const;
   bool match(const RibUnicastEntry& route) const;
   bool applyAction(RibUnicastEntry& route);
-  PolicyChange applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes);
+  // the same, counting invalidated routes into *invalidated (thread-safe for
+  // distinct routes and counters)
+  bool applyAction(RibUnicastEntry& route, uint64_t* invalidated) const;
+  PolicyChange applyPolicy(UnicastRouteMap& routes);
   // decision.rib_policy.invalidated_routes (RibPolicy.cpp:150-153)
   uint64_t invalidatedRoutes() const { return invalidated_; }
 

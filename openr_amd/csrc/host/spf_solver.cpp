@@ -4,6 +4,7 @@
 #include "parallel.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,6 +34,26 @@ struct RouteProf {
     t = now;
   }
 };
+
+// parts[w] -> into, shard by shard on the pool; a key in two parts is a
+// duplicate route (RouteUpdate.h:39 CHECK)
+template <class Map>
+void mergeParts(Map& into, std::vector<Map>& parts, WorkerPool& pool) {
+  std::atomic<bool> dup{false};
+  pool.parallelFor(Map::kShards, [&](size_t, size_t b, size_t e) {
+    for (size_t s = b; s < e; ++s) {
+      auto& dst = into.shard(s);
+      size_t n = dst.size();
+      for (auto& p : parts) n += p.shard(s).size();
+      dst.reserve(n);
+      for (auto& p : parts) {
+        dst.merge(p.shard(s));
+        if (!p.shard(s).empty()) dup = true;
+      }
+    }
+  });
+  if (dup) throw std::logic_error("duplicate unicast route");
+}
 
 MplsAction mpls(int32_t code, std::optional<int32_t> swap = std::nullopt,
                 std::optional<std::vector<int32_t>> push = std::nullopt) {
@@ -844,7 +865,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   for (const auto& [_, ls] : als) ls.getSpfResult(me);
   prof.mark("spf(me)");
   DecisionRouteDb db;
-  db.unicastRoutes.reserve(ps.prefixes().size());
+  if (ps.prefixes().size() < kParallelMin) db.unicastRoutes.reserve(ps.prefixes().size());
   auto& pool = WorkerPool::instance();
   // per-prefix selection on the device; the host materialises the routes it
   // selected and runs the full reference logic for the prefixes it returns
@@ -925,57 +946,51 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       };
       std::vector<decltype(db.unicastRoutes)> parts(pool.size());
       pool.parallelFor(n + dbs.size(), [&](size_t w, size_t b, size_t e) {
-        parts[w].reserve(parts[w].size() + (std::min<size_t>(e, n) - std::min<size_t>(b, n)));
         for (size_t i = b; i < e; ++i) {
           if (i < n) one(static_cast<uint32_t>(i), parts[w]);
           else label(i - n);
         }
       });
       prof.mark("unicast + labels (pool)");
-      pool.parallelFor(2, [&](size_t, size_t b, size_t e) {
-        for (size_t c = b; c < e; ++c) {
-          if (c == 0) {
-            for (auto& part : parts) {
-              db.unicastRoutes.merge(part);
-              if (!part.empty()) throw std::logic_error("duplicate unicast route");
-            }
-            for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
-              if (db.unicastRoutes.count(prefix)) continue;
-              RibUnicastEntry se;
-              se.prefix = prefix;
-              se.nexthops.insert(nhs.begin(), nhs.end());
-              db.unicastRoutes.emplace(prefix, std::move(se));
-            }
-          } else {
-            // duplicate labels: the smaller node name wins (:675-688)
-            std::unordered_map<int32_t, std::pair<const std::string*, size_t>> win;
-            win.reserve(dbs.size());
-            for (size_t i = 0; i < dbs.size(); ++i) {
-              const int32_t lbl = dbs[i]->nodeLabel;
-              if (lbl == 0 || !isMplsLabelValid(lbl)) continue;
-              auto it = win.find(lbl);
-              if (it != win.end() && *it->second.first < dbs[i]->thisNodeName) continue;
-              if (!cand[i]) continue;
-              win[lbl] = {&dbs[i]->thisNodeName, i};
-            }
-            db.mplsRoutes.reserve(win.size() + 64);
-            for (auto& [lbl, w] : win) db.mplsRoutes.emplace(lbl, std::move(*cand[w.second]));
+      mergeParts(db.unicastRoutes, parts, pool);
+      for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
+        if (db.unicastRoutes.count(prefix)) continue;
+        RibUnicastEntry se;
+        se.prefix = prefix;
+        se.nexthops.insert(nhs.begin(), nhs.end());
+        db.unicastRoutes.emplace(prefix, std::move(se));
+      }
+      prof.mark("unicast merge");
+      // duplicate labels: the smaller node name wins among the nodes with a
+      // route (:675-688); labels are resolved shard by shard on the pool
+      std::vector<std::vector<uint32_t>> byShard(MplsRouteMap::kShards);
+      for (size_t i = 0; i < dbs.size(); ++i) {
+        const int32_t lbl = dbs[i]->nodeLabel;
+        if (lbl == 0 || !isMplsLabelValid(lbl) || !cand[i]) continue;
+        byShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
+      }
+      pool.parallelFor(MplsRouteMap::kShards, [&](size_t, size_t b, size_t e) {
+        for (size_t sh = b; sh < e; ++sh) {
+          std::unordered_map<int32_t, uint32_t> win;
+          win.reserve(byShard[sh].size());
+          for (uint32_t i : byShard[sh]) {
+            auto [it, fresh] = win.emplace(dbs[i]->nodeLabel, i);
+            if (!fresh && dbs[i]->thisNodeName < dbs[it->second]->thisNodeName) it->second = i;
           }
+          auto& dst = db.mplsRoutes.shard(sh);
+          dst.reserve(dst.size() + win.size() + 1);
+          for (auto& [lbl, i] : win) dst.emplace(lbl, std::move(*cand[i]));
         }
       });
-      prof.mark("unicast merge || label map");
+      prof.mark("label map");
       labelsDone = true;
     } else if (!hasKsp && n >= kParallelMin && pool.size() > 1) {
       std::vector<decltype(db.unicastRoutes)> parts(pool.size());
       pool.parallelFor(n, [&](size_t w, size_t b, size_t e) {
-        parts[w].reserve(parts[w].size() + (e - b));
         for (size_t pid = b; pid < e; ++pid) one(static_cast<uint32_t>(pid), parts[w]);
       });
       prof.mark("unicast (pool)");
-      for (auto& part : parts) {
-        db.unicastRoutes.merge(part);
-        if (!part.empty()) throw std::logic_error("duplicate unicast route");
-      }
+      mergeParts(db.unicastRoutes, parts, pool);
     } else {
       for (uint32_t pid = 0; pid < n; ++pid) one(pid, db.unicastRoutes);
     }
@@ -992,7 +1007,6 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     // (no entry is copied or moved)
     std::vector<decltype(db.unicastRoutes)> parts(pool.size());
     pool.parallelFor(keys.size(), [&](size_t w, size_t b, size_t e) {
-      parts[w].reserve(parts[w].size() + (e - b));
       for (size_t i = b; i < e; ++i)
         if (auto r = createRouteForPrefix(me, als, ps, *keys[i])) {
           Cidr k = r->prefix;
@@ -1000,10 +1014,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
         }
     });
     prof.mark("unicast (pool)");
-    for (auto& part : parts) {
-      db.unicastRoutes.merge(part);
-      if (!part.empty()) throw std::logic_error("duplicate unicast route");
-    }
+    mergeParts(db.unicastRoutes, parts, pool);
   } else {
     for (const Cidr* prefix : keys) {
       if (auto r = createRouteForPrefix(me, als, ps, *prefix)) {
@@ -1113,7 +1124,6 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       win[label] = {&adjDb.thisNodeName, i};
     }
     if (als.size() == 1) {  // one area: the winners are the routes
-      db.mplsRoutes.reserve(win.size() + 64);
       for (auto& [label, w] : win) db.mplsRoutes.emplace(label, std::move(*cand[w.second]));
       continue;
     }
