@@ -220,6 +220,22 @@ int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words
 #define ORH_GRAPH_WIDE_METRIC 2u /* link-metric path sums can reach 2^32 - 1 */
 int orh_graph_flags(const orh_graph* g, uint32_t* flags);
 
+/* ---- KSP2 (LinkState::getKthPaths, LinkState.cpp:762-791) --------------
+ * For each dsts[i]: the k = 1 paths, traced (traceOnePath, :398-419) over
+ * src's SPF with link metrics, then the k = 2 paths over a fresh SPF that
+ * ignores every k = 1 link - all fresh SPFs of the call in batched launches.
+ * pathLinks follow runSpf's insertion order: predecessors in extraction
+ * order (metric, then name rank; the exact kernel's order with zero
+ * metrics), parallel links in CSR row order (= the caller's LinkSet
+ * iteration order, which orh_csr rows must follow for KSP2 parity).
+ * Output words, per dst and k = 1, 2: n_paths, then per path its length
+ * and its link ids (orh_csr link ids, src -> dst order). *n_words receives
+ * the total; when it exceeds cap, nothing is written and ORH_E_INVALID is
+ * returned (query with cap = 0 first). Replaces the reference's memoized
+ * getKthPaths(src, dst, 1 / 2) pair for a batch of destinations. */
+int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, uint32_t* out,
+             size_t cap, size_t* n_words);
+
 /* ---- device prefix mirror (PrefixState) ------------------------------- */
 /* Replaces the per-prefix PrefixEntries map PrefixState::prefixes() hands to
  * the route build (openr/decision/PrefixState.h:22-70, updatePrefix /

@@ -579,6 +579,43 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              return out;
            })
+      .def("ksp2_abi",  // orh_ksp2 straight through the C ABI: per dst (k = 1 paths, k = 2 paths)
+           [](const LinkState& s, const std::string& a, const std::vector<std::string>& dsts) {
+             auto src = s.nodeId(a);
+             if (!src) throw std::invalid_argument("ksp2_abi: unknown source " + a);
+             std::vector<uint32_t> ids;
+             for (const auto& d : dsts) {
+               auto id = s.nodeId(d);
+               if (!id) throw std::invalid_argument("ksp2_abi: unknown destination " + d);
+               ids.push_back(*id);
+             }
+             orh_graph* g = s.deviceGraph();
+             size_t need = 0;
+             if (orh_ksp2(g, *src, ids.data(), static_cast<uint32_t>(ids.size()), nullptr, 0, &need) != ORH_OK)
+               throw std::runtime_error(std::string("orh_ksp2: ") + orh_last_error(s.context()));
+             std::vector<uint32_t> buf(need);
+             if (orh_ksp2(g, *src, ids.data(), static_cast<uint32_t>(ids.size()), buf.data(), buf.size(),
+                          &need) != ORH_OK)
+               throw std::runtime_error(std::string("orh_ksp2: ") + orh_last_error(s.context()));
+             py::list out;
+             size_t w = 0;
+             for (size_t i = 0; i < ids.size(); ++i) {
+               py::list ks;
+               for (int k = 0; k < 2; ++k) {
+                 py::list paths;
+                 const uint32_t np = buf[w++];
+                 for (uint32_t p = 0; p < np; ++p) {
+                   py::list path;
+                   const uint32_t len = buf[w++];
+                   for (uint32_t l = 0; l < len; ++l) path.append(linkDesc(s.link(buf[w++])));
+                   paths.append(path);
+                 }
+                 ks.append(paths);
+               }
+               out.append(ks);
+             }
+             return out;
+           })
       .def("get_metric_from_a_to_b", &LinkState::getMetricFromAToB, py::arg("a"), py::arg("b"),
            py::arg("use_link_metric") = true)
       .def("get_hops_from_a_to_b",

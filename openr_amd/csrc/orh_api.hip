@@ -1247,6 +1247,229 @@ int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words
   return rc;
 }
 
+}  // extern "C"
+
+namespace {
+
+// one source's SPF row as the KSP2 traces read it: u64 distances (~0 =
+// unreachable) and, from the exact kernel, the extraction rank (else empty:
+// extraction order is (distance, name rank))
+struct KspRow {
+  std::vector<uint64_t> dist;
+  std::vector<uint32_t> rank;
+};
+
+// rows for `n` searches from src (ignore sets ign_ptr / ign, or none), in
+// chunks that bound the device and host buffers
+int ksp_rows(orh_graph* g, uint32_t src, uint32_t n, const uint32_t* ign_ptr, const uint32_t* ign,
+             std::vector<KspRow>& rows) {
+  orh_ctx* ctx = g->ctx;
+  const uint32_t N = g->n_nodes;
+  uint32_t words = 1;
+  int rc = orh_spf_words(g, &src, 1, &words);
+  if (rc) return rc;
+  const bool exact = g->has_zero || wide_metrics(g);
+  const uint32_t chunk = static_cast<uint32_t>(std::max<size_t>(1, (size_t{256} << 20) / (size_t{N} * (12 + 4 * words))));
+  rows.resize(n);
+  std::vector<uint32_t> srcs, ptr;
+  std::vector<uint32_t> d32;
+  for (uint32_t r0 = 0; r0 < n; r0 += chunk) {
+    const uint32_t m = std::min(chunk, n - r0);
+    srcs.assign(m, src);
+    orh_spf_request req{};
+    req.h_srcs = srcs.data();
+    req.n_src = m;
+    req.use_link_metric = 1;
+    if (ign_ptr) {
+      ptr.assign(m + 1, 0);
+      for (uint32_t i = 0; i <= m; ++i) ptr[i] = ign_ptr[r0 + i] - ign_ptr[r0];
+      req.h_ignore_ptr = ptr.data();
+      req.h_ignore_links = ign + ign_ptr[r0];
+      if (ptr[m] == 0) req.h_ignore_links = ptr.data();  // non-null, nothing read
+    }
+    const size_t nd = static_cast<size_t>(m) * N;
+    const size_t bytes = nd * 8 + nd * 4 + nd * 4 * words;
+    rc = ensure_bytes(ctx, &ctx->d_batch_x, &ctx->d_batch_x_cap, bytes);
+    if (rc) return rc;
+    uint64_t* dd64 = reinterpret_cast<uint64_t*>(ctx->d_batch_x);
+    uint32_t* drank = reinterpret_cast<uint32_t*>(dd64 + nd);
+    uint32_t* dnh = drank + nd;
+    if (exact) {
+      rc = run_exact(g, &req, words, nullptr, dd64, dnh, drank);
+    } else {
+      rc = orh_spf_run(g, &req, words, reinterpret_cast<uint32_t*>(dd64), dnh);
+    }
+    if (rc) return rc;
+    if (exact) {
+      std::vector<uint64_t> h(nd);
+      std::vector<uint32_t> hr(nd);
+      ORH_HIP(ctx, hipMemcpyAsync(h.data(), dd64, nd * 8, hipMemcpyDeviceToHost, ctx->stream));
+      ORH_HIP(ctx, hipMemcpyAsync(hr.data(), drank, nd * 4, hipMemcpyDeviceToHost, ctx->stream));
+      ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      for (uint32_t i = 0; i < m; ++i) {
+        rows[r0 + i].dist.assign(h.begin() + size_t{i} * N, h.begin() + size_t{i + 1} * N);
+        rows[r0 + i].rank.assign(hr.begin() + size_t{i} * N, hr.begin() + size_t{i + 1} * N);
+      }
+    } else {
+      d32.resize(nd);
+      ORH_HIP(ctx, hipMemcpyAsync(d32.data(), dd64, nd * 4, hipMemcpyDeviceToHost, ctx->stream));
+      ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      for (uint32_t i = 0; i < m; ++i) {
+        auto& d = rows[r0 + i].dist;
+        d.resize(N);
+        for (uint32_t v = 0; v < N; ++v) {
+          const uint32_t x = d32[size_t{i} * N + v];
+          d[v] = x == ORH_UNREACHABLE ? ~0ull : x;
+        }
+        rows[r0 + i].rank.clear();
+      }
+    }
+  }
+  return ORH_OK;
+}
+
+// NodeSpfResult::pathLinks of v (LinkState.cpp:857-873 insertion order):
+// (link id, prev) over live, non-ignored CSR entries v <- u with
+// dist[u] + metric(u -> v) == dist[v], u extracted before v and transit
+// (u == src or not overloaded); by u's extraction order, then the link's
+// position in u's row
+void ksp_path_links(const orh_graph* g, uint32_t src, const KspRow& row, uint32_t v,
+                    const std::vector<uint32_t>& ign, std::vector<std::pair<uint32_t, uint32_t>>& out) {
+  out.clear();
+  const uint64_t dv = row.dist[v];
+  if (dv == ~0ull || v == src) return;
+  struct Cand {
+    uint64_t k1;
+    uint32_t k2, pos, link, prev;
+  };
+  std::vector<Cand> c;
+  for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) {
+    if (g->meta[e] & ORH_META_DOWN) continue;
+    const uint32_t link = g->meta[e] & ORH_META_LINK_MASK;
+    if (!ign.empty() && std::binary_search(ign.begin(), ign.end(), link)) continue;
+    const uint32_t u = g->col[e];
+    const uint64_t du = row.dist[u];
+    if (du == ~0ull) continue;
+    if (u != src && g->overloaded[u]) continue;
+    if (du + g->w_in[e] != dv) continue;
+    if (!row.rank.empty() && row.rank[u] > row.rank[v]) continue;
+    uint32_t pos = 0;
+    for (uint32_t f = g->row_ptr[u]; f < g->row_ptr[u + 1]; ++f, ++pos)
+      if ((g->meta[f] & ORH_META_LINK_MASK) == link && g->col[f] == v) break;
+    if (row.rank.empty()) c.push_back({du, g->name_rank[u], pos, link, u});
+    else c.push_back({row.rank[u], 0u, pos, link, u});
+  }
+  std::sort(c.begin(), c.end(), [](const Cand& a, const Cand& b) {
+    if (a.k1 != b.k1) return a.k1 < b.k1;
+    if (a.k2 != b.k2) return a.k2 < b.k2;
+    return a.pos < b.pos;
+  });
+  for (const auto& x : c) out.emplace_back(x.link, x.prev);
+}
+
+// traceOnePath (LinkState.cpp:398-419): greedy DFS dst -> src; a link is
+// consumed on first touch even when its branch fails. false = no path.
+bool ksp_trace(const orh_graph* g, uint32_t src, uint32_t dst, const KspRow& row,
+               const std::vector<uint32_t>& ign, std::vector<uint8_t>& visited,
+               std::vector<uint32_t>& path) {
+  if (src == dst) return true;
+  std::vector<std::pair<uint32_t, uint32_t>> links;
+  ksp_path_links(g, src, row, dst, ign, links);
+  for (const auto& [link, prev] : links) {
+    if (visited[link]) continue;
+    visited[link] = 1;
+    if (ksp_trace(g, src, prev, row, ign, visited, path)) {
+      path.push_back(link);
+      return true;
+    }
+  }
+  return false;
+}
+
+// successive traces sharing one visited-link set (LinkState.cpp:778-787)
+std::vector<std::vector<uint32_t>> ksp_paths(const orh_graph* g, uint32_t src, uint32_t dst,
+                                             const KspRow& row, const std::vector<uint32_t>& ign) {
+  std::vector<std::vector<uint32_t>> paths;
+  if (src != dst && row.dist[dst] == ~0ull) return paths;
+  std::vector<uint8_t> visited(std::max<uint32_t>(g->n_links, 1), 0);
+  for (;;) {
+    std::vector<uint32_t> p;
+    if (!ksp_trace(g, src, dst, row, ign, visited, p) || p.empty()) break;
+    paths.push_back(std::move(p));
+  }
+  return paths;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, uint32_t* out,
+             size_t cap, size_t* n_words) {
+  if (!g || !n_words || (n_dst && !dsts) || (cap && !out)) return ORH_E_INVALID;
+  orh_ctx* ctx = g->ctx;
+  if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_ksp2: no graph loaded");
+  if (src >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_ksp2: source out of range");
+  for (uint32_t i = 0; i < n_dst; ++i)
+    if (dsts[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_ksp2: destination out of range");
+  for (uint32_t e = 0; e < g->n_edges; ++e)
+    if ((g->meta[e] & ORH_META_LINK_MASK) >= std::max<uint32_t>(g->n_links, 1))
+      return fail(ctx, ORH_E_INVALID, "orh_ksp2: link id >= n_links");
+  // k = 1: src's own SPF
+  std::vector<KspRow> base;
+  int rc = ksp_rows(g, src, 1, nullptr, nullptr, base);
+  if (rc) return rc;
+  const std::vector<uint32_t> none;
+  std::vector<std::vector<std::vector<uint32_t>>> k1(n_dst), k2(n_dst);
+  std::vector<uint32_t> ptr(1, 0), ign;
+  std::vector<std::vector<uint32_t>> sets(n_dst);
+  for (uint32_t i = 0; i < n_dst; ++i) {
+    k1[i] = ksp_paths(g, src, dsts[i], base[0], none);
+    for (const auto& p : k1[i]) sets[i].insert(sets[i].end(), p.begin(), p.end());
+    std::sort(sets[i].begin(), sets[i].end());
+    sets[i].erase(std::unique(sets[i].begin(), sets[i].end()), sets[i].end());
+  }
+  // k = 2: one fresh SPF per destination whose k = 1 paths exist; without
+  // k = 1 links the memoized row serves (LinkState.cpp:775-776)
+  std::vector<uint32_t> fresh;
+  for (uint32_t i = 0; i < n_dst; ++i) {
+    if (sets[i].empty()) continue;
+    fresh.push_back(i);
+    ign.insert(ign.end(), sets[i].begin(), sets[i].end());
+    ptr.push_back(static_cast<uint32_t>(ign.size()));
+  }
+  std::vector<KspRow> rows;
+  if (!fresh.empty()) {
+    rc = ksp_rows(g, src, static_cast<uint32_t>(fresh.size()), ptr.data(), ign.data(), rows);
+    if (rc) return rc;
+  }
+  for (uint32_t i = 0, f = 0; i < n_dst; ++i) {
+    if (sets[i].empty()) {
+      k2[i] = ksp_paths(g, src, dsts[i], base[0], none);
+    } else {
+      k2[i] = ksp_paths(g, src, dsts[i], rows[f++], sets[i]);
+    }
+  }
+  size_t need = 0;
+  for (uint32_t i = 0; i < n_dst; ++i)
+    for (const auto* ks : {&k1[i], &k2[i]}) {
+      need += 1;
+      for (const auto& p : *ks) need += 1 + p.size();
+    }
+  *n_words = need;
+  if (need > cap) return cap ? fail(ctx, ORH_E_INVALID, "orh_ksp2: output buffer too small") : ORH_OK;
+  size_t w = 0;
+  for (uint32_t i = 0; i < n_dst; ++i)
+    for (const auto* ks : {&k1[i], &k2[i]}) {
+      out[w++] = static_cast<uint32_t>(ks->size());
+      for (const auto& p : *ks) {
+        out[w++] = static_cast<uint32_t>(p.size());
+        for (uint32_t l : p) out[w++] = l;
+      }
+    }
+  return ORH_OK;
+}
+
 // ---- device prefix mirror + route selection ---------------------------------
 }  // extern "C"
 

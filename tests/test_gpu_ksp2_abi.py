@@ -1,0 +1,76 @@
+"""orh_ksp2 (the C-ABI KSP2 entry point) against the oracle's getKthPaths
+(``-m gpu``): k = 1 and k = 2 paths, link by link, in order.
+
+Covers parallel links (tie order = CSR row order = LinkSet order), drained
+nodes and adjacencies, zero and 64-bit metrics (exact kernel rows), and the
+C4 WAN at full size (50,000 nodes) on sampled (src, dst) pairs - the batched
+k = 2 SPFs of one call run in one launch.
+"""
+import random
+
+import pytest
+
+from openr_amd.facade import LinkDesc, load_topology
+from openr_amd.topology import wan
+from openr_amd.types import K_TESTING_AREA
+
+from test_gpu_parity import random_topology
+
+pytestmark = pytest.mark.gpu
+A = K_TESTING_AREA
+
+
+def _check(als_h, als_o, src, dsts):
+    got = als_h[A]._impl.ksp2_abi(src, dsts)
+    for d, (k1, k2) in zip(dsts, got):
+        for k, paths in ((1, k1), (2, k2)):
+            mine = [[LinkDesc(*l) for l in p] for p in paths]
+            assert mine == als_o[A].get_kth_paths(src, d, k), (src, d, k)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ksp2_abi_random(hip, oracle, seed):
+    dbs = random_topology(1900 + seed, n=18, extra=30, max_metric=3, parallel=0.4, overload=0.1,
+                          link_overload=0.05)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    for src in names[:5]:
+        _check(als_h, als_o, src, names)
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 2), (1 << 30, (1 << 31) - 1)])
+def test_ksp2_abi_exact_rows(hip, oracle, lo, hi):
+    from test_gpu_exact import _topology
+    dbs = _topology(1950, n=16, extra=24, min_metric=lo, max_metric=hi, parallel=0.4, overload=0.0,
+                    link_overload=0.0)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    for src in names[:4]:
+        _check(als_h, als_o, src, names)
+
+
+def test_ksp2_abi_wan_50k(hip, oracle):
+    """C4's WAN: one source, 3 sampled destinations in one call (the oracle's
+    runSpf takes ~10 s per fresh SPF at this size)."""
+    adj_dbs, _ = wan(50000, seed=4)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    rng = random.Random(4)
+    dsts = [f"w{rng.randrange(50000)}" for _ in range(3)]
+    _check(als_h, als_o, "w17", dsts)
+
+
+def test_ksp2_prefetch_wan_50k(hip, oracle):
+    """The LinkState path at C4 size: prefetchKthPaths over sampled pairs
+    (all k = 2 re-runs in one launch), then the memoized getKthPaths."""
+    adj_dbs, _ = wan(50000, seed=4)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    rng = random.Random(44)
+    pairs = [("w17", f"w{rng.randrange(50000)}") for _ in range(2)]
+    als_h[A]._impl.prefetch_kth_paths(pairs)
+    for s, d in pairs:
+        for k in (1, 2):
+            assert als_h[A].get_kth_paths(s, d, k) == als_o[A].get_kth_paths(s, d, k), (s, d, k)
