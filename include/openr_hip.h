@@ -62,6 +62,9 @@ extern "C" {
 #define ORH_META_LINK_MASK 0x3FFFFFFFu /* link id of the CSR entry */
 #define ORH_META_COL_OVERLOADED 0x40000000u /* neighbour node is overloaded */
 #define ORH_META_DOWN 0x80000000u      /* !Link::isUp() (LinkState.cpp:233-236) */
+/* a free CSR slot (row capacity not in use): down, link id all ones; its
+ * col is ignored (the library keeps it at the row's own node) */
+#define ORH_META_EMPTY (ORH_META_DOWN | ORH_META_LINK_MASK)
 
 typedef struct orh_ctx orh_ctx;
 typedef struct orh_graph orh_graph;
@@ -181,6 +184,19 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* h_edge_idx,
                           const uint32_t* h_meta);
 int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* h_node_idx,
                           const uint8_t* h_overloaded);
+/* structural delta (links added / removed: LinkState::addLink / removeLink /
+ * removeNode, LinkState.cpp:421-455, as updateAdjacencyDatabase and
+ * deleteAdjacencyDatabase drive them, :564-738): row h_rows[i] becomes the
+ * entries [h_ptr[i], h_ptr[i+1]) of h_col / h_w_out / h_w_in / h_meta, in
+ * the caller's LinkSet order, and the rest of the row's capacity (its slot
+ * count at load) turns into free slots. CSR entry indices stay stable, so
+ * orh_graph_patch_edges keeps addressing entries by them. n_links is the new
+ * link-id bound. Node ids and n_nodes are unchanged (a new node needs
+ * orh_graph_load). ORH_E_UNSUPPORTED when a row outgrows its capacity:
+ * reload. Only the changed rows' device records are re-uploaded. */
+int orh_graph_apply_delta(orh_graph* g, uint32_t n_rows, const uint32_t* h_rows,
+                          const uint32_t* h_ptr, const uint32_t* h_col, const uint32_t* h_w_out,
+                          const uint32_t* h_w_in, const uint32_t* h_meta, uint32_t n_links);
 int orh_graph_info(const orh_graph* g, uint32_t* n_nodes, uint32_t* n_edges);
 /* device array of the graph's node overload flags (u8 [n_nodes]), valid
  * until the next orh_graph_load (route selection's drained-node filter) */

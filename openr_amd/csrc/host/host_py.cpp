@@ -579,6 +579,7 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              return out;
            })
+      .def("mirror_stats", &LinkState::mirrorStats)
       .def("ksp2_abi",  // orh_ksp2 straight through the C ABI: per dst (k = 1 paths, k = 2 paths)
            [](const LinkState& s, const std::string& a, const std::vector<std::string>& dsts) {
              auto src = s.nodeId(a);

@@ -186,7 +186,8 @@ uint32_t LinkState::addLink(Link&& l) {  // LinkState.cpp:421-426
   if (!setOf(first).insert(id).second || !setOf(second).insert(id).second)
     throw std::logic_error("LinkState: duplicate link");
   ++nLinks_;
-  structDirty_ = true;
+  rowsDirty_.insert(first);
+  rowsDirty_.insert(second);
   return id;
 }
 
@@ -198,20 +199,22 @@ void LinkState::removeLink(uint32_t id) {  // LinkState.cpp:429-434
   k.alive = false;
   freeLinks_.push_back(id);
   --nLinks_;
-  structDirty_ = true;
+  rowsDirty_.insert(first);
+  rowsDirty_.insert(k.other(first));
 }
 
 void LinkState::removeNode(uint32_t v) {  // LinkState.cpp:436-455
   std::vector<uint32_t> ids(setOf(v).begin(), setOf(v).end());
   for (uint32_t id : ids) {
     setOf(links_[id].other(v)).erase(id);
+    rowsDirty_.insert(links_[id].other(v));
     links_[id].alive = false;
     freeLinks_.push_back(id);
     --nLinks_;
   }
   setOf(v).clear();
-  nodeOverloads_.erase(names_[v]);
-  structDirty_ = true;
+  rowsDirty_.insert(v);
+  if (nodeOverloads_.erase(names_[v])) patchNodes_.insert(v);
 }
 
 std::vector<uint32_t> LinkState::orderedLinks(uint32_t v) const {
@@ -364,6 +367,56 @@ bool LinkState::hasHolds() const {
 // ---- device mirror -----------------------------------------------------------
 void LinkState::flushMirror() const {
   const uint32_t N = static_cast<uint32_t>(names_.size());
+  if (!structDirty_ && !rowsDirty_.empty()) {
+    // links added / removed, node set unchanged: rewrite only the changed
+    // rows (in LinkSet order) inside their load-time capacity
+    std::vector<uint32_t> rows(rowsDirty_.begin(), rowsDirty_.end()), ptr(1, 0), col, wout, win, meta;
+    std::sort(rows.begin(), rows.end());
+    bool fits = true;
+    for (uint32_t v : rows) {
+      if (nodeLinks_[v]->size() > rowPtr_[v + 1] - rowPtr_[v]) {
+        fits = false;
+        break;
+      }
+      for (uint32_t id : *nodeLinks_[v]) {
+        const Link& l = links_[id];
+        const uint32_t u = l.other(v);
+        const bool up = l.isUp();
+        col.push_back(u);
+        wout.push_back(up ? toDeviceMetric(l.metricFrom(v)) : 1u);
+        win.push_back(up ? toDeviceMetric(l.metricFrom(u)) : 1u);
+        meta.push_back(id | (up ? 0u : ORH_META_DOWN));
+      }
+      ptr.push_back(static_cast<uint32_t>(col.size()));
+    }
+    const int rc = fits ? orh_graph_apply_delta(graph_, static_cast<uint32_t>(rows.size()), rows.data(),
+                                                ptr.data(), col.data(), wout.data(), win.data(),
+                                                meta.data(), static_cast<uint32_t>(links_.size()))
+                        : ORH_E_UNSUPPORTED;
+    if (rc == ORH_OK) {
+      ++mirrorDeltas_;
+      entriesOfLink_.resize(links_.size(), {0u, 0u});
+      for (uint32_t v : rows) {
+        uint32_t e = rowPtr_[v];
+        for (uint32_t id : *nodeLinks_[v]) {
+          const Link& l = links_[id];
+          col_[e] = l.other(v);
+          linkOfEntry_[e] = id;
+          (l.is1(v) ? entriesOfLink_[id].first : entriesOfLink_[id].second) = e;
+          ++e;
+        }
+        for (; e < rowPtr_[v + 1]; ++e) {
+          col_[e] = v;
+          linkOfEntry_[e] = ~0u;
+        }
+      }
+      rowsDirty_.clear();
+    } else if (rc == ORH_E_UNSUPPORTED) {
+      structDirty_ = true;  // a row outgrew its capacity: reload
+    } else {
+      check(ctx_, rc, "orh_graph_apply_delta");
+    }
+  }
   if (structDirty_) {
     rowPtr_.assign(N + 1, 0);
     col_.clear();
@@ -406,7 +459,9 @@ void LinkState::flushMirror() const {
     c.meta = meta.data();
     c.node_overloaded = ovl.data();
     check(ctx_, orh_graph_load(graph_, &c), "orh_graph_load");
+    ++mirrorLoads_;
     structDirty_ = false;
+    rowsDirty_.clear();
     patchLinks_.clear();
     patchNodes_.clear();
     return;

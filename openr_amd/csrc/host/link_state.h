@@ -193,6 +193,8 @@ class LinkState {
 
   // device mirror access (bench / batch callers)
   orh_graph* deviceGraph() const;  // flushes pending deltas first
+  // device mirror uploads so far: full orh_graph_load calls, row deltas
+  std::pair<uint64_t, uint64_t> mirrorStats() const { return {mirrorLoads_, mirrorDeltas_}; }
   orh_ctx* context() const { return ctx_; }
 
  private:
@@ -239,7 +241,9 @@ class LinkState {
   std::unordered_map<std::string, AdjacencyDatabase> adjacencyDatabases_;
 
   // device mirror bookkeeping
-  mutable bool structDirty_{true};
+  mutable bool structDirty_{true};                 // node set changed: full orh_graph_load
+  mutable std::unordered_set<uint32_t> rowsDirty_;  // link sets changed: orh_graph_apply_delta
+  mutable uint64_t mirrorLoads_{0}, mirrorDeltas_{0};
   mutable std::unordered_set<uint32_t> patchLinks_;
   mutable std::unordered_set<uint32_t> patchNodes_;
   mutable std::vector<uint32_t> rowPtr_;  // host copy of the uploaded CSR

@@ -165,6 +165,10 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s,
 hipError_t launch_ms_finalize(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
 
 // recs[pos[i]] = vals[i] for i < n (device pointers)
+// recs[pos[i]] = vals[i], link[pos[i]] = links[i], rank[pos[i]] = ranks[i]
+hipError_t launch_scatter_rows(uint2* recs, uint32_t* link, uint16_t* rank, const uint32_t* pos,
+                               const uint2* vals, const uint32_t* links, const uint16_t* ranks,
+                               uint32_t n, hipStream_t s);
 hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* vals, uint32_t n,
                                hipStream_t s);
 

@@ -1957,6 +1957,27 @@ __global__ __launch_bounds__(kBlock) void scatter_recs_kernel(uint2* recs, const
   if (i < n) recs[pos[i]] = vals[i];
 }
 
+__global__ __launch_bounds__(kBlock) void scatter_rows_kernel(uint2* recs, uint32_t* link, uint16_t* rank,
+                                                               const uint32_t* pos, const uint2* vals,
+                                                               const uint32_t* links,
+                                                               const uint16_t* ranks, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t q = pos[i];
+  recs[q] = vals[i];
+  link[q] = links[i];
+  rank[q] = ranks[i];
+}
+
+hipError_t launch_scatter_rows(uint2* recs, uint32_t* link, uint16_t* rank, const uint32_t* pos,
+                               const uint2* vals, const uint32_t* links, const uint16_t* ranks,
+                               uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, recs,
+                     link, rank, pos, vals, links, ranks, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_scatter_recs(uint2* recs, const uint32_t* pos, const uint2* vals, uint32_t n,
                                hipStream_t s) {
   if (n == 0) return hipSuccess;

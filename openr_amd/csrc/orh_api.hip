@@ -152,12 +152,15 @@ void build_neighbours(orh_graph* g) {
   g->rank_out.assign(g->n_edges, 0);
   std::vector<uint32_t> l;
   for (uint32_t v = 0; v < N; ++v) {
-    l.assign(g->col.begin() + g->row_ptr[v], g->col.begin() + g->row_ptr[v + 1]);
+    l.clear();
+    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e)
+      if (g->meta[e] != ORH_META_EMPTY) l.push_back(g->col[e]);
     std::sort(l.begin(), l.end());
     l.erase(std::unique(l.begin(), l.end()), l.end());
     for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e)
-      g->rank_out[e] = static_cast<uint16_t>(
-          std::lower_bound(l.begin(), l.end(), g->col[e]) - l.begin());
+      g->rank_out[e] = g->meta[e] == ORH_META_EMPTY
+          ? 0
+          : static_cast<uint16_t>(std::lower_bound(l.begin(), l.end(), g->col[e]) - l.begin());
     g->dn.insert(g->dn.end(), l.begin(), l.end());
     g->dn_ptr[v + 1] = static_cast<uint32_t>(g->dn.size());
   }
@@ -592,7 +595,8 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
     if (c->row_ptr[v] > c->row_ptr[v + 1])
       return fail(ctx, ORH_E_INVALID, "orh_graph_load: row_ptr not monotone");
   for (uint32_t e = 0; e < c->n_edges; ++e)
-    if (c->col[e] >= c->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_graph_load: col out of range");
+    if (c->meta[e] != ORH_META_EMPTY && c->col[e] >= c->n_nodes)
+      return fail(ctx, ORH_E_INVALID, "orh_graph_load: col out of range");
   if (c->name_rank)
     for (uint32_t v = 0; v < c->n_nodes; ++v)
       if (c->name_rank[v] >= c->n_nodes)
@@ -608,6 +612,9 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   g->w_out.assign(c->w_out, c->w_out + c->n_edges);
   g->w_in.assign(c->w_in, c->w_in + c->n_edges);
   g->meta.assign(c->meta, c->meta + c->n_edges);
+  for (uint32_t v = 0; v < c->n_nodes; ++v)  // free slots point at their own row
+    for (uint32_t e = c->row_ptr[v]; e < c->row_ptr[v + 1]; ++e)
+      if (g->meta[e] == ORH_META_EMPTY) g->col[e] = v;
   g->overloaded.assign(c->node_overloaded, c->node_overloaded + c->n_nodes);
   for (auto& o : g->overloaded) o = o ? 1 : 0;
   g->name_rank.resize(c->n_nodes);
@@ -659,7 +666,9 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
     const uint32_t e = idx[i];
     if (e >= g->n_edges) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: bad edge index");
     if ((meta[i] & ORH_META_LINK_MASK) != (g->meta[e] & ORH_META_LINK_MASK))
-      return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: link id changed (use load)");
+      return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: link id changed (use orh_graph_apply_delta)");
+    if (g->meta[e] == ORH_META_EMPTY && meta[i] != ORH_META_EMPTY)
+      return fail(ctx, ORH_E_INVALID, "orh_graph_patch_edges: free slot (use orh_graph_apply_delta)");
   }
   ORH_HIP(ctx, hipSetDevice(ctx->device));
   std::vector<std::pair<uint32_t, uint32_t>> edges;
@@ -676,6 +685,98 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
   int rc = upload_records(g, edges);
   if (rc) return rc;
   recompute_bounds(g);
+  return ORH_OK;
+}
+
+int orh_graph_apply_delta(orh_graph* g, uint32_t n_rows, const uint32_t* rows, const uint32_t* ptr,
+                          const uint32_t* col, const uint32_t* w_out, const uint32_t* w_in,
+                          const uint32_t* meta, uint32_t n_links) {
+  if (!g || (n_rows && (!rows || !ptr))) return ORH_E_INVALID;
+  orh_ctx* ctx = g->ctx;
+  if (!g->d_recs) return fail(ctx, ORH_E_STATE, "orh_graph_apply_delta: no graph loaded");
+  const uint32_t N = g->n_nodes;
+  if (n_rows && ptr[0] != 0) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: ptr[0] != 0");
+  std::vector<uint8_t> seen(N, 0);
+  for (uint32_t i = 0; i < n_rows; ++i) {
+    const uint32_t v = rows[i];
+    if (v >= N || seen[v]) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: bad or repeated row");
+    seen[v] = 1;
+    if (ptr[i + 1] < ptr[i]) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: ptr not monotone");
+    if (ptr[i + 1] - ptr[i] > g->row_ptr[v + 1] - g->row_ptr[v])
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_apply_delta: row " + std::to_string(v) +
+                                              " outgrows its capacity (reload)");
+  }
+  const uint32_t n_ent = n_rows ? ptr[n_rows] : 0u;
+  if (n_ent && (!col || !w_out || !w_in || !meta)) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: null array");
+  for (uint32_t k = 0; k < n_ent; ++k) {
+    if (col[k] >= N) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: col out of range");
+    if (meta[k] != ORH_META_EMPTY && (meta[k] & ORH_META_LINK_MASK) >= std::max<uint32_t>(n_links, 1))
+      return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: link id >= n_links");
+  }
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  for (uint32_t i = 0; i < n_rows; ++i) {
+    const uint32_t v = rows[i], e0 = g->row_ptr[v], cap = g->row_ptr[v + 1] - e0;
+    const uint32_t d = ptr[i + 1] - ptr[i];
+    for (uint32_t j = 0; j < cap; ++j) {
+      const uint32_t e = e0 + j;
+      if (j < d) {
+        const uint32_t k = ptr[i] + j;
+        g->col[e] = meta[k] == ORH_META_EMPTY ? v : col[k];
+        g->w_out[e] = w_out[k];
+        g->w_in[e] = w_in[k];
+        g->meta[e] = meta[k] == ORH_META_EMPTY ? meta[k] : meta[k] & ~ORH_META_COL_OVERLOADED;
+      } else {
+        g->col[e] = v;
+        g->w_out[e] = g->w_in[e] = 1;
+        g->meta[e] = ORH_META_EMPTY;
+      }
+    }
+  }
+  g->n_links = n_links;
+  build_neighbours(g);
+  for (uint32_t i = 0; i < n_rows; ++i)
+    if (n_distinct(g, rows[i]) > 0xFFFFu)
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_apply_delta: more than 65535 neighbours (reload)");
+  recompute_bounds(g);
+  // the changed rows' device records, link ids and neighbour ranks
+  std::vector<uint32_t> pos;
+  std::vector<uint2> vals;
+  std::vector<uint32_t> links;
+  std::vector<uint16_t> ranks;
+  for (uint32_t i = 0; i < n_rows; ++i) {
+    const uint32_t v = rows[i];
+    for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) {
+      pos.push_back(g->pos[e]);
+      vals.push_back(device_record(g, v, e));
+      links.push_back(g->meta[e] & ORH_META_LINK_MASK);
+      ranks.push_back(g->rank_out[e]);
+    }
+  }
+  const uint32_t n = static_cast<uint32_t>(pos.size());
+  if (n) {
+    // staging: pos u32[n] | links u32[n] | vals uint2[n] | ranks u16[n]
+    const size_t words = 2 * size_t{n} + 2 * size_t{n} + (size_t{n} + 1) / 2;
+    std::vector<uint32_t> st(words, 0);
+    std::memcpy(st.data(), pos.data(), 4 * size_t{n});
+    std::memcpy(st.data() + n, links.data(), 4 * size_t{n});
+    std::memcpy(st.data() + 2 * size_t{n}, vals.data(), 8 * size_t{n});
+    std::memcpy(st.data() + 4 * size_t{n}, ranks.data(), 2 * size_t{n});
+    if (st.size() > ctx->d_patch_cap) {
+      (void)hipFree(ctx->d_patch);
+      ctx->d_patch = nullptr;
+      ctx->d_patch_cap = 0;
+      ORH_HIP(ctx, hipMalloc(&ctx->d_patch, st.size() * sizeof(uint32_t)));
+      ctx->d_patch_cap = st.size();
+    }
+    ORH_HIP(ctx, hipMemcpyAsync(ctx->d_patch, st.data(), st.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, orh::launch_scatter_rows(
+                     g->d_recs, g->d_link, g->d_rank_out, ctx->d_patch,
+                     reinterpret_cast<const uint2*>(ctx->d_patch + 2 * size_t{n}), ctx->d_patch + n,
+                     reinterpret_cast<const uint16_t*>(ctx->d_patch + 4 * size_t{n}), n, ctx->stream));
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
+  }
+  g->ms_dirty = true;
+  g->gen = next_graph_gen();  // staged requests hold neighbour lists of the old rows
   return ORH_OK;
 }
 
@@ -1413,7 +1514,7 @@ int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, u
   for (uint32_t i = 0; i < n_dst; ++i)
     if (dsts[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_ksp2: destination out of range");
   for (uint32_t e = 0; e < g->n_edges; ++e)
-    if ((g->meta[e] & ORH_META_LINK_MASK) >= std::max<uint32_t>(g->n_links, 1))
+    if (g->meta[e] != ORH_META_EMPTY && (g->meta[e] & ORH_META_LINK_MASK) >= std::max<uint32_t>(g->n_links, 1))
       return fail(ctx, ORH_E_INVALID, "orh_ksp2: link id >= n_links");
   // k = 1: src's own SPF
   std::vector<KspRow> base;
