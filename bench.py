@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
     p.add_argument("--topologies", type=int, default=8,
                    help="what-if variants per step (--scaling whatif)")
+    p.add_argument("--lanes", type=int, default=1,
+                   help="stream lanes per rank: a rank's what-if variants are dealt over this many "
+                        "contexts (own HIP stream each) so their sweeps overlap on the GPU")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="oracle threads (0: every CPU this process may use)")
@@ -121,11 +124,11 @@ def main():
         units = [(rank, names)]
         total_units = n * n * world
     sweeps, base = [], None
-    for t, srcs in units:
+    for i, (t, srcs) in enumerate(units):
         adj_dbs, prefixes = bench_grid(n, 1)
         if t > 0:
             drain_what_if_link(adj_dbs, n, t)
-        als, ps = load_topology(hip, adj_dbs, prefixes)
+        als, ps = load_topology(hip, adj_dbs, prefixes, lane=i % max(1, args.lanes))
         ls = als[K_TESTING_AREA]
         if srcs is None:
             degrees = [len(db.adjacencies) for db in adj_dbs]

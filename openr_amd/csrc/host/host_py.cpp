@@ -269,6 +269,7 @@ py::dict rowToDict(const LinkState& ls, const SpfRow& row, bool withPaths) {
 
 struct AreaMap {
   AreaLinkStates m;
+  unsigned lane = 0;  // stream lane of every area's context (laneContext)
 };
 
 // all-sources sweep over a LinkState's device mirror (bench / parity tools):
@@ -737,11 +738,17 @@ PYBIND11_MODULE(_openr_host, m) {
   });
 
   py::class_<AreaMap>(m, "AreaLinkStates")
-      .def(py::init<>())
+      .def(py::init([](unsigned lane) {
+             laneContext(lane);  // validate (and create) before any area uses it
+             auto* a = new AreaMap();
+             a->lane = lane;
+             return a;
+           }),
+           py::arg("lane") = 0u)
       .def("add_area",
            [](AreaMap& a, const std::string& area) {
              a.m.emplace(std::piecewise_construct, std::forward_as_tuple(area),
-                         std::forward_as_tuple(area));
+                         std::forward_as_tuple(area, laneContext(a.lane)));
            })
       .def("area", [](AreaMap& a, const std::string& area) -> LinkState& { return a.m.at(area); },
            py::return_value_policy::reference_internal)

@@ -49,6 +49,23 @@ orh_ctx* defaultContext() {
   return ctx;
 }
 
+orh_ctx* laneContext(unsigned lane) {
+  if (lane == 0) return defaultContext();
+  if (lane >= kMaxLanes) throw std::invalid_argument("laneContext: lane out of range");
+  static std::mutex mu;
+  static orh_ctx* lanes[kMaxLanes] = {};
+  std::lock_guard<std::mutex> lock(mu);
+  if (!lanes[lane]) {
+    int dev = 0;
+    if (const char* e = std::getenv("ORH_DEVICE")) dev = std::atoi(e);
+    const int rc = orh_create(dev, 0, &lanes[lane]);
+    if (rc != ORH_OK)
+      throw std::runtime_error("libopenr_hip: orh_create for lane " + std::to_string(lane) +
+                               " failed (rc=" + std::to_string(rc) + ")");
+  }
+  return lanes[lane];
+}
+
 // ---- HoldableValue (LinkState.cpp:87-121) ---------------------------------
 template <>
 bool Holdable<bool>::update(bool v, Metric upTtl, Metric downTtl) {

@@ -36,6 +36,12 @@ namespace openr_amd {
 // (ORH_DEVICE env or device 0); throws if no GPU is available
 orh_ctx* defaultContext();
 
+// context of stream lane `lane` on the same device: lane 0 is defaultContext(),
+// lanes 1..kMaxLanes-1 are extra contexts (own HIP stream, own scratch) created
+// on first use, so independent searches (what-if topologies) overlap on the GPU
+constexpr unsigned kMaxLanes = 32;
+orh_ctx* laneContext(unsigned lane);
+
 template <class T>
 class Holdable {  // HoldableValue, LinkState.h:36-58
  public:

@@ -99,8 +99,8 @@ class LinkState:
 class AreaLinkStates:
     """std::unordered_map<std::string /* area */, LinkState>."""
 
-    def __init__(self, backend_mod):
-        self._impl = backend_mod.AreaLinkStates()
+    def __init__(self, backend_mod, lane: int = 0):
+        self._impl = backend_mod.AreaLinkStates(lane) if lane else backend_mod.AreaLinkStates()
         self._areas = {}
 
     def add_area(self, area: str) -> LinkState:
@@ -198,8 +198,10 @@ class Backend:
         self.module = module
         self.name = name
 
-    def area_link_states(self, *areas) -> AreaLinkStates:
-        als = AreaLinkStates(self.module)
+    def area_link_states(self, *areas, lane: int = 0) -> AreaLinkStates:
+        """lane > 0: the areas' device work goes to stream lane `lane` (its own
+        context and HIP stream), so independent topologies overlap on the GPU."""
+        als = AreaLinkStates(self.module, lane) if lane else AreaLinkStates(self.module)
         for a in areas:
             als.add_area(a)
         return als
@@ -224,11 +226,11 @@ class Backend:
         return f"Backend({self.name})"
 
 
-def load_topology(backend: Backend, adj_dbs, prefixes, als=None, ps=None):
+def load_topology(backend: Backend, adj_dbs, prefixes, als=None, ps=None, lane: int = 0):
     """Feed generator output (openr_amd.topology) into a backend."""
     if als is None:
         areas = sorted({db.area for db in adj_dbs} | {a for _, a, _ in prefixes})
-        als = backend.area_link_states(*areas)
+        als = backend.area_link_states(*areas, lane=lane) if lane else backend.area_link_states(*areas)
     if ps is None:
         ps = backend.prefix_state()
     for db in adj_dbs:

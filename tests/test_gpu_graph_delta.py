@@ -73,4 +73,6 @@ def test_delete_adjacency_database(hip, oracle):
             ls.delete_adjacency_database(victim)
         _views_equal(als_h, als_o, names, victim)
     loads, deltas = als_h[A]._impl.mirror_stats()
-    assert deltas >= 3 and loads == 1, (loads, deltas)
+    # one row delta per deletion that still removed links (a victim whose
+    # links all went with earlier victims changes no row), never a reload
+    assert 1 <= deltas <= 3 and loads == 1, (loads, deltas)
