@@ -12,7 +12,9 @@ A step (--scaling):
                     (variant 0 the grid itself, variant t > 0 the grid with one
                     seeded link drained), every one swept from all 10,000
                     sources; the variants are split over the ranks (strong
-                    scaling: total work fixed, no data-path collective)
+                    scaling: total work fixed, no data-path collective), and a
+                    rank deals its variants over --lanes contexts (one HIP
+                    stream each) so independent sweeps overlap on the GPU
   strong            one topology, its 10,000 sources split into contiguous
                     degree-weighted blocks over the ranks
   weak              every rank sweeps all sources of its own variant
@@ -47,9 +49,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--grid", type=int, default=100)
     p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
-    p.add_argument("--topologies", type=int, default=8,
+    p.add_argument("--topologies", type=int, default=32,
                    help="what-if variants per step (--scaling whatif)")
-    p.add_argument("--lanes", type=int, default=1,
+    p.add_argument("--lanes", type=int, default=4,
                    help="stream lanes per rank: a rank's what-if variants are dealt over this many "
                         "contexts (own HIP stream each) so their sweeps overlap on the GPU")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
@@ -63,7 +65,8 @@ def parse():
 
 
 def drain_what_if_link(adj_dbs, n, rank):
-    """Overload both adjacencies of one seeded grid link (a what-if failure)."""
+    """Overload both adjacencies of one seeded grid link (a what-if failure);
+    returns them (clear isOverloaded to undo)."""
     import random
     rng = random.Random(1000 + rank)
     db = adj_dbs[rng.randrange(n * n)]
@@ -73,7 +76,8 @@ def drain_what_if_link(adj_dbs, n, rank):
     for back in peer.adjacencies:
         if back.otherNodeName == db.thisNodeName:
             back.isOverloaded = True
-            break
+            return [adj, back]
+    return [adj]
 
 
 def median_ms(fn, reps):
@@ -124,11 +128,12 @@ def main():
         units = [(rank, names)]
         total_units = n * n * world
     sweeps, base = [], None
+    adj_dbs, prefixes = bench_grid(n, 1)  # one grid; a variant drains a link while it loads
     for i, (t, srcs) in enumerate(units):
-        adj_dbs, prefixes = bench_grid(n, 1)
-        if t > 0:
-            drain_what_if_link(adj_dbs, n, t)
+        drained = drain_what_if_link(adj_dbs, n, t) if t > 0 else []
         als, ps = load_topology(hip, adj_dbs, prefixes, lane=i % max(1, args.lanes))
+        for adj in drained:
+            adj.isOverloaded = False
         ls = als[K_TESTING_AREA]
         if srcs is None:
             degrees = [len(db.adjacencies) for db in adj_dbs]

@@ -133,6 +133,17 @@ int orh_reset_counters(orh_ctx* ctx);
  * anyway for graphs with a zero-metric live link */
 #define ORH_SPF_EXACT 4
 int orh_set_spf_mode(orh_ctx* ctx, int mode);
+/* what-if repair for ignore-set batches (runSpf(src, m, linksToIgnore)):
+ * the batch's distinct sources get plain SPFs and every request's row is
+ * derived from its source's row (only nodes below a tight ignored link are
+ * recomputed; results are identical). ORH_REPAIR_AUTO (default) uses it when
+ * sources repeat (distinct <= half the requests) and every ignore set has at
+ * most 8 links; ORH_REPAIR_ALWAYS for every batch it can take; env
+ * ORH_WHATIF_REPAIR sets the initial mode */
+#define ORH_REPAIR_OFF 0
+#define ORH_REPAIR_AUTO 1
+#define ORH_REPAIR_ALWAYS 2
+int orh_set_repair_mode(orh_ctx* ctx, int mode);
 /* kernel plan of the last orh_spf_run on this context (tests and profiling
  * assert which variant ran; results never depend on it) */
 #define ORH_VARIANT_MSBFS 1     /* bit-parallel multi-source BFS */
@@ -145,6 +156,8 @@ int orh_set_spf_mode(orh_ctx* ctx, int mode);
 #define ORH_VARIANT_GLOBAL_NH 8 /* HBM frontier kernel with fused first hops */
 #define ORH_VARIANT_EXACT 9     /* exact Dijkstra in the reference's extraction order */
 #define ORH_VARIANT_BFS_NH 10   /* BFS with fused first hops, one workgroup per source */
+#define ORH_VARIANT_REPAIR 11   /* ignore-set batch repaired from its sources' plain rows
+                                   (batch_sources = distinct sources searched) */
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */

@@ -25,7 +25,8 @@ HOST_MOD = os.path.join(PKG, "_openr_host" + EXT)
 ARCH = os.environ.get("OPENR_HIP_ARCH", "gfx950")
 
 HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "spf_kernels.hip"),
-            os.path.join(CSRC, "kernels", "route_kernels.hip")]
+            os.path.join(CSRC, "kernels", "route_kernels.hip"),
+            os.path.join(CSRC, "kernels", "whatif_kernels.hip")]
 HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "prefix_state.cpp", "spf_solver.cpp",
                                                    "rib_policy.cpp", "host_py.cpp")]
 
@@ -58,13 +59,38 @@ def _run(cmd):
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
+def _includes(src, seen=None):
+    """The source and every header it reaches through #include "..." lines."""
+    import re
+    seen = set() if seen is None else seen
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    with open(src) as f:
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            _includes(os.path.normpath(os.path.join(os.path.dirname(src), m.group(1))), seen)
+    return seen
+
+
 def build_hip_lib(force: bool = False) -> str:
-    deps = _deps(HIP_SRCS, [os.path.join(CSRC, "kernels"), os.path.join(ROOT, "include")])
-    if force or _stale(HIP_LIB, deps):
-        os.makedirs(LIB_DIR, exist_ok=True)
+    """One object per HIP source (rebuilt when it or a header it includes
+    changed), compiled in parallel, then one shared link."""
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    objs = [os.path.join(obj_dir, os.path.basename(s) + ".o") for s in HIP_SRCS]
+    todo = [(s, o) for s, o in zip(HIP_SRCS, objs) if force or _stale(o, sorted(_includes(s)))]
+
+    def compile_one(so):
+        src, obj = so
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c",
+              "-Wno-unused-value", "-Wno-unused-result", "-o", obj + ".tmp", src])
+        os.replace(obj + ".tmp", obj)
+
+    with ThreadPoolExecutor(max(1, len(todo))) as ex:
+        list(ex.map(compile_one, todo))
+    if force or todo or _stale(HIP_LIB, objs):
         tmp = HIP_LIB + ".tmp"
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wno-unused-value", "-Wno-unused-result", "-o", tmp] + HIP_SRCS)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", tmp] + objs)
         os.replace(tmp, HIP_LIB)
     return HIP_LIB
 

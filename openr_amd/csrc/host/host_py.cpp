@@ -581,6 +581,16 @@ PYBIND11_MODULE(_openr_host, m) {
              return out;
            })
       .def("mirror_stats", &LinkState::mirrorStats)
+      .def("last_spf_info",  // kernel plan of the last SPF launch on this LinkState's context
+           [](const LinkState& s) {
+             orh_spf_info i{};
+             orh_last_spf_info(s.context(), &i);
+             py::dict d;
+             d["variant"] = i.variant;
+             d["rows"] = i.rows;
+             d["batch_sources"] = i.batch_sources;
+             return d;
+           })
       .def("ksp2_abi",  // orh_ksp2 straight through the C ABI: per dst (k = 1 paths, k = 2 paths)
            [](const LinkState& s, const std::string& a, const std::vector<std::string>& dsts) {
              auto src = s.nodeId(a);
@@ -670,7 +680,7 @@ PYBIND11_MODULE(_openr_host, m) {
            py::keep_alive<0, 1>())
       .def("run_spf_batch",
            [](const LinkState& s, const std::vector<std::string>& srcs,
-              const std::vector<std::vector<uint32_t>>& ignore) {
+              const std::vector<std::vector<uint32_t>>& ignore, bool useLinkMetric) {
              std::vector<uint32_t> ids;
              for (const auto& n : srcs) {
                auto id = s.nodeId(n);
@@ -678,7 +688,7 @@ PYBIND11_MODULE(_openr_host, m) {
                ids.push_back(*id);
              }
              py::list out;
-             for (const auto& row : s.runSpfBatch(ids, true, ignore.empty() ? nullptr : &ignore)) {
+             for (const auto& row : s.runSpfBatch(ids, useLinkMetric, ignore.empty() ? nullptr : &ignore)) {
                py::dict d;
                for (auto item : rowToDict(s, row, false)) {
                  auto v = item.second.cast<py::tuple>();
@@ -687,7 +697,8 @@ PYBIND11_MODULE(_openr_host, m) {
                out.append(d);
              }
              return out;
-           })
+           },
+           py::arg("srcs"), py::arg("ignore"), py::arg("use_link_metric") = true)
       .def("prefetch_spf_results", &LinkState::prefetchSpfResults, py::arg("nodes"),
            py::arg("use_link_metric") = true)
       .def("prefetch_kth_paths", &LinkState::prefetchKthPaths)
@@ -921,6 +932,11 @@ PYBIND11_MODULE(_openr_host, m) {
   });
   // distance-kernel selection on the default context (ORH_SPF_AUTO /
   // ORH_SPF_PER_SOURCE / ORH_SPF_GLOBAL); results are identical in every mode
+  // what-if repair on the default context (ORH_REPAIR_OFF / _AUTO / _ALWAYS)
+  m.def("set_repair_mode", [](int mode) {
+    if (orh_set_repair_mode(defaultContext(), mode) != ORH_OK)
+      throw std::invalid_argument("set_repair_mode: bad mode");
+  });
   m.def("set_spf_mode", [](int mode) {
     if (orh_set_spf_mode(defaultContext(), mode) != ORH_OK)
       throw std::invalid_argument("set_spf_mode: mode must be 0, 1, 2 or 3");

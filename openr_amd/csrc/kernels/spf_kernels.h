@@ -48,6 +48,9 @@ struct SpfArgs {
   const uint16_t* rank_out;
   uint8_t* lvl_rows;  // multi-source BFS: u8 level row per row [n_rows][lvl_pitch]
   uint32_t lvl_pitch;  // N rounded up to 16
+  // HBM kernel with fused first hops: rows whose flag is 0 are skipped (the
+  // what-if repair's fallback searches only the rows it could not repair)
+  const uint32_t* row_mask;  // [n_rows], nullable
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -86,7 +89,8 @@ enum class SpfVariant {
   kUnsupported = 0, kMsBfs, kBfs8, kBfs16, kBfs32, kDist16, kDist32, kGlobal,
   kGlobalNh,  // HBM frontier kernel that also derives the first hops (no phase 2)
   kExact,     // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
-  kBfsNh      // uniform metric, few sources: BFS with the first hops fused (no phase 2)
+  kBfsNh,     // uniform metric, few sources: BFS with the first hops fused (no phase 2)
+  kRepair     // ignore-set batch derived from its sources' plain SPFs (whatif_kernels.hip)
 };
 // fused BFS + first hops (spf_bfs_nh_kernel): workgroup size, nodes per
 // thread and LDS bytes for N nodes and `words` first-hop words per node;

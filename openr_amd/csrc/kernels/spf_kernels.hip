@@ -1137,7 +1137,7 @@ __global__ __launch_bounds__(256) void spf_global_kernel(SpfArgs a) {
 // every far push, recomputed exactly while promoting), so advancing the
 // threshold costs one pass over the far nodes instead of two.
 template <int K>
-__global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
+__global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_flag[3];
   __shared__ uint32_t s_min[2];
@@ -1145,9 +1145,14 @@ __global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
   constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
+  // frontier nodes a thread expands together: their record, label and
+  // neighbour-label loads are in flight at once (one round trip per stage
+  // for the group instead of per node)
+  constexpr int G = K <= 4 ? 4 : 2;
   uint32_t* near0 = lds;
   uint32_t* near1 = lds + NB;
   uint32_t* far = lds + 2 * NB;
+  if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
   const Src s(a, row);
   unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
 
@@ -1169,55 +1174,95 @@ __global__ __launch_bounds__(256) void spf_global_nh_kernel(SpfArgs a) {
   uint32_t mpar = 0;  // s_min[mpar] bounds the far set from below
   for (uint32_t it = 0;; ++it) {
     bool pushed_near = false;
-    for (uint32_t w = tid; w < NB; w += nthr) {
-      uint32_t bits = cur[w];
-      if (!bits) continue;
-      cur[w] = 0u;
-      while (bits) {
-        const uint32_t v = w * 32 + __builtin_ctz(bits);
+    // merge the candidate {nd, cnh} into u's label: smaller replaces, equal
+    // ORs (cl: u's label as loaded); re-queue u if the label changed
+    auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, unsigned long long cl) {
+      for (;;) {
+        const uint32_t cd = static_cast<uint32_t>(cl >> 32);
+        if (nd > cd) return;
+        const unsigned long long nl = nd < cd
+            ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
+            : (cl | cnh);
+        if (nl == cl) return;
+        const unsigned long long old = atomicCAS(&lab[u], cl, nl);
+        if (old == cl) break;
+        cl = old;
+      }
+      const uint32_t bit = 1u << (u & 31u);
+      if (nd < T) {
+        atomicOr(&nxt[u >> 5], bit);
+        atomicAnd(&far[u >> 5], ~bit);  // expanded from the near set instead
+        pushed_near = true;
+      } else {
+        atomicOr(&far[u >> 5], bit);
+        atomicMin(&s_min[mpar], nd);
+      }
+    };
+    uint32_t w = tid, bits = 0, wbase = 0;
+    for (;;) {
+      // up to G frontier nodes of this thread's words
+      uint32_t vs[G];
+      int c = 0;
+      while (c < G) {
+        while (!bits && w < NB) {
+          bits = cur[w];
+          if (bits) {
+            cur[w] = 0u;
+            wbase = w * 32;
+          }
+          w += nthr;
+        }
+        if (!bits) break;
+        vs[c++] = wbase + __builtin_ctz(bits);
         bits &= bits - 1;
-        uint2 rec[K];
-        load_recs<K>(a, v, rec);
-        if (v != s.node && (rec[0].x & ORH_REC_ROW_OVL)) continue;  // no transit
-        const unsigned long long lv =
-            __hip_atomic_load(&lab[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t dv = static_cast<uint32_t>(lv >> 32);
-        const uint32_t nhv = static_cast<uint32_t>(lv);
-        const bool from_src = v == s.node;
-        auto relax = [&](const uint2& r, uint32_t q) {
-          if (!live(a, s, r, q)) return;
-          const uint32_t u = r.x & ORH_REC_COL_MASK;
-          const uint32_t nd = dv + (a.use_link_metric ? r.y : 1u);
-          const uint32_t cnh = from_src ? (1u << a.rank_out[q]) : nhv;
-          unsigned long long cl =
-              __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          for (;;) {
-            const uint32_t cd = static_cast<uint32_t>(cl >> 32);
-            if (nd > cd) return;
-            const unsigned long long nl = nd < cd
-                ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
-                : (cl | cnh);
-            if (nl == cl) return;
-            const unsigned long long old = atomicCAS(&lab[u], cl, nl);
-            if (old == cl) break;
-            cl = old;
-          }
-          const uint32_t bit = 1u << (u & 31u);
-          if (nd < T) {
-            atomicOr(&nxt[u >> 5], bit);
-            atomicAnd(&far[u >> 5], ~bit);  // expanded from the near set instead
-            pushed_near = true;
-          } else {
-            atomicOr(&far[u >> 5], bit);
-            atomicMin(&s_min[mpar], nd);
-          }
-        };
+      }
+      if (c == 0) break;
+      uint2 rec[G][K];
+      unsigned long long lv[G];
 #pragma unroll
-        for (int j = 0; j < K; ++j) relax(rec[j], v * K + j);
-        const uint2 last = rec[K - 1];
+      for (int g = 0; g < G; ++g) {
+        if (g >= c) break;
+        load_recs<K>(a, vs[g], rec[g]);
+        lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unsigned long long cl[G][K];
+      bool ok[G][K];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
+          if (ok[g][j])
+            cl[g][j] = __hip_atomic_load(&lab[rec[g][j].x & ORH_REC_COL_MASK], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (g >= c) break;
+        const uint32_t v = vs[g];
+        if (v != s.node && (rec[g][0].x & ORH_REC_ROW_OVL)) continue;  // no transit
+        const uint32_t dv = static_cast<uint32_t>(lv[g] >> 32);
+        const uint32_t nhv = static_cast<uint32_t>(lv[g]);
+        const bool from_src = v == s.node;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          if (!ok[g][j]) continue;
+          const uint2 r = rec[g][j];
+          merge(r.x & ORH_REC_COL_MASK, dv + (a.use_link_metric ? r.y : 1u),
+                from_src ? (1u << a.rank_out[v * K + j]) : nhv, cl[g][j]);
+        }
+        const uint2 last = rec[g][K - 1];
         if (last.x & ORH_REC_CONT) {
           const uint32_t start = last.x & ORH_REC_COL_MASK;
-          for (uint32_t q = 0; q < last.y; ++q) relax(a.recs[start + q], start + q);
+          for (uint32_t q = 0; q < last.y; ++q) {
+            const uint2 r = a.recs[start + q];
+            if (!live(a, s, r, start + q)) continue;
+            const uint32_t u = r.x & ORH_REC_COL_MASK;
+            merge(u, dv + (a.use_link_metric ? r.y : 1u), from_src ? (1u << a.rank_out[start + q]) : nhv,
+                  __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          }
         }
       }
     }

@@ -17,6 +17,7 @@
 #include "../../include/openr_hip.h"
 #include "kernels/route_kernels.h"
 #include "kernels/spf_kernels.h"
+#include "kernels/whatif_kernels.h"
 
 struct orh_ctx {
   int device = 0;
@@ -29,12 +30,10 @@ struct orh_ctx {
   // 50 measured best on the C4 WAN what-if batch (25: 12.4, 50: 11.9,
   // 100: 13.1, 200: 17.0, 400: 23.6 ms; log-normal metrics, mean ~3x median)
   uint32_t delta_pct = 50;
-  uint32_t req_xcd_group = 0;  // HopArgs::xcd_group of the staged request
   orh_spf_info last_info{};    // orh_last_spf_info
   std::string err;
   orh_counters counters{};
-  // reusable device staging for request arrays, keyed by the request that
-  // filled it (a repeated sweep skips the host rebuild and the upload)
+  // reusable device staging for the exact kernel's request arrays
   uint32_t* d_req = nullptr;
   size_t d_req_cap = 0;
   std::vector<uint32_t> req_key;
@@ -63,6 +62,18 @@ struct orh_ctx {
   size_t d_exact_cap = 0;  // in bytes
   uint8_t* d_batch_x = nullptr;
   size_t d_batch_x_cap = 0;  // in bytes
+  // what-if repair: base rows of the batch's distinct sources, and the staged
+  // request (base row, source, ignore sets, cut records, fallback flags)
+  uint8_t* d_rep_base = nullptr;
+  size_t d_rep_base_cap = 0;  // in bytes
+  uint32_t* d_rep = nullptr;
+  size_t d_rep_cap = 0;  // in u32
+  std::vector<uint32_t> rep_key;
+  uint8_t* d_rep_slots = nullptr;  // global repair slots (requests that outgrow LDS)
+  size_t d_rep_slots_cap = 0;
+  // ORH_WHATIF_REPAIR: 0 off, 1 automatic (sources repeat, small ignore
+  // sets), 2 every ignore-set batch the repair can take
+  int repair_mode = 1;
 };
 
 struct orh_graph {
@@ -104,6 +115,18 @@ struct orh_graph {
   uint32_t* d_ms_dev_of = nullptr;
   uint32_t* d_ms_host_of = nullptr;
   std::vector<int32_t> row_of;  // scratch for orh_spf_run (all -1 between calls)
+  // orh_spf_run's staged request on this graph (sources, ignore sets,
+  // neighbour rows, batch order), keyed by the request: a repeated sweep
+  // neither rebuilds nor uploads it, even when several graphs share a context
+  uint32_t* d_req = nullptr;
+  size_t d_req_cap = 0;
+  std::vector<uint32_t> req_key;
+  uint32_t req_xcd_group = 0;  // HopArgs::xcd_group of the staged request
+  // what-if repair: per record, the record of the same link from the other
+  // end; per link, its two CSR entries (~0 when absent); valid for rev_gen
+  uint32_t* d_rev = nullptr;
+  uint64_t rev_gen = 0;
+  std::vector<uint32_t> link_ent;  // [2 * n_links]
 };
 
 namespace {
@@ -132,6 +155,13 @@ void free_graph_device(orh_graph* g) {
   (void)hipFree(g->d_ms_dev_of);
   (void)hipFree(g->d_ms_host_of);
   (void)hipFree(g->d_name_rank);
+  (void)hipFree(g->d_rev);
+  g->d_rev = nullptr;
+  (void)hipFree(g->d_req);
+  g->d_req = nullptr;
+  g->d_req_cap = 0;
+  g->req_key.clear();
+  g->rev_gen = 0;
   g->d_name_rank = nullptr;
   g->d_ms_recs = nullptr;
   g->d_ms_dev_of = nullptr;
@@ -382,6 +412,18 @@ int ensure_req(orh_ctx* ctx, size_t words) {
   return ORH_OK;
 }
 
+int ensure_graph_req(orh_graph* g, size_t words) {
+  if (words <= g->d_req_cap) return ORH_OK;
+  hipFree(g->d_req);
+  g->d_req = nullptr;
+  g->d_req_cap = 0;
+  g->req_key.clear();
+  const size_t cap = std::max<size_t>(words, 4096);
+  ORH_HIP(g->ctx, hipMalloc(&g->d_req, cap * sizeof(uint32_t)));
+  g->d_req_cap = cap;
+  return ORH_OK;
+}
+
 int ensure_lvl_rows(orh_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->d_lvl_rows_cap) return ORH_OK;
   hipFree(ctx->d_lvl_rows);
@@ -469,6 +511,7 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
   }
   if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % orh::kSpfModes);
   if (const char* e = getenv("ORH_DELTA_PCT")) ctx->delta_pct = std::max(1, atoi(e));
+  if (const char* e = getenv("ORH_WHATIF_REPAIR")) ctx->repair_mode = atoi(e);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
@@ -481,6 +524,12 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
 int orh_set_spf_mode(orh_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode >= orh::kSpfModes) return ORH_E_INVALID;
   ctx->spf_mode = static_cast<orh::SpfMode>(mode);
+  return ORH_OK;
+}
+
+int orh_set_repair_mode(orh_ctx* ctx, int mode) {
+  if (!ctx || mode < ORH_REPAIR_OFF || mode > ORH_REPAIR_ALWAYS) return ORH_E_INVALID;
+  ctx->repair_mode = mode;
   return ORH_OK;
 }
 
@@ -497,6 +546,9 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_patch);
   hipFree(ctx->d_exact);
   hipFree(ctx->d_batch_x);
+  hipFree(ctx->d_rep_base);
+  hipFree(ctx->d_rep);
+  hipFree(ctx->d_rep_slots);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -577,6 +629,7 @@ int orh_graph_destroy(orh_graph* g) {
   hipStreamSynchronize(g->ctx->stream);
   free_graph_device(g);
   g->ctx->req_key.clear();  // the staged request may describe this graph
+  g->ctx->rep_key.clear();
   delete g;
   return ORH_OK;
 }
@@ -927,6 +980,242 @@ static int run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, u
   return ORH_OK;
 }
 
+// ---- what-if repair (whatif_kernels.hip) ----------------------------------
+// per-record reverse records and per-link CSR entries of the current structure
+static int ensure_rev(orh_graph* g) {
+  if (g->d_rev && g->rev_gen == g->gen) return ORH_OK;
+  orh_ctx* ctx = g->ctx;
+  const uint32_t L = g->n_links;
+  g->link_ent.assign(2 * static_cast<size_t>(L), ~0u);
+  for (uint32_t e = 0; e < g->n_edges; ++e) {
+    if (g->meta[e] == ORH_META_EMPTY) continue;
+    const uint32_t l = g->meta[e] & ORH_META_LINK_MASK;
+    if (l >= L) continue;
+    uint32_t* ent = &g->link_ent[2 * static_cast<size_t>(l)];
+    (ent[0] == ~0u ? ent[0] : ent[1]) = e;
+  }
+  std::vector<uint32_t> rev(std::max<uint32_t>(g->n_recs, 1), 0u);
+  for (uint32_t e = 0; e < g->n_recs && e < rev.size(); ++e) rev[e] = e;
+  for (uint32_t l = 0; l < L; ++l) {
+    const uint32_t a = g->link_ent[2 * l], b = g->link_ent[2 * l + 1];
+    if (a == ~0u || b == ~0u) continue;
+    rev[g->pos[a]] = g->pos[b];
+    rev[g->pos[b]] = g->pos[a];
+  }
+  if (!g->d_rev) ORH_HIP(ctx, hipMalloc(&g->d_rev, rev.size() * sizeof(uint32_t)));
+  ORH_HIP(ctx, hipMemcpyAsync(g->d_rev, rev.data(), rev.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                              ctx->stream));
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // rev is a local
+  g->rev_gen = g->gen;
+  return ORH_OK;
+}
+
+constexpr uint32_t kRepairCapA = 1024, kRepairCapE = 4096;
+constexpr uint32_t kRepairSlots = 64;       // second pass: whole-graph state in global memory
+constexpr size_t kRepairSlotBudget = 1ull << 30;  // bytes for all slots
+constexpr uint32_t kRepairMaxIgnore = 8;  // link-failure sets; KSP2 k = 2 sets are whole paths
+
+// Can run_repair take this ignore-set batch? (sources repeat, small sets,
+// one mask word, the LDS state fits, and the fallback search has a plan)
+static bool repair_eligible(const orh_graph* g, const orh_spf_request* req, uint32_t words,
+                            uint64_t bound, bool uniform) {
+  const orh_ctx* ctx = g->ctx;
+  if (ctx->repair_mode == 0 || words != 1 || !req->h_ignore_ptr) return false;
+  if (orh::repair_lds_bytes(g->n_nodes, kRepairCapA, kRepairCapE) > ctx->lds_limit) return false;
+  const orh::SpfPlan fp = orh::plan_spf(g->n_nodes, uniform, bound, g->ell_k, ctx->lds_limit, false,
+                                        orh::SpfMode::kGlobal);
+  if (fp.variant == orh::SpfVariant::kUnsupported) return false;
+  if (ctx->repair_mode >= 2) return true;
+  for (uint32_t i = 0; i < req->n_src; ++i)
+    if (req->h_ignore_ptr[i + 1] - req->h_ignore_ptr[i] > kRepairMaxIgnore) return false;
+  std::vector<uint32_t> s(req->h_srcs, req->h_srcs + req->n_src);
+  std::sort(s.begin(), s.end());
+  const size_t m = static_cast<size_t>(std::unique(s.begin(), s.end()) - s.begin());
+  return 2 * m <= req->n_src;
+}
+
+// runSpf(src, useLinkMetric, ignore) for every request from the plain rows of
+// its source (one orh_spf_run over the distinct sources), then copy + repair;
+// requests the repair cannot hold in LDS are searched in full
+// (spf_global_nh_kernel with the fallback flags as row mask)
+static int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist, uint32_t* d_nh,
+                      uint64_t bound, bool uniform) {
+  orh_ctx* ctx = g->ctx;
+  const uint32_t N = g->n_nodes, n_src = req->n_src;
+  std::vector<uint32_t> base_srcs, base_row(n_src);
+  auto& ro = g->row_of;
+  for (uint32_t i = 0; i < n_src; ++i) {
+    const uint32_t s = req->h_srcs[i];
+    if (ro[s] < 0) {
+      ro[s] = static_cast<int32_t>(base_srcs.size());
+      base_srcs.push_back(s);
+    }
+    base_row[i] = static_cast<uint32_t>(ro[s]);
+  }
+  for (uint32_t s : base_srcs) ro[s] = -1;
+  const uint32_t m = static_cast<uint32_t>(base_srcs.size());
+  const size_t nd = static_cast<size_t>(m) * N;
+  int rc = ensure_bytes(ctx, &ctx->d_rep_base, &ctx->d_rep_base_cap, nd * 8);
+  if (rc) return rc;
+  uint32_t* base_dist = reinterpret_cast<uint32_t*>(ctx->d_rep_base);
+  uint32_t* base_nh = base_dist + nd;
+  rc = ensure_rev(g);
+  if (rc) return rc;
+  // the plain SPFs of the distinct sources (counted below as the batch's runs)
+  orh_spf_request br{};
+  br.h_srcs = base_srcs.data();
+  br.n_src = m;
+  br.use_link_metric = req->use_link_metric;
+  const orh_counters c0 = ctx->counters;
+  rc = orh_spf_run(g, &br, 1, base_dist, base_nh);
+  if (rc) return rc;
+  ctx->counters = c0;
+
+  // staging: base_row[n] | srcs[n] | ign_ptr[n+1] | ign[..] | cut_ptr[n+1] |
+  // flags[n] | (pad to 16 B) cuts uint4[..]
+  const uint32_t n_ign = req->h_ignore_ptr[n_src];
+  std::vector<uint32_t> key;
+  key.reserve(4 + 2 * n_src + 1 + n_ign);
+  const uint64_t gp = reinterpret_cast<uintptr_t>(g);
+  key.insert(key.end(), {static_cast<uint32_t>(gp), static_cast<uint32_t>(gp >> 32),
+                         static_cast<uint32_t>(g->gen), static_cast<uint32_t>(g->gen >> 32), n_src});
+  key.insert(key.end(), req->h_srcs, req->h_srcs + n_src);
+  key.insert(key.end(), req->h_ignore_ptr, req->h_ignore_ptr + n_src + 1);
+  key.insert(key.end(), req->h_ignore_links, req->h_ignore_links + n_ign);
+  size_t off_src = n_src, off_ip = 2 * size_t{n_src}, off_ign = off_ip + n_src + 1, off_cp = 0, off_flags = 0,
+         off_cuts = 0;
+  if (key != ctx->rep_key) {
+    std::vector<uint32_t> st(base_row);
+    st.insert(st.end(), req->h_srcs, req->h_srcs + n_src);
+    std::vector<uint32_t> ign_ptr(1, 0), ign, cut_ptr(1, 0), cuts;
+    for (uint32_t i = 0; i < n_src; ++i) {
+      std::vector<uint32_t> set(req->h_ignore_links + req->h_ignore_ptr[i],
+                                req->h_ignore_links + req->h_ignore_ptr[i + 1]);
+      std::sort(set.begin(), set.end());
+      set.erase(std::unique(set.begin(), set.end()), set.end());
+      ign.insert(ign.end(), set.begin(), set.end());
+      ign_ptr.push_back(static_cast<uint32_t>(ign.size()));
+      for (uint32_t l : set) {
+        if (l >= g->n_links) continue;
+        for (int k = 0; k < 2; ++k) {
+          const uint32_t e = g->link_ent[2 * static_cast<size_t>(l) + k];
+          if (e == ~0u) continue;
+          cuts.insert(cuts.end(), {row_of(g, e), g->col[e], g->pos[e], 0u});
+        }
+      }
+      cut_ptr.push_back(static_cast<uint32_t>(cuts.size() / 4));
+    }
+    st.insert(st.end(), ign_ptr.begin(), ign_ptr.end());
+    st.insert(st.end(), ign.begin(), ign.end());
+    off_cp = st.size();
+    st.insert(st.end(), cut_ptr.begin(), cut_ptr.end());
+    off_flags = st.size();
+    st.insert(st.end(), n_src + 1, 0u);  // flags, then the slot counter
+    while (st.size() % 4) st.push_back(0u);
+    off_cuts = st.size();
+    st.insert(st.end(), cuts.begin(), cuts.end());
+    st.push_back(0u);
+    while (st.size() % 4) st.push_back(0u);
+    if (st.size() > ctx->d_rep_cap) {
+      hipFree(ctx->d_rep);
+      ctx->d_rep = nullptr;
+      ctx->d_rep_cap = 0;
+      ctx->rep_key.clear();
+      ORH_HIP(ctx, hipMalloc(&ctx->d_rep, st.size() * sizeof(uint32_t)));
+      ctx->d_rep_cap = st.size();
+    }
+    ORH_HIP(ctx, hipMemcpyAsync(ctx->d_rep, st.data(), st.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // st is a local
+    key.insert(key.end(), {static_cast<uint32_t>(off_cp), static_cast<uint32_t>(off_flags),
+                           static_cast<uint32_t>(off_cuts)});
+    ctx->rep_key = std::move(key);
+  }
+  {
+    const auto& k = ctx->rep_key;
+    off_cp = k[k.size() - 3];
+    off_flags = k[k.size() - 2];
+    off_cuts = k[k.size() - 1];
+  }
+  uint32_t* flags = ctx->d_rep + off_flags;
+  ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
+  ORH_HIP(ctx, hipMemsetAsync(flags, 0, (n_src + 1) * sizeof(uint32_t), ctx->stream));
+  // global slots for the requests whose affected set outgrows LDS
+  const size_t slot_bytes = orh::repair_slot_bytes(N, g->n_recs);
+  const uint32_t n_slots = static_cast<uint32_t>(
+      std::min<size_t>(std::min<size_t>(kRepairSlots, n_src), kRepairSlotBudget / std::max<size_t>(slot_bytes, 1)));
+  if (n_slots) {
+    rc = ensure_bytes(ctx, &ctx->d_rep_slots, &ctx->d_rep_slots_cap, n_slots * slot_bytes);
+    if (rc) return rc;
+  }
+  orh::RepairArgs ra{};
+  ra.n_nodes = N;
+  ra.n_req = n_src;
+  ra.use_link_metric = req->use_link_metric;
+  ra.cap_a = kRepairCapA;
+  ra.cap_e = kRepairCapE;
+  ra.recs = g->d_recs;
+  ra.link = g->d_link;
+  ra.rank_out = g->d_rank_out;
+  ra.rev = g->d_rev;
+  ra.ovl = g->d_ovl;
+  ra.base_dist = base_dist;
+  ra.base_nh = base_nh;
+  ra.base_row = ctx->d_rep;
+  ra.srcs = ctx->d_rep + off_src;
+  ra.ign_ptr = ctx->d_rep + off_ip;
+  ra.ign = ctx->d_rep + off_ign;
+  ra.cut_ptr = ctx->d_rep + off_cp;
+  ra.cuts = reinterpret_cast<const uint4*>(ctx->d_rep + off_cuts);
+  ra.out_dist = d_dist;
+  ra.out_nh = d_nh;
+  ra.fallback = flags;
+  ra.slot_mem = ctx->d_rep_slots;
+  ra.slot_bytes = slot_bytes;
+  ra.n_slots = n_slots;
+  ra.slot_next = flags + n_src;
+  ra.n_recs = g->n_recs;
+  hipError_t e = orh::launch_repair(ra, g->ell_k, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch");
+  // fallback: the full HBM search for the flagged rows only
+  orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
+  fp.variant = orh::SpfVariant::kGlobalNh;
+  fp.block = 1024;  // only the flagged rows search; the rest exit at once
+  rc = ensure_labels(ctx, static_cast<size_t>(n_src) * N);
+  if (rc) return rc;
+  orh::SpfArgs a{};
+  a.n_nodes = N;
+  a.n_out = n_src;
+  a.recs = g->d_recs;
+  a.link = g->d_link;
+  a.srcs = ra.srcs;
+  a.ignore_ptr = ra.ign_ptr;
+  a.ignore_links = ra.ign;
+  a.use_link_metric = req->use_link_metric;
+  a.w0 = req->use_link_metric ? g->max_out : 1u;
+  a.delta = uniform ? a.w0
+                    : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                 static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+  a.out_dist = d_dist;
+  a.scratch = ctx->d_scratch;
+  a.labels = ctx->d_labels;
+  a.out_nh = d_nh;
+  a.words = 1;
+  a.rank_out = g->d_rank_out;
+  a.row_mask = flags;
+  e = orh::launch_spf(fp, a, n_src, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "what-if fallback launch");
+  ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  orh_spf_info info{};
+  info.variant = static_cast<int32_t>(orh::SpfVariant::kRepair);
+  info.rows = n_src;
+  info.batch_sources = m;
+  ctx->last_info = info;
+  ctx->counters.spf_runs += n_src;
+  ctx->counters.spf_launches += 1;
+  ctx->counters.last_kernel_ms = -1.0;
+  return ORH_OK;
+}
+
 // Phase 1 computes a distance row for every requested source and for every
 // distinct neighbour of one (the first-hop phase reads them). Without ignore
 // sets rows are shared by node: a neighbour that is itself requested reuses
@@ -962,6 +1251,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       : req->use_link_metric ? g->sum_max_metric / 2 + g->max_metric
                              : static_cast<uint64_t>(g->n_links) + 1;
   const bool has_ign = req->h_ignore_ptr != nullptr;
+  if (has_ign && ctx->spf_mode == orh::SpfMode::kAuto && max_nbr <= 32 &&
+      repair_eligible(g, req, words, bound, uniform)) {
+    hipSetDevice(ctx->device);
+    return run_repair(g, req, d_dist, d_nh, bound, uniform);
+  }
   const orh::SpfPlan plan =
       orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, !has_ign, ctx->spf_mode);
   if (plan.variant == orh::SpfVariant::kUnsupported)
@@ -988,7 +1282,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // staged layout: srcs[n_rows] | ign_ptr[n_rows+1] ign[..] | nbr_ptr[n_src+1] nbr_row[..]
   uint32_t n_rows = n_src;
   size_t off_ign_ptr = 0, off_ign = 0, off_nbr_ptr = 0, off_nbr_row = 0, off_order = 0;
-  if (key != ctx->req_key) {
+  if (key != g->req_key) {
     std::vector<uint32_t> srcs(req->h_srcs, req->h_srcs + n_src), nbr_ptr(n_src + 1, 0), nbr_row;
     std::vector<uint32_t> ign_ptr, ign;
     std::vector<uint32_t> row_owner;  // source index whose ignore set a row uses
@@ -1041,7 +1335,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
         sum += d;
         mx = std::max(mx, d);
       }
-      ctx->req_xcd_group = static_cast<uint64_t>(mx) * n_src <= 2 * sum ? 0u : 16u;
+      g->req_xcd_group = static_cast<uint64_t>(mx) * n_src <= 2 * sum ? 0u : 16u;
     }
     std::vector<uint32_t> staging;
     staging.reserve(srcs.size() + ign_ptr.size() + ign.size() + nbr_ptr.size() + nbr_row.size() + 1);
@@ -1069,9 +1363,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       });
       staging.insert(staging.end(), order.begin(), order.end());
     }
-    int rc = ensure_req(ctx, staging.size());
+    int rc = ensure_graph_req(g, staging.size());
     if (rc) return rc;
-    ORH_HIP(ctx, hipMemcpyAsync(ctx->d_req, staging.data(), staging.size() * 4,
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_req, staging.data(), staging.size() * 4,
                                 hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
     key.push_back(static_cast<uint32_t>(off_ign_ptr));
@@ -1080,10 +1374,10 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     key.push_back(static_cast<uint32_t>(off_nbr_row));
     key.push_back(static_cast<uint32_t>(off_order));
     key.push_back(n_rows);
-    ctx->req_key = std::move(key);
+    g->req_key = std::move(key);
   }
   {
-    const auto& k = ctx->req_key;
+    const auto& k = g->req_key;
     const size_t t = k.size();
     off_order = k[t - 2];
     off_ign_ptr = k[t - 6];
@@ -1120,6 +1414,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       (ctx->spf_mode == orh::SpfMode::kGlobal || n_rows > n_src)) {
     run_plan.variant = orh::SpfVariant::kGlobalNh;
     n_rows = n_src;
+    // few rows: wider workgroups (a big frontier phase is split over more
+    // threads; the rows do not fill the CUs anyway)
+    run_plan.block = n_src <= ctx->n_cu ? 1024u : n_src <= 2 * ctx->n_cu ? 512u : 256u;
     int rc = ensure_labels(ctx, static_cast<size_t>(n_src) * N);
     if (rc) return rc;
   }
@@ -1152,10 +1449,10 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     if (rc) return rc;
     a.lvl_rows = ctx->d_lvl_rows;
   }
-  a.order = ctx->d_req + off_order;
-  a.srcs = ctx->d_req + 1;
-  a.ignore_ptr = has_ign ? ctx->d_req + off_ign_ptr : nullptr;
-  a.ignore_links = has_ign ? ctx->d_req + off_ign : nullptr;
+  a.order = g->d_req + off_order;
+  a.srcs = g->d_req + 1;
+  a.ignore_ptr = has_ign ? g->d_req + off_ign_ptr : nullptr;
+  a.ignore_links = has_ign ? g->d_req + off_ign : nullptr;
   a.use_link_metric = req->use_link_metric;
   a.w0 = w0;
   // near/far width of the HBM kernel: the mean live metric (one BFS level
@@ -1183,9 +1480,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   h.ignore_ptr = a.ignore_ptr;
   h.ignore_links = a.ignore_links;
   h.use_link_metric = req->use_link_metric;
-  h.nbr_ptr = ctx->d_req + off_nbr_ptr;
-  h.xcd_group = ctx->req_xcd_group;
-  h.nbr_row = ctx->d_req + off_nbr_row;
+  h.nbr_ptr = g->d_req + off_nbr_ptr;
+  h.xcd_group = g->req_xcd_group;
+  h.nbr_row = g->d_req + off_nbr_row;
   h.dist = d_dist;
   h.scratch = ctx->d_scratch;
   h.out_nh = d_nh;
