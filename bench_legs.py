@@ -123,6 +123,12 @@ def leg_c4(hip, cpu, n_links=64, n_srcs=16, n_ksp=256):
         sweep.run()
     sweep.sync()
     dt = (time.perf_counter() - t0) / 3
+    sweep.run()
+    dev_ms = sweep.last_ms()  # HIP events around the base searches + repair
+    info = sweep.info()
+    n_nodes, n_edges = sweep.nodes, sweep.edges
+    # per what-if SPF the same B_spf as a plain source
+    b_spf = 4 * (n_nodes + 1) + 8 * n_edges + n_nodes * (4 + 4 * sweep.words)
     kp = c4_ksp2_pairs(names, n_ksp)
     t0 = time.perf_counter()
     ls.prefetch_kth_paths(kp)
@@ -131,6 +137,12 @@ def leg_c4(hip, cpu, n_links=64, n_srcs=16, n_ksp=256):
            "what_if_spfs_per_s": round(len(pairs) / dt, 1),
            "what_if_batch": f"{len(pairs)} runSpf(src, true, {{link}}) = {n_links} links x {n_srcs} sources",
            "what_if_batch_ms": round(dt * 1e3, 3),
+           "what_if_device_ms": round(dev_ms, 3),
+           "what_if_plan": (f"repair: {info['batch_sources']} plain SPFs, then copy + re-derive below "
+                            "the ignored link" if info["variant"] == 11 else f"variant {info['variant']}"),
+           "what_if_roofline": {"bound": "hbm", "bytes_per_spf": b_spf,
+                                "achieved_gbs": round(len(pairs) * b_spf / (dev_ms * 1e-3) / 1e9, 1),
+                                "frac": round(len(pairs) * b_spf / (dev_ms * 1e-3) / 1e9 / 8000.0, 4)},
            "ksp2_pairs_per_s": round(n_ksp / kdt, 1),
            "ksp2_batch": f"{n_ksp} (src, dst) getKthPaths k=1,2 (host trace + 2 device batches)"}
     if cpu:
