@@ -553,7 +553,21 @@ PYBIND11_MODULE(_openr_host, m) {
            })
       .def("get_spf_result",
            [](const LinkState& s, const std::string& n, bool useLinkMetric) {
-             return rowToDict(s, s.getSpfResult(n, useLinkMetric), true);
+             return rowToDict(s, s.getSpfRow(n, useLinkMetric), true);
+           },
+           py::arg("node"), py::arg("use_link_metric") = true)
+      .def("get_spf_result_ref",  // the reference-shaped SpfResult (LinkState::getSpfResult)
+           [](const LinkState& s, const std::string& n, bool useLinkMetric) {
+             py::dict d;
+             for (const auto& [name, r] : s.getSpfResult(n, useLinkMetric)) {
+               std::vector<std::string> nhs(r.nextHops().begin(), r.nextHops().end());
+               std::sort(nhs.begin(), nhs.end());
+               py::list pls;
+               for (const auto& pl : r.pathLinks())
+                 pls.append(py::make_tuple(linkDesc(s.link(pl.link)), pl.prevNode));
+               d[py::str(name)] = py::make_tuple(static_cast<uint64_t>(r.metric()), nhs, pls);
+             }
+             return d;
            },
            py::arg("node"), py::arg("use_link_metric") = true)
       .def("run_spf_ignoring",

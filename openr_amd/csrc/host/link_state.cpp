@@ -257,6 +257,7 @@ bool LinkState::updateNodeOverloaded(const std::string& n, bool o, Metric up, Me
 void LinkState::invalidate(bool topologyChanged) {
   if (topologyChanged) {
     spfResults_.clear();
+    spfMaps_.clear();
     kthPaths_.clear();
   }
 }
@@ -668,7 +669,7 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
   }
 }
 
-const SpfRow& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) const {
+const SpfRow& LinkState::getSpfRow(const std::string& node, bool useLinkMetric) const {
   auto key = std::make_pair(node, useLinkMetric);
   auto it = spfResults_.find(key);
   if (it != spfResults_.end()) return it->second;
@@ -684,6 +685,27 @@ const SpfRow& LinkState::getSpfResult(const std::string& node, bool useLinkMetri
     ++spfRuns_;
   }
   return spfResults_.emplace(key, std::move(row)).first->second;
+}
+
+const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMetric) const {
+  auto key = std::make_pair(node, useLinkMetric);
+  auto it = spfMaps_.find(key);
+  if (it != spfMaps_.end()) return it->second;
+  const SpfRow& row = getSpfRow(node, useLinkMetric);
+  SpfResult res;
+  if (!row.known) {
+    res.emplace(node, NodeSpfResult(0));  // only the source itself (LinkState.cpp:817-819)
+  } else {
+    res.reserve(row.n);
+    for (uint32_t v = 0; v < row.n; ++v) {
+      if (!row.reachable(v)) continue;
+      NodeSpfResult r(row.metric(v));
+      row.forEachNextHop(v, [&](uint32_t nb) { r.addNextHop(names_[nb]); });
+      for (const auto& [lid, prev] : pathLinks(row, v)) r.addPath(lid, names_[prev]);
+      res.emplace(names_[v], std::move(r));
+    }
+  }
+  return spfMaps_.emplace(key, std::move(res)).first->second;
 }
 
 SpfRow LinkState::runSpf(const std::string& node, bool useLinkMetric,
@@ -702,14 +724,14 @@ SpfRow LinkState::runSpf(const std::string& node, bool useLinkMetric,
 std::optional<Metric> LinkState::getMetricFromAToB(const std::string& a, const std::string& b,
                                                    bool useLinkMetric) const {
   if (a == b) return 0;  // LinkState.cpp:740-751
-  const SpfRow& row = getSpfResult(a, useLinkMetric);
+  const SpfRow& row = getSpfRow(a, useLinkMetric);
   auto id = nodeId(b);
   if (!id || !row.reachable(*id)) return std::nullopt;
   return row.metric(*id);
 }
 
 Metric LinkState::getMaxHopsToNode(const std::string& node) const {
-  const SpfRow& row = getSpfResult(node, false);  // LinkState.cpp:753-760
+  const SpfRow& row = getSpfRow(node, false);  // LinkState.cpp:753-760
   Metric mx = 0;
   if (!row.known) return 0;
   for (uint32_t v = 0; v < row.n; ++v)
@@ -793,7 +815,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
   SpfRow fresh;
   const SpfRow* row;
   if (ignore.empty()) {
-    row = &getSpfResult(src, true);
+    row = &getSpfRow(src, true);
   } else {
     std::vector<uint32_t> ign(ignore.begin(), ignore.end());
     fresh = runSpf(src, true, ign);

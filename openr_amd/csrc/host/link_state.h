@@ -139,6 +139,30 @@ struct SpfRow {
   }
 };
 
+// LinkState::NodeSpfResult (LinkState.h:203-256): metric, the first-hop
+// neighbour names and the (link, previous node) predecessors in the
+// reference's pathLinks order; links are named by their LinkState id
+// (LinkState::link(id)) instead of a shared_ptr<Link>
+class NodeSpfResult {
+ public:
+  struct PathLink {
+    uint32_t link;
+    std::string prevNode;
+  };
+  explicit NodeSpfResult(Metric m) : metric_(m) {}
+  Metric metric() const { return metric_; }
+  const std::vector<PathLink>& pathLinks() const { return pathLinks_; }
+  const std::unordered_set<std::string>& nextHops() const { return nextHops_; }
+  void addPath(uint32_t link, const std::string& prevNode) { pathLinks_.push_back({link, prevNode}); }
+  void addNextHop(const std::string& nh) { nextHops_.insert(nh); }
+
+ private:
+  Metric metric_;
+  std::vector<PathLink> pathLinks_;
+  std::unordered_set<std::string> nextHops_;
+};
+using SpfResult = std::unordered_map<std::string /* otherNodeName */, NodeSpfResult>;
+
 class LinkState {
  public:
   explicit LinkState(const std::string& area, orh_ctx* ctx = nullptr);
@@ -154,8 +178,13 @@ class LinkState {
   LinkStateChange decrementHolds();
   bool hasHolds() const;
 
-  // memoized SPF from `node` (LinkState.cpp:793-803)
-  const SpfRow& getSpfResult(const std::string& node, bool useLinkMetric = true) const;
+  // memoized SPF from `node` (LinkState.cpp:793-803) in the reference's
+  // shape: reachable node name -> {metric, nextHops, pathLinks}
+  // (LinkState.h:203-260, :271-272); built from the row on first use
+  const SpfResult& getSpfResult(const std::string& node, bool useLinkMetric = true) const;
+  // the same memoized SPF as the device row (dist + first-hop bitmask per
+  // node): what route building reads, without materialising names
+  const SpfRow& getSpfRow(const std::string& node, bool useLinkMetric = true) const;
   // fresh SPF with links ignored (runSpf(src, true, linksToIgnore))
   SpfRow runSpf(const std::string& node, bool useLinkMetric,
                 const std::vector<uint32_t>& ignoreLinks) const;
@@ -258,6 +287,7 @@ class LinkState {
 
   // memo (LinkState.h:279-301)
   mutable std::map<std::pair<std::string, bool>, SpfRow> spfResults_;
+  mutable std::map<std::pair<std::string, bool>, SpfResult> spfMaps_;  // getSpfResult views
   mutable std::map<std::tuple<std::string, std::string, size_t>, std::vector<Path>> kthPaths_;
   mutable uint64_t spfRuns_{0};
 };

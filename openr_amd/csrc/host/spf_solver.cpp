@@ -231,7 +231,7 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
   const PrefixEntries* ep = &search->second;
   PrefixEntries kept;
   for (const auto& [area, ls] : als) {
-    const SpfRow& row = ls.getSpfResult(me);
+    const SpfRow& row = ls.getSpfRow(me);
     for (auto it = ep->begin(); it != ep->end();) {
       if (area != it->first.second || rowHas(ls, row, it->first.first)) {
         ++it;
@@ -366,7 +366,7 @@ bool SpfSolver::fastSpEcmp(const std::string& me, const LinkState& ls, const std
   // and non-per-destination forwarding (Decision.cpp:1152-1334) on the row:
   // min over advertisers, OR of first-hop masks, then my links whose metric
   // equals the distance to their neighbour.
-  const SpfRow& row = ls.getSpfResult(me);
+  const SpfRow& row = ls.getSpfRow(me);
   Metric shortest = std::numeric_limits<Metric>::max();
   std::vector<uint32_t> mask(row.words, 0u);
   bool any = false;
@@ -410,7 +410,7 @@ std::pair<Metric, SpfSolver::NhMap> SpfSolver::getNextHopsWithMetric(
   NhMap nhs;
   Metric shortest = std::numeric_limits<Metric>::max();
   for (const auto& [area, ls] : als) {
-    const SpfRow& row = ls.getSpfResult(me);
+    const SpfRow& row = ls.getSpfRow(me);
     Metric areaMin = std::numeric_limits<Metric>::max();
     std::vector<std::string> minNodes;
     for (const auto& [dst, _] : dsts) {  // getMinCostNodes: area ignored
@@ -639,7 +639,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   if (selCtx_ && selCtx_ != ctx) return false;
   // the kernel reads u32 distance rows: path metrics past 32 bits stay on the host
   for (const auto& [_, ls] : als)
-    if (ls.getSpfResult(me).known && !ls.getSpfResult(me).dist64.empty()) return false;
+    if (ls.getSpfRow(me).known && !ls.getSpfRow(me).dist64.empty()) return false;
   // getNextHopsWithMetric keys nexthops by neighbour name only (:1221): a
   // neighbour name shared by two areas couples their links, keep those
   // topologies on the host path
@@ -677,7 +677,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     const LinkState* ls = order[a];
     if (!ls) continue;
     sel[a].present = 1;
-    const SpfRow& row = ls->getSpfResult(me);
+    const SpfRow& row = ls->getSpfRow(me);
     orh_graph* g = ls->deviceGraph();
     if (!row.known) continue;  // me's SpfResult holds only me: nothing reachable
     const uint32_t N = row.n;
@@ -862,7 +862,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // found paths in other areas may still trace lazily, so their presence
   // keeps the loop sequential.
   prof.mark("ksp2 plan");
-  for (const auto& [_, ls] : als) ls.getSpfResult(me);
+  for (const auto& [_, ls] : als) ls.getSpfRow(me);
   prof.mark("spf(me)");
   DecisionRouteDb db;
   if (ps.prefixes().size() < kParallelMin) db.unicastRoutes.reserve(ps.prefixes().size());
@@ -905,7 +905,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
         if (w.ls == &als.begin()->second && w.words) tw = &w;
     if (!hasKsp && tw && shardWorld_ == 1 && n >= kParallelMin && pool.size() > 1) {
       const auto& [area, ls] = *als.begin();
-      const SpfRow& myRow = ls.getSpfResult(me);
+      const SpfRow& myRow = ls.getSpfRow(me);
       std::vector<const AdjacencyDatabase*> dbs;
       dbs.reserve(ls.getAdjacencyDatabases().size());
       for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
@@ -1054,7 +1054,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     if (dev && als.size() == 1)
       for (const auto& w : areaWork_)
         if (w.ls == &ls && w.words) tw = &w;
-    const SpfRow* myRow = tw ? &ls.getSpfResult(me) : nullptr;
+    const SpfRow* myRow = tw ? &ls.getSpfRow(me) : nullptr;
     auto compute = [&, &area = area, &ls = ls](size_t i) {
       const AdjacencyDatabase& adjDb = *dbs[i];
       const int32_t label = adjDb.nodeLabel;
