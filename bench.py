@@ -238,7 +238,14 @@ def main():
                      "algorithmic_bytes_per_source": bytes_per_source,
                      "sources_per_launch": srcs_probe,
                      "output_floor": {"bytes": out_bytes,
-                                      "frac": round(out_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+                                      "frac": round(out_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                     # the timed region as a whole: every sweep's algorithmic
+                     # bytes over the wall time of a step (overlapping lanes)
+                     "step": {"achieved": round(bytes_per_source * total_units / world / (ms_per_step * 1e-3) / 1e9, 1),
+                              "frac": round(bytes_per_source * total_units / world / (ms_per_step * 1e-3) / 1e9
+                                            / HBM_PEAK_GBS, 4),
+                              "note": "per-GPU algorithmic bytes of one step / ms_per_step; 'achieved' above "
+                                      "is one sweep launch alone (HIP events), as rocprof's kernel averages"}},
     }
 
     if not args.no_route_db and base is not None:

@@ -12,5 +12,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$REPO/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-route-db --legs '' > "$OUT/trace.log" 2>&1
+  python3 "$REPO/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-route-db --legs '' --topologies 1 --lanes 1 > "$OUT/trace.log" 2>&1
 echo "gpu_round $TAG done"
