@@ -1,0 +1,230 @@
+// Decision::processPublication over the drop-in LinkState / PrefixState; see
+// decision_ingest.h.
+#include "decision_ingest.h"
+
+#include <arpa/inet.h>
+
+#include <algorithm>
+#include <regex>
+
+#include "thrift_compact.h"
+
+namespace openr_amd {
+
+namespace {
+
+using compact::Reader;
+using compact::Type;
+using compact::Writer;
+
+constexpr const char* kAdjDbMarker = "adj:";        // Constants.h:209
+constexpr const char* kPrefixDbMarker = "prefix:";  // Constants.h:210
+constexpr const char* kFibTimeMarker = "fibtime:";  // Constants.h:212
+
+bool startsWith(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+KvValue readValue(Reader& r) {  // Types.thrift:555-605
+  KvValue v;
+  r.structBegin();
+  int16_t id;
+  Type t;
+  while (r.field(&id, &t)) {
+    switch (id) {
+      case 1: v.version = r.i64(); break;
+      case 3: v.originatorId = r.binary(); break;
+      case 2: v.value = r.binary(); break;
+      case 4: v.ttl = r.i64(); break;
+      case 5: v.ttlVersion = r.i64(); break;
+      case 6: v.hash = r.i64(); break;
+      default: r.skip(t);
+    }
+  }
+  r.structEnd();
+  return v;
+}
+
+void writeValue(Writer& w, const KvValue& v) {
+  w.structBegin();
+  w.fieldI64(1, v.version);
+  if (v.value) w.fieldBinary(2, *v.value);
+  w.fieldBinary(3, v.originatorId);
+  w.fieldI64(4, v.ttl);
+  w.fieldI64(5, v.ttlVersion);
+  if (v.hash) w.fieldI64(6, *v.hash);
+  w.structEnd();
+}
+
+// the CIDR of text "<addr>/<len>", masked like folly::IPAddress::createNetwork
+std::optional<Cidr> parseCidr(const std::string& ip, int len) {
+  unsigned char buf[16];
+  size_t n = 0;
+  if (inet_pton(AF_INET, ip.c_str(), buf) == 1) n = 4;
+  else if (inet_pton(AF_INET6, ip.c_str(), buf) == 1) n = 16;
+  else return std::nullopt;
+  if (len < 0 || len > static_cast<int>(8 * n)) return std::nullopt;
+  for (size_t i = 0; i < n; ++i) {
+    const int keep = std::clamp(len - static_cast<int>(8 * i), 0, 8);
+    buf[i] &= static_cast<unsigned char>(0xFF00u >> keep);
+  }
+  return Cidr{AddrBytes(reinterpret_cast<const char*>(buf), n), len};
+}
+
+}  // namespace
+
+Publication publicationFromCompact(const std::string& bytes) {
+  Reader r(bytes);
+  Publication p;
+  r.structBegin();
+  int16_t id;
+  Type t;
+  while (r.field(&id, &t)) {
+    if (id == 2 && t == compact::kMap) {  // KeyVals = map<string, Value>
+      Type kt, vt;
+      uint32_t n;
+      r.mapBegin(&kt, &vt, &n);
+      if (n && (kt != compact::kBinary || vt != compact::kStruct))
+        throw std::invalid_argument("compact: keyVals is not map<string, Value>");
+      p.keyVals.reserve(n);
+      for (uint32_t i = 0; i < n; ++i) {
+        std::string key = r.binary();
+        p.keyVals[std::move(key)] = readValue(r);
+      }
+    } else if (id == 3 && t == compact::kList) {
+      Type e;
+      uint32_t n;
+      r.listBegin(&e, &n);
+      if (n && e != compact::kBinary) throw std::invalid_argument("compact: expiredKeys is not list<string>");
+      for (uint32_t i = 0; i < n; ++i) p.expiredKeys.push_back(r.binary());
+    } else if (id == 7 && t == compact::kBinary) {
+      p.area = r.binary();
+    } else {
+      r.skip(t);
+    }
+  }
+  r.structEnd();
+  return p;
+}
+
+std::string publicationToCompact(const Publication& pub) {
+  Writer w;
+  w.structBegin();
+  std::vector<const std::pair<const std::string, KvValue>*> kv;
+  for (const auto& x : pub.keyVals) kv.push_back(&x);
+  std::sort(kv.begin(), kv.end(), [](auto* a, auto* b) { return a->first < b->first; });
+  w.field(2, compact::kMap);
+  w.mapBegin(compact::kBinary, compact::kStruct, kv.size());
+  for (const auto* x : kv) {
+    w.binary(x->first);
+    writeValue(w, x->second);
+  }
+  w.field(3, compact::kList);
+  w.listBegin(compact::kBinary, pub.expiredKeys.size());
+  for (const auto& k : pub.expiredKeys) w.binary(k);
+  w.fieldBinary(7, pub.area);
+  w.structEnd();
+  return w.take();
+}
+
+std::optional<PrefixKeyParts> parsePrefixKey(const std::string& key) {
+  // getPrefixRE2 (Types.h:354-362)
+  static const std::regex re(
+      R"(prefix:([a-zA-Z\d\.\-\_]+):([a-zA-Z0-9\.\_\-]+):\[([a-fA-F\d\.\:]+)/(\d{1,3})\])");
+  std::smatch m;
+  if (!std::regex_match(key, m, re)) return std::nullopt;
+  auto cidr = parseCidr(m[3].str(), std::stoi(m[4].str()));
+  if (!cidr) return std::nullopt;
+  return PrefixKeyParts{m[1].str(), m[2].str(), *cidr};
+}
+
+std::string nodeNameFromKey(const std::string& key) {
+  const size_t a = key.find(':');
+  if (a == std::string::npos) return "";
+  const size_t b = key.find(':', a + 1);
+  return key.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
+}
+
+void processPublication(const Publication& pub, const std::string& me, bool orderedFib,
+                        AreaLinkStates& areaLinkStates, PrefixState& prefixState,
+                        DecisionPendingUpdates& pending,
+                        std::unordered_map<std::string, int64_t>& fibTimes, IngestStats& stats,
+                        unsigned lane) {
+  if (pub.area.empty()) throw std::invalid_argument("processPublication: empty area");  // CHECK
+  const std::string& area = pub.area;
+  if (!areaLinkStates.count(area))
+    areaLinkStates.emplace(std::piecewise_construct, std::forward_as_tuple(area),
+                           std::forward_as_tuple(area, laneContext(lane)));
+  LinkState& ls = areaLinkStates.at(area);
+  if (pub.keyVals.empty() && pub.expiredKeys.empty()) return;
+
+  // LSDB addition / update (Decision.cpp:1697-1790)
+  for (const auto& [key, val] : pub.keyVals) {
+    if (!val.value) {  // TTL refresh
+      ++stats.ttlRefreshes;
+      continue;
+    }
+    try {
+      if (startsWith(key, kAdjDbMarker)) {
+        AdjacencyDatabase db = compact::adjacencyDatabase(*val.value);
+        db.area = area;  // Decision.cpp:1712-1714
+        Metric up = 0, down = 0;
+        if (orderedFib) {  // :1715-1723
+          if (auto hops = ls.getMetricFromAToB(me, db.thisNodeName, false)) {
+            up = *hops;
+            down = ls.getMaxHopsToNode(db.thisNodeName) - up;
+          }
+        }
+        ++stats.adjDbUpdates;
+        const std::string node = db.thisNodeName;
+        pending.applyLinkStateChange(node, ls.updateAdjacencyDatabase(db, up, down));
+        continue;
+      }
+      if (startsWith(key, kPrefixDbMarker)) {
+        compact::PrefixDatabase db = compact::prefixDatabase(*val.value);
+        if (db.prefixEntries.size() != 1) {  // :1740-1745
+          ++stats.errors;
+          continue;
+        }
+        const PrefixEntry& e = db.prefixEntries.front();
+        const auto& areaStack = db.areaStacks.front();
+        // self-redistributed route reflection (:1747-1756)
+        if (db.thisNodeName == me && !areaStack.empty() && areaLinkStates.count(areaStack.back()))
+          continue;
+        ++stats.prefixDbUpdates;
+        pending.applyPrefixStateChange(db.deletePrefix
+                                           ? prefixState.deletePrefix(db.thisNodeName, area, Cidr{e.addr, e.len})
+                                           : prefixState.updatePrefix(db.thisNodeName, area, e));
+        continue;
+      }
+      if (startsWith(key, kFibTimeMarker)) {
+        try {
+          fibTimes[nodeNameFromKey(key)] = std::stoll(*val.value);
+        } catch (...) {
+          ++stats.errors;
+        }
+        continue;
+      }
+    } catch (const std::exception&) {
+      ++stats.errors;  // "Failed to deserialize info for key" (:1785-1788)
+    }
+  }
+
+  // LSDB deletion (:1792-1823)
+  for (const auto& key : pub.expiredKeys) {
+    const std::string node = nodeNameFromKey(key);
+    if (startsWith(key, kAdjDbMarker)) {
+      pending.applyLinkStateChange(node, ls.deleteAdjacencyDatabase(node));
+      continue;
+    }
+    if (startsWith(key, kPrefixDbMarker)) {
+      auto pk = parsePrefixKey(key);
+      if (!pk) {
+        ++stats.errors;
+        continue;
+      }
+      pending.applyPrefixStateChange(prefixState.deletePrefix(pk->node, area, pk->prefix));
+      continue;
+    }
+  }
+}
+
+}  // namespace openr_amd

@@ -12,6 +12,8 @@
 #include "parallel.h"
 #include "rib_policy.h"
 #include "spf_solver.h"
+#include "decision_ingest.h"
+#include "thrift_compact.h"
 
 namespace py = pybind11;
 using namespace openr_amd;
@@ -265,6 +267,15 @@ py::dict rowToDict(const LinkState& ls, const SpfRow& row, bool withPaths) {
     d[py::str(ls.nodeName(v))] = py::make_tuple(static_cast<uint64_t>(row.metric(v)), nhs, pls);
   }
   return d;
+}
+
+py::tuple adjDbToWire(const AdjacencyDatabase& db) {
+  py::list adjs;
+  for (const auto& a : db.adjacencies)
+    adjs.append(py::make_tuple(a.otherNodeName, a.ifName, pyBytes(a.nextHopV6.addr), pyBytes(a.nextHopV4.addr),
+                               a.metric, a.adjLabel, a.isOverloaded, a.rtt, a.timestamp, a.weight,
+                               a.otherIfName));
+  return py::make_tuple(db.thisNodeName, db.isOverloaded, adjs, db.nodeLabel, db.area);
 }
 
 struct AreaMap {
@@ -750,6 +761,57 @@ PYBIND11_MODULE(_openr_host, m) {
       .def_property_readonly("sources", &SpfSweep::sources);
 
   // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
+  // ---- thrift Compact wire -----------------------
+  m.def("route_db_thrift", [](py::tuple db, const std::string& node) {  // DecisionRouteDb::toThrift
+    return py::bytes(compact::routeDatabase(routeDbFromWire(db), node));
+  });
+  m.def("route_delta_thrift", [](py::tuple old_db, py::tuple new_db) {  // calculateUpdate -> toThrift
+    return py::bytes(compact::routeDatabaseDelta(routeDbFromWire(old_db).calculateUpdate(routeDbFromWire(new_db))));
+  });
+  m.def("adj_db_to_compact", [](py::tuple db) { return py::bytes(compact::adjacencyDatabaseBytes(adjDbFromWire(db))); });
+  m.def("adj_db_from_compact", [](py::bytes b) { return adjDbToWire(compact::adjacencyDatabase(std::string(b))); });
+  m.def("prefix_db_to_compact",
+        [](const std::string& node, const std::string& area, std::vector<py::tuple> entries, bool del,
+           std::vector<std::vector<std::string>> areaStacks) {
+          compact::PrefixDatabase db;
+          db.thisNodeName = node;
+          db.area = area;
+          db.deletePrefix = del;
+          for (auto& e : entries) db.prefixEntries.push_back(entryFromWire(e));
+          db.areaStacks = std::move(areaStacks);
+          return py::bytes(compact::prefixDatabaseBytes(db));
+        },
+        py::arg("node"), py::arg("area"), py::arg("entries"), py::arg("delete_prefix") = false,
+        py::arg("area_stacks") = std::vector<std::vector<std::string>>{});
+  m.def("prefix_db_from_compact", [](py::bytes b) {
+    const auto db = compact::prefixDatabase(std::string(b));
+    py::list entries;
+    for (const auto& e : db.prefixEntries) entries.append(entryToWire(e));
+    return py::make_tuple(db.thisNodeName, db.area, entries, db.deletePrefix, db.areaStacks);
+  });
+  // publication: {key: (version, originatorId, value bytes | None, ttl, ttlVersion)}
+  m.def("publication_to_compact", [](const std::string& area, py::dict keyVals, std::vector<std::string> expired) {
+    Publication p;
+    p.area = area;
+    p.expiredKeys = std::move(expired);
+    for (auto kv : keyVals) {
+      auto t = kv.second.cast<py::tuple>();
+      KvValue v;
+      v.version = t[0].cast<int64_t>();
+      v.originatorId = str(t[1]);
+      if (!t[2].is_none()) v.value = std::string(t[2].cast<py::bytes>());
+      v.ttl = t[3].cast<int64_t>();
+      v.ttlVersion = t[4].cast<int64_t>();
+      p.keyVals[str(kv.first)] = std::move(v);
+    }
+    return py::bytes(publicationToCompact(p));
+  });
+  m.def("parse_prefix_key", [](const std::string& key) -> py::object {  // PrefixKey::fromStr
+    auto k = parsePrefixKey(key);
+    if (!k) return py::none();
+    return py::make_tuple(k->node, k->area, pyBytes(k->prefix.first), k->prefix.second);
+  });
+
   m.def("calculate_update", [](py::tuple old_db, py::tuple new_db) {
     return deltaToWire(routeDbFromWire(old_db).calculateUpdate(routeDbFromWire(new_db)));
   });
@@ -781,6 +843,43 @@ PYBIND11_MODULE(_openr_host, m) {
         std::vector<std::string> v;
         for (const auto& kv : a.m) v.push_back(kv.first);
         return v;
+      });
+
+  // Decision::processPublication state: pending updates, fib times, counters
+  struct Ingest {
+    std::string me;
+    bool orderedFib;
+    DecisionPendingUpdates pending;
+    std::unordered_map<std::string, int64_t> fibTimes;
+    IngestStats stats;
+    Ingest(const std::string& n, bool o) : me(n), orderedFib(o), pending(n) {}
+  };
+  py::class_<Ingest>(m, "DecisionIngest")
+      .def(py::init<const std::string&, bool>(), py::arg("my_node"), py::arg("ordered_fib") = false)
+      .def("process_publication",  // thrift::Publication in Compact bytes
+           [](Ingest& g, py::bytes pub, AreaMap& als, PrefixState& ps) {
+             processPublication(publicationFromCompact(std::string(pub)), g.me, g.orderedFib, als.m, ps,
+                                g.pending, g.fibTimes, g.stats, als.lane);
+           })
+      .def("pending", [](const Ingest& g) {
+        py::list pfx;
+        for (const auto& c : g.pending.updatedPrefixes()) pfx.append(py::make_tuple(pyBytes(c.first), c.second));
+        py::dict d;
+        d["needs_full_rebuild"] = g.pending.needsFullRebuild();
+        d["needs_route_update"] = g.pending.needsRouteUpdate();
+        d["updated_prefixes"] = pfx;
+        d["count"] = g.pending.count();
+        return d;
+      })
+      .def("reset", [](Ingest& g) { g.pending.reset(); })
+      .def("fib_times", [](const Ingest& g) { return g.fibTimes; })
+      .def("stats", [](const Ingest& g) {
+        py::dict d;
+        d["adj_db_update"] = g.stats.adjDbUpdates;
+        d["prefix_db_update"] = g.stats.prefixDbUpdates;
+        d["error"] = g.stats.errors;
+        d["ttl_refresh"] = g.stats.ttlRefreshes;
+        return d;
       });
 
   py::class_<PrefixState>(m, "PrefixState")
@@ -821,6 +920,12 @@ PYBIND11_MODULE(_openr_host, m) {
              auto db = s.buildRouteDb(me, als.m, ps);
              if (!db) return py::none();
              return routeDbToWire(*db);
+           })
+      .def("build_route_db_thrift",  // thrift::RouteDatabase in Compact bytes (canonical order)
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps) -> py::object {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             if (!db) return py::none();
+             return py::bytes(compact::routeDatabase(*db, me));
            })
       .def("build_route_db_digest",
            [](SpfSolver& s, const std::string& me, const AreaMap& als,
