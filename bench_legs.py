@@ -192,10 +192,13 @@ def leg_c5(hip, cpu):
         als[a].update_adjacency_database(db)
     upd_s = time.perf_counter() - t0
     t0 = time.perf_counter()
-    solver._impl.time_build_route_db("me", als._impl, ps._impl)
+    rebuild_s, _ = solver._impl.time_build_route_db("me", als._impl, ps._impl)
     out["incremental"] = {"updates": "10k prefix add/withdraw + 100 adjacency metric changes",
                           "apply_s": round(upd_s, 3),
-                          "rebuild_ms": round((time.perf_counter() - t0) * 1e3, 2)}
+                          "rebuild_ms": round(rebuild_s * 1e3, 2),
+                          # + freeing the returned 1M-route DB (glibc), outside the reference's
+                          # route_build_ms too
+                          "rebuild_wall_ms": round((time.perf_counter() - t0) * 1e3, 2)}
     policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
         0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
     build_s, policy_s, routes, updated = solver._impl.time_build_route_db_with_policy(
