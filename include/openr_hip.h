@@ -230,6 +230,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
 /* synchronous convenience form: results copied into host buffers */
 int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32_t* h_dist,
                   uint32_t* h_nh);
+/* orh_spf_batch into context-owned pinned host memory: *h_dist / *h_nh point
+ * at n_src rows of dist / n_src * N * words masks, valid until the next call
+ * on this context (no pageable bounce copy, no caller allocation) */
+int orh_spf_batch_pinned(orh_graph* g, const orh_spf_request* req, uint32_t words,
+                         const uint32_t** h_dist, const uint32_t** h_nh);
 
 /* Exact SPF: LinkState::runSpf (LinkState.cpp:808-882) in the reference's own
  * extraction order, with 64-bit path metrics (LinkStateMetric = uint64_t,

@@ -1,6 +1,8 @@
 // Drop-in LinkState over libopenr_hip (see link_state.h).
 #include "link_state.h"
 
+#include "parallel.h"
+
 #include <set>
 
 #include <algorithm>
@@ -531,11 +533,12 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
   check(ctx_, orh_spf_words(graph_, srcIds.data(), n, &words), "orh_spf_words");
   check(ctx_, orh_graph_flags(graph_, &flags), "orh_graph_flags");
   const size_t nd = static_cast<size_t>(n) * N;
-  std::vector<uint32_t> dist, nh(nd * words), order;
+  std::vector<uint32_t> nh, order;
   std::vector<uint64_t> dist64;
   // zero-metric links / 64-bit path metrics: the reference's extraction order
   // decides the first hops and the pathLinks order (LinkState.cpp:808-882)
   const bool exact = useLinkMetric && flags != 0;
+  if (exact) nh.resize(nd * words);
   const bool wide = useLinkMetric && (flags & ORH_GRAPH_WIDE_METRIC);
   if (exact) {
     dist64.resize(nd);
@@ -543,8 +546,18 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
     check(ctx_, orh_spf_batch_exact(graph_, &req, words, dist64.data(), nh.data(), order.data()),
           "orh_spf_batch_exact");
   } else {
-    dist.resize(nd);
-    check(ctx_, orh_spf_batch(graph_, &req, words, dist.data(), nh.data()), "orh_spf_batch");
+    // rows land in the context's pinned buffer; copied out per row below
+    const uint32_t *hd = nullptr, *hn = nullptr;
+    check(ctx_, orh_spf_batch_pinned(graph_, &req, words, &hd, &hn), "orh_spf_batch_pinned");
+    auto fill = [&](size_t, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        const size_t b = i * N;
+        rows[i].dist.assign(hd + b, hd + b + N);
+        rows[i].nh.assign(hn + b * words, hn + (b + N) * words);
+      }
+    };
+    if (n > 1) WorkerPool::instance().parallelFor(n, fill);
+    else fill(0, 0, n);
   }
   for (uint32_t i = 0; i < n; ++i) {
     SpfRow& row = rows[i];
@@ -557,7 +570,7 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
     row.words = words;
     row.n = N;
     if (!exact) {
-      row.dist.assign(dist.begin() + b, dist.begin() + b + N);
+      // filled from the pinned rows above
     } else if (wide) {
       row.dist64.assign(dist64.begin() + b, dist64.begin() + b + N);
     } else {  // path metrics < 2^32 - 1: the u32 row (route selection reads it)
@@ -565,8 +578,10 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
       for (uint32_t v = 0; v < N; ++v)
         row.dist[v] = dist64[b + v] == ~0ull ? ORH_UNREACHABLE : static_cast<uint32_t>(dist64[b + v]);
     }
-    if (exact) row.order.assign(order.begin() + b, order.begin() + b + N);
-    row.nh.assign(nh.begin() + b * words, nh.begin() + (b + N) * words);
+    if (exact) {
+      row.order.assign(order.begin() + b, order.begin() + b + N);
+      row.nh.assign(nh.begin() + b * words, nh.begin() + (b + N) * words);
+    }
     uint32_t nn = 0;
     check(ctx_, orh_graph_neighbors(graph_, src, nullptr, 0, &nn), "orh_graph_neighbors");
     row.nbrs.resize(nn);

@@ -71,6 +71,8 @@ struct orh_ctx {
   std::vector<uint32_t> rep_key;
   uint8_t* d_rep_slots = nullptr;  // global repair slots (requests that outgrow LDS)
   size_t d_rep_slots_cap = 0;
+  uint32_t* h_pinned = nullptr;  // orh_spf_batch_pinned's host rows (hipHostMalloc)
+  size_t h_pinned_cap = 0;       // in u32
   // ORH_WHATIF_REPAIR: 0 off, 1 automatic (sources repeat, small ignore
   // sets), 2 every ignore-set batch the repair can take
   int repair_mode = 1;
@@ -549,6 +551,7 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_rep_base);
   hipFree(ctx->d_rep);
   hipFree(ctx->d_rep_slots);
+  if (ctx->h_pinned) hipHostFree(ctx->h_pinned);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
@@ -1601,6 +1604,47 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
     }
   }
   return rc;
+}
+
+int orh_spf_batch_pinned(orh_graph* g, const orh_spf_request* req, uint32_t words,
+                         const uint32_t** h_dist, const uint32_t** h_nh) {
+  if (!g || !req || !h_dist || !h_nh) return ORH_E_INVALID;
+  orh_ctx* ctx = g->ctx;
+  *h_dist = *h_nh = nullptr;
+  if (req->n_src == 0) return ORH_OK;
+  const size_t nd = static_cast<size_t>(req->n_src) * g->n_nodes;
+  hipSetDevice(ctx->device);
+  if (nd * (1 + words) > ctx->d_batch_cap) {
+    hipFree(ctx->d_batch);
+    ctx->d_batch = nullptr;
+    ctx->d_batch_cap = 0;
+    if (hipMalloc(&ctx->d_batch, nd * (1 + words) * 4) != hipSuccess)
+      return fail(ctx, ORH_E_NOMEM, "orh_spf_batch_pinned: device allocation failed");
+    ctx->d_batch_cap = nd * (1 + words);
+  }
+  if (nd * (1 + words) > ctx->h_pinned_cap) {
+    if (ctx->h_pinned) hipHostFree(ctx->h_pinned);
+    ctx->h_pinned = nullptr;
+    ctx->h_pinned_cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pinned), nd * (1 + words) * 4, hipHostMallocDefault) !=
+        hipSuccess)
+      return fail(ctx, ORH_E_NOMEM, "orh_spf_batch_pinned: pinned host allocation failed");
+    ctx->h_pinned_cap = nd * (1 + words);
+  }
+  int rc = orh_spf_run(g, req, words, ctx->d_batch, ctx->d_batch + nd);
+  if (rc != ORH_OK) return rc;
+  hipError_t e = hipMemcpyAsync(ctx->h_pinned, ctx->d_batch, nd * (1 + words) * 4, hipMemcpyDeviceToHost,
+                                ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "orh_spf_batch_pinned: copy-out");
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess) {
+    ctx->counters.last_kernel_ms = ms;
+    ctx->counters.total_kernel_ms += ms;
+  }
+  *h_dist = ctx->h_pinned;
+  *h_nh = ctx->h_pinned + nd;
+  return ORH_OK;
 }
 
 int orh_spf_run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, uint64_t* d_dist,
