@@ -43,7 +43,8 @@
 namespace orh {
 namespace {
 
-constexpr uint32_t kRepBlock = 256;
+constexpr uint32_t kRepBlock = 256;    // LDS pass: small state, several requests per CU
+constexpr uint32_t kSlotBlock = 1024;  // slot pass: few large affected sets, one per CU
 constexpr uint32_t kInfD = 0xFFFFFFFFu;
 constexpr unsigned long long kInfLab = 0xFFFFFFFF00000000ull;  // {dist = inf, mask = 0}
 
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t
 // sized for the whole graph (A <= N, edges <= records), so the repair itself
 // cannot overflow; when the slots run out the flag stays for the full search
 template <int K, bool kSlot>
-__global__ __launch_bounds__(kRepBlock) void whatif_repair_kernel(RepairArgs a) {
+__global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_kernel(RepairArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_cnt, s_ecnt, s_ovf, s_slot;
   __shared__ uint32_t s_flag[3];
@@ -268,7 +269,18 @@ __global__ __launch_bounds__(kRepBlock) void whatif_repair_kernel(RepairArgs a) 
     for (uint32_t k = tid; k < n; k += B) {
       unsigned long long nl = blab[k];
       const uint2 er = erange[k];
-      for (uint32_t e = er.x; e < er.y; ++e) {
+      uint32_t e = er.x;
+      for (; e + 4 <= er.y; e += 4) {  // four predecessor labels in flight
+        uint2 ed[4];
+        unsigned long long lj[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ed[q] = edges[e + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lj[q] = lab[ed[q].x];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nl = meet(nl, (lj[q] >> 32) + ed[q].y, static_cast<uint32_t>(lj[q]));
+      }
+      for (; e < er.y; ++e) {
         const uint2 ed = edges[e];
         const unsigned long long lj = lab[ed.x];
         nl = meet(nl, (lj >> 32) + ed.y, static_cast<uint32_t>(lj));
@@ -325,9 +337,9 @@ hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, hipStream_t s) {
   e = hipGetLastError();
   if (e != hipSuccess || a.n_slots == 0) return e;
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, true>), dim3(a.n_req), dim3(kRepBlock), 0, s, a);
+    hipLaunchKernelGGL((whatif_repair_kernel<8, true>), dim3(a.n_req), dim3(kSlotBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, true>), dim3(a.n_req), dim3(kRepBlock), 0, s, a);
+    hipLaunchKernelGGL((whatif_repair_kernel<4, true>), dim3(a.n_req), dim3(kSlotBlock), 0, s, a);
   return hipGetLastError();
 }
 
