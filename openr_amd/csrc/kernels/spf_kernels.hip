@@ -1174,6 +1174,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   uint32_t mpar = 0;  // s_min[mpar] bounds the far set from below
   for (uint32_t it = 0;; ++it) {
     bool pushed_near = false;
+    uint32_t far_min = kInf;  // this thread's smallest far push (one LDS atomic per wave below)
     // merge the candidate {nd, cnh} into u's label: smaller replaces, equal
     // ORs (cl: u's label as loaded); re-queue u if the label changed
     auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, unsigned long long cl) {
@@ -1195,7 +1196,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
         pushed_near = true;
       } else {
         atomicOr(&far[u >> 5], bit);
-        atomicMin(&s_min[mpar], nd);
+        far_min = min(far_min, nd);
       }
     };
     uint32_t w = tid, bits = 0, wbase = 0;
@@ -1265,6 +1266,10 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
           }
         }
       }
+    }
+    {  // the far set's lower bound: every far push folded per wave, not per push
+      const uint32_t fm = wave_min(far_min);
+      if ((tid & 63u) == 0 && fm != kInf) atomicMin(&s_min[mpar], fm);
     }
     const uint32_t par = it % 3u;
     if (pushed_near) s_flag[par] = 1u;
