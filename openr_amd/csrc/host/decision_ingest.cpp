@@ -156,6 +156,24 @@ void processPublication(const Publication& pub, const std::string& me, bool orde
   LinkState& ls = areaLinkStates.at(area);
   if (pub.keyVals.empty() && pub.expiredKeys.empty()) return;
 
+  // ordered FIB: the hold TTLs of every adjacency update
+  // read hop-count SPFs from `me` and from the updated node
+  // (Decision.cpp:1715-1723); fetch all of them in one device batch up front.
+  // The memo still drops them on a topology change, so an update after one
+  // recomputes exactly what the reference's sequential loop would.
+  if (orderedFib) {
+    std::vector<std::string> hopSrcs{me};
+    for (const auto& [key, val] : pub.keyVals) {
+      if (!val.value || !startsWith(key, kAdjDbMarker)) continue;
+      try {
+        hopSrcs.push_back(compact::adjacencyDatabase(*val.value).thisNodeName);
+      } catch (const std::exception&) {
+        // reported by the update loop below
+      }
+    }
+    ls.prefetchSpfResults(hopSrcs, false);
+  }
+
   // LSDB addition / update (Decision.cpp:1697-1790)
   for (const auto& [key, val] : pub.keyVals) {
     if (!val.value) {  // TTL refresh

@@ -185,3 +185,63 @@ def _prefix_key_in(node, entry, area):
     import ipaddress
     p = entry.prefix
     return f"prefix:{node}:{area}:[{ipaddress.ip_address(p.prefixAddress.addr)}/{p.prefixLength}]"
+
+
+def test_ordered_fib_publication_holds(hip, oracle):
+    """Ordered FIB (Decision.cpp:1715-1723): each adjacency
+    update gets hold TTLs from hop counts (me -> node, max hops from node),
+    whose SPFs the product fetches for the whole publication in one batch.
+    The oracle applies the same databases one by one with TTLs from its own
+    hop queries; holds, their expiry and the route DBs must agree."""
+    from openr_amd.topology import bench_grid
+    mod = hip.module
+    dbs, pfx = bench_grid(6, 1)
+    for db in dbs:
+        db.area = AREA
+    pfx = [(n, AREA, e) for n, _, e in pfx]
+    me = "0"
+    als_h = hip.area_link_states()
+    ps_h = hip.prefix_state()
+    als_o = oracle.area_link_states(AREA)
+    ps_o = oracle.prefix_state()
+    ingest = mod.DecisionIngest(me, True)
+
+    def oracle_update(db):
+        ls = als_o[AREA]
+        up = down = 0
+        hops = ls.get_hops_from_a_to_b(me, db.thisNodeName)
+        if hops is not None:
+            up = hops
+            down = ls.get_max_hops_to_node(db.thisNodeName) - up
+        ls.update_adjacency_database(db, up, down)
+
+    def adj_val(db, ver):
+        return (ver, db.thisNodeName, mod.adj_db_to_compact(db.to_wire()), 1, 1)
+
+    for db in dbs:  # one publication per database: a defined order
+        ingest.process_publication(mod.publication_to_compact(AREA, {f"adj:{db.thisNodeName}": adj_val(db, 1)}, []),
+                                   als_h._impl, ps_h._impl)
+        oracle_update(db)
+    kv = {f"prefix:{n}:{AREA}:[{__import__('ipaddress').ip_address(e.prefix.prefixAddress.addr)}/"
+          f"{e.prefix.prefixLength}]": (1, n, mod.prefix_db_to_compact(n, AREA, [e.to_wire()]), 1, 1)
+          for n, _, e in pfx}
+    ingest.process_publication(mod.publication_to_compact(AREA, kv, []), als_h._impl, ps_h._impl)
+    for n, a, e in pfx:
+        ps_o.update_prefix(n, a, e)
+    # one publication of metric changes on many nodes: hop counts do not depend
+    # on metrics, so the per-update TTLs are the same in any order
+    changed = [db for db in dbs if int(db.thisNodeName) % 5 == 2]
+    for db in changed:
+        for adj in db.adjacencies:
+            adj.metric += 3
+    ingest.process_publication(mod.publication_to_compact(
+        AREA, {f"adj:{db.thisNodeName}": adj_val(db, 2) for db in changed}, []), als_h._impl, ps_h._impl)
+    for db in changed:
+        oracle_update(db)
+    ls_h = als_h._impl.area(AREA)
+    assert ls_h.has_holds() and als_o[AREA].has_holds()  # the metric increases are held
+    for tick in range(12):
+        assert _routes(hip, als_h._impl, ps_h._impl, me) == _routes(oracle, als_o._impl, ps_o._impl, me), tick
+        ls_h.decrement_holds()
+        als_o[AREA].decrement_holds()
+        assert ls_h.has_holds() == als_o[AREA].has_holds(), tick
