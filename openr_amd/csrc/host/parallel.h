@@ -45,6 +45,15 @@ class WorkerPool {
     lock.unlock();
     runChunk(0);
     lock.lock();
+    // the caller keeps claiming chunks too: a worker that wakes late then
+    // finds nothing left instead of holding the phase up
+    while (next_ < parts_) {
+      const size_t c = next_++;
+      lock.unlock();
+      runChunk(c);
+      lock.lock();
+      --pending_;
+    }
     done_.wait(lock, [&] { return pending_ == 0; });
     job_ = nullptr;
     if (err_) std::rethrow_exception(err_);
