@@ -51,13 +51,16 @@ def parse():
     p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
     p.add_argument("--topologies", type=int, default=32,
                    help="what-if variants per step (--scaling whatif)")
-    p.add_argument("--lanes", type=int, default=4,
+    p.add_argument("--lanes", type=int, default=8,
                    help="stream lanes per rank: a rank's what-if variants are dealt over this many "
                         "contexts (own HIP stream each) so their sweeps overlap on the GPU")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="oracle threads (0: every CPU this process may use)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rehearse-on-one-gpu", action="store_true",
+                   help="rehearsal of the N-rank path on a one-GPU box: every rank drives GPU 0 "
+                        "and the ranks sync over gloo (never used for reported numbers)")
     p.add_argument("--no-route-db", action="store_true")
     p.add_argument("--legs", default="c1,c3,c4,c5",
                    help="extra BASELINE configs reported under 'legs' (c1,c3,c4,c5; '' for none)")
@@ -87,13 +90,23 @@ def median_ms(fn, reps):
 def main():
     args = parse()
     rank, world, local = dist_env()
+    # hardware queues of this process (HIP default 4): one per stream lane, so
+    # the lanes' kernels reach the GPU on separate queues (tools/lanes_probe.py:
+    # 32 sweeps on 8 lanes 11.28 M SPF-sources/s at 16 queues vs 11.02 at 4);
+    # set before the first HIP call
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    if args.rehearse_on_one_gpu:
+        local = 0
     os.environ.setdefault("ORH_DEVICE", str(local))  # before the host library opens a context
     import torch
     import torch.distributed as dist
 
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_on_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     def barrier():
         if world > 1:
@@ -102,7 +115,8 @@ def main():
     def max_over_ranks(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64,
+                         device="cpu" if args.rehearse_on_one_gpu else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 

@@ -13,7 +13,7 @@ n = 100
 names = [str(i) for i in range(n * n)]
 T = int(os.environ.get("T", "16"))
 lss = {}
-for L in (1, 2, 4, 8):
+for L in [int(x) for x in os.environ.get("LANES", "1,2,4,8").split(",")]:
     sweeps = []
     for t in range(T):
         adj, pfx = bench_grid(n, 1)
