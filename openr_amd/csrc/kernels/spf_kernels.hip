@@ -1963,7 +1963,15 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
   a.tiles = (a.n_nodes + kBlock * kHopPer - 1) / (kBlock * kHopPer);
   const uint64_t grid = static_cast<uint64_t>(a.tiles) * a.n_out;
   if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  const size_t lds = std::max<size_t>(hop_lds_bytes(max_nbr), 16);
+  size_t lds = std::max<size_t>(hop_lds_bytes(max_nbr), 16);
+  // ORH_HOP_LDS_MIN (experiment): reserve at least this much LDS per
+  // first-hop workgroup, capping how many share a CU with the level searches
+  // of other streams
+  static const size_t lds_min = [] {
+    const char* e = getenv("ORH_HOP_LDS_MIN");
+    return e ? static_cast<size_t>(atol(e)) : size_t{0};
+  }();
+  lds = std::max(lds, lds_min);
   if (a.lvl_rows) {
     // 16 nodes per thread unless that leaves fewer than ~32 workgroups per CU
     // a workgroup per source walks the tiles (one gather of the source's
