@@ -199,6 +199,25 @@ def leg_c5(hip, cpu):
                           # + freeing the returned 1M-route DB (glibc), outside the reference's
                           # route_build_ms too
                           "rebuild_wall_ms": round((time.perf_counter() - t0) * 1e3, 2)}
+    # Decision::rebuildRoutes after prefix-only updates (Decision.cpp:1902-1924):
+    # only the updated prefixes are rebuilt (one device selection pass over
+    # the prefix mirror + host materialisation of those routes)
+    rib = hip.module.DecisionRib()
+    rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, True, [])
+    changed = set()
+    for i in range(10_000):
+        node, area, e = pfx[rng.randrange(len(pfx))]
+        if i % 2:
+            got = ps.delete_prefix(node, area, e.prefix)
+        else:
+            got = ps.update_prefix(node, area, PrefixEntry(e.prefix, metrics=PrefixMetrics(
+                1, rng.randint(0, 3), rng.randint(0, 3), rng.randint(0, 3)), tags=e.tags))
+        changed |= {(p.prefixAddress.addr, p.prefixLength) for p in got}
+    (uu, ud, _, _), sec = rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, False, sorted(changed))
+    out["incremental_prefix_only"] = {"updates": "10k prefix add/withdraw, no topology change",
+                                      "prefixes_rebuilt": len(changed),
+                                      "rebuild_ms": round(sec * 1e3, 2),
+                                      "routes_updated": len(uu), "routes_deleted": len(ud)}
     policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
         0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
     build_s, policy_s, routes, updated = solver._impl.time_build_route_db_with_policy(

@@ -245,4 +245,41 @@ void processPublication(const Publication& pub, const std::string& me, bool orde
   }
 }
 
+DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::string& me,
+                                              const AreaLinkStates& als, const PrefixState& ps,
+                                              bool fullRebuild, const std::vector<Cidr>& updatedPrefixes,
+                                              RibPolicy* policy) {
+  DecisionRouteUpdate update;
+  if (fullRebuild) {
+    DecisionRouteDb db = solver.buildRouteDb(me, als, ps).value_or(DecisionRouteDb{});
+    if (policy) policy->applyPolicy(db.unicastRoutes);
+    update = routeDb_.calculateUpdate(std::move(db));
+  } else {
+    auto routes = solver.createRoutesForPrefixes(me, als, ps, updatedPrefixes);
+    for (size_t i = 0; i < routes.size(); ++i) {
+      if (routes[i]) {
+        if (!update.unicastRoutesToUpdate.emplace(updatedPrefixes[i], std::move(*routes[i])).second)
+          throw std::logic_error("rebuildRoutes: duplicate prefix");  // RouteUpdate.h:39 CHECK
+      } else {
+        update.unicastRoutesToDelete.push_back(updatedPrefixes[i]);
+      }
+    }
+    if (policy) {
+      for (const auto& p : policy->applyPolicy(update.unicastRoutesToUpdate).deletedRoutes)
+        update.unicastRoutesToDelete.push_back(p);
+    }
+  }
+  routeDb_.update(update);
+  return update;
+}
+
+DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::string& me,
+                                              const AreaLinkStates& als, const PrefixState& ps,
+                                              DecisionPendingUpdates& pending, RibPolicy* policy) {
+  std::vector<Cidr> prefixes(pending.updatedPrefixes().begin(), pending.updatedPrefixes().end());
+  auto u = rebuildRoutes(solver, me, als, ps, pending.needsFullRebuild(), prefixes, policy);
+  pending.reset();
+  return u;
+}
+
 }  // namespace openr_amd

@@ -18,6 +18,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "rib_policy.h"
 #include "spf_solver.h"
 
 namespace openr_amd {
@@ -90,5 +91,25 @@ void processPublication(const Publication& pub, const std::string& me, bool orde
                         DecisionPendingUpdates& pending,
                         std::unordered_map<std::string, int64_t>& fibTimes, IngestStats& stats,
                         unsigned lane = 0);
+
+// Decision's route database and Decision::rebuildRoutes (Decision.cpp:1865-1930):
+// a full rebuild (buildRouteDb, RibPolicy, calculateUpdate against the
+// previous database) when the pending updates need one, else only the
+// updated prefixes (createRouteForPrefixOrGetStaticRoute, here batched over
+// one device selection pass); the database takes the update either way.
+class DecisionRib {
+ public:
+  DecisionRouteUpdate rebuildRoutes(SpfSolver& solver, const std::string& me,
+                                    const AreaLinkStates& als, const PrefixState& ps,
+                                    bool fullRebuild, const std::vector<Cidr>& updatedPrefixes,
+                                    RibPolicy* policy);
+  DecisionRouteUpdate rebuildRoutes(SpfSolver& solver, const std::string& me,
+                                    const AreaLinkStates& als, const PrefixState& ps,
+                                    DecisionPendingUpdates& pending, RibPolicy* policy);
+  const DecisionRouteDb& routeDb() const { return routeDb_; }
+
+ private:
+  DecisionRouteDb routeDb_;
+};
 
 }  // namespace openr_amd

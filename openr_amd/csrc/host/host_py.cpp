@@ -882,6 +882,32 @@ PYBIND11_MODULE(_openr_host, m) {
         return d;
       });
 
+  // Decision::routeDb_ + rebuildRoutes (Decision.cpp:1865-1930); returns
+  // (delta wire, seconds)
+  py::class_<DecisionRib>(m, "DecisionRib")
+      .def(py::init<>())
+      .def("rebuild_routes",
+           [](DecisionRib& r, SpfSolver& solver, const std::string& me, const AreaMap& als,
+              const PrefixState& ps, bool full, std::vector<py::tuple> prefixes, RibPolicy* policy) {
+             std::vector<Cidr> pfx;
+             pfx.reserve(prefixes.size());
+             for (auto& t : prefixes) pfx.emplace_back(AddrBytes(str(t[0])), t[1].cast<int32_t>());
+             const auto t0 = std::chrono::steady_clock::now();
+             auto u = r.rebuildRoutes(solver, me, als.m, ps, full, pfx, policy);
+             const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             return py::make_tuple(deltaToWire(u), sec);
+           },
+           py::arg("solver"), py::arg("me"), py::arg("als"), py::arg("ps"), py::arg("full"),
+           py::arg("prefixes"), py::arg("policy") = nullptr)
+      .def("rebuild_routes_pending",  // from a DecisionIngest's pending updates (then reset)
+           [](DecisionRib& r, SpfSolver& solver, const std::string& me, const AreaMap& als,
+              const PrefixState& ps, Ingest& g, RibPolicy* policy) {
+             return deltaToWire(r.rebuildRoutes(solver, me, als.m, ps, g.pending, policy));
+           },
+           py::arg("solver"), py::arg("me"), py::arg("als"), py::arg("ps"), py::arg("ingest"),
+           py::arg("policy") = nullptr)
+      .def("route_db", [](const DecisionRib& r) { return routeDbToWire(r.routeDb()); });
+
   py::class_<PrefixState>(m, "PrefixState")
       .def(py::init<>())
       .def("update_prefix",

@@ -115,4 +115,12 @@ RibPolicy::PolicyChange RibPolicy::applyPolicy(UnicastRouteMap& routes) {
   return change;
 }
 
+RibPolicy::PolicyChange RibPolicy::applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes) {
+  PolicyChange change;
+  if (!isActive()) return change;
+  for (auto& [prefix, route] : routes)
+    if (applyAction(route, &invalidated_)) change.updatedRoutes.push_back(route.prefix);
+  return change;
+}
+
 }  // namespace openr_amd

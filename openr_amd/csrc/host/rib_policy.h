@@ -64,6 +64,8 @@ class RibPolicy {
   // distinct routes and counters)
   bool applyAction(RibUnicastEntry& route, uint64_t* invalidated) const;
   PolicyChange applyPolicy(UnicastRouteMap& routes);
+  // the same over a DecisionRouteUpdate's routes (Decision.cpp:1912-1924)
+  PolicyChange applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes);
   // decision.rib_policy.invalidated_routes (RibPolicy.cpp:150-153)
   uint64_t invalidatedRoutes() const { return invalidated_; }
 

@@ -219,6 +219,56 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
   return e;
 }
 
+std::vector<std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+    const std::vector<Cidr>& prefixes) {
+  std::vector<std::optional<RibUnicastEntry>> out(prefixes.size());
+  // KSP2 prefixes may trace paths lazily (memo writes): one prefix at a time
+  const bool hasKsp = ps.ksp2Entries() > 0;
+  bool dev = false;
+  if (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64) {
+    for (const auto& [_, ls] : als) ls.getSpfRow(me);
+    dev = selectOnDevice(me, als, ps);
+  }
+  auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
+    auto it = staticUnicastRoutes_.find(p);
+    if (it == staticUnicastRoutes_.end()) return std::nullopt;
+    RibUnicastEntry e;
+    e.prefix = p;
+    e.nexthops.insert(it->second.begin(), it->second.end());
+    return e;
+  };
+  auto one = [&](size_t i) {
+    const Cidr& p = prefixes[i];
+    if (!dev) {
+      out[i] = createRouteForPrefixOrGetStaticRoute(me, als, ps, p);
+      return;
+    }
+    if (auto pid = ps.pidOf(p); pid && ps.prefixLive(*pid)) {
+      if (selStatus_[*pid] == ORH_SEL_ROUTE) {
+        out[i] = materialize(*pid, ps);
+        return;
+      }
+      if (selStatus_[*pid] == ORH_SEL_HOST) {
+        if (auto r = createRouteForPrefix(me, als, ps, p)) {
+          out[i] = std::move(r);
+          return;
+        }
+      }
+    }
+    out[i] = staticRoute(p);
+  };
+  auto& pool = WorkerPool::instance();
+  if (!hasKsp && prefixes.size() >= 64 && pool.size() > 1) {
+    pool.parallelFor(prefixes.size(), [&](size_t, size_t b, size_t e) {
+      for (size_t i = b; i < e; ++i) one(i);
+    });
+  } else {
+    for (size_t i = 0; i < prefixes.size(); ++i) one(i);
+  }
+  return out;
+}
+
 std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string& me,
                                                                const AreaLinkStates& als,
                                                                const PrefixState& ps,

@@ -129,6 +129,15 @@ class SpfSolver {
       const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
       const Cidr& prefix);
 
+  // createRouteForPrefixOrGetStaticRoute for many prefixes at once (the
+  // incremental branch of Decision::rebuildRoutes, Decision.cpp:1902-1911):
+  // one device selection pass over the prefix mirror, then the listed
+  // prefixes materialised on the host pool; the same results as one call per
+  // prefix
+  std::vector<std::optional<RibUnicastEntry>> createRoutesForPrefixes(
+      const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+      const std::vector<Cidr>& prefixes);
+
   uint64_t routeBuildRuns() const { return routeBuildRuns_; }
   // prefixes of the last buildRouteDb whose selection ran on the device /
   // took the host path (BGP, SR_MPLS, KSP2, minNexthop, self-advertised)

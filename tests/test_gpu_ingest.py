@@ -14,7 +14,7 @@ import random
 import pytest
 
 from openr_amd.facade import load_topology
-from openr_amd.types import IpPrefix, RouteDb, create_prefix_entry
+from openr_amd.types import K_TESTING_AREA as A_DEF, IpPrefix, PrefixMetrics, RouteDb, create_prefix_entry
 
 from test_gpu_parity import random_topology
 
@@ -245,3 +245,72 @@ def test_ordered_fib_publication_holds(hip, oracle):
         ls_h.decrement_holds()
         als_o[AREA].decrement_holds()
         assert ls_h.has_holds() == als_o[AREA].has_holds(), tick
+
+
+def test_rebuild_routes_incremental(hip, oracle):
+    """Decision::rebuildRoutes (Decision.cpp:1865-1930): a full rebuild, then
+    prefix-only updates rebuilt incrementally (only the updated prefixes; the
+    device-selection batch from 64 prefixes on, the per-prefix host path
+    below). After each rebuild the route database equals a full build of the
+    same state on the oracle; with a RibPolicy, the incremental result equals
+    a full rebuild with that policy."""
+    from openr_amd.rib_policy import RibPolicy, RibPolicyStatement, RibRouteActionWeight
+    mod = hip.module
+    dbs = random_topology(6200, n=24, extra=36, max_metric=9)
+    rng = random.Random(62)
+    pfx = []
+    for i in range(80):
+        for db in rng.sample(dbs, rng.randint(1, 3)):
+            pfx.append((db.thisNodeName, A_DEF, create_prefix_entry(IpPrefix.of(f"fd00:{i:x}::/64"))))
+    als_h, ps_h = load_topology(hip, dbs, pfx)
+    als_o, ps_o = load_topology(oracle, dbs, pfx)
+    me = sorted(db.thisNodeName for db in dbs)[3]
+    solver = hip.spf_solver(me, True)._impl
+    rib = mod.DecisionRib()
+    rib.rebuild_routes(solver, me, als_h._impl, ps_h._impl, True, [])
+    assert RouteDb.from_wire(rib.route_db()).canonical() == _routes(oracle, als_o._impl, ps_o._impl, me)
+
+    def prefix_round(n_changes, policy=None):
+        changed = set()
+        for _ in range(n_changes):
+            r = rng.random()
+            if r < 0.4:  # withdraw an advertisement
+                node, area, e = pfx[rng.randrange(len(pfx))]
+                for be_ps in (ps_h, ps_o):
+                    changed |= {(p.prefixAddress.addr, p.prefixLength) for p in be_ps.delete_prefix(node, area, e.prefix)}
+            elif r < 0.7:  # a new prefix
+                node = rng.choice(dbs).thisNodeName
+                e = create_prefix_entry(IpPrefix.of(f"fd01:{rng.randrange(1 << 16):x}::/64"))
+                pfx.append((node, A_DEF, e))
+                for be_ps in (ps_h, ps_o):
+                    changed |= {(p.prefixAddress.addr, p.prefixLength) for p in be_ps.update_prefix(node, A_DEF, e)}
+            else:  # re-advertise with other metrics
+                node, area, e = pfx[rng.randrange(len(pfx))]
+                e2 = create_prefix_entry(e.prefix)
+                e2.metrics = PrefixMetrics(1, rng.randint(0, 2), rng.randint(0, 2), rng.randint(0, 2))
+                for be_ps in (ps_h, ps_o):
+                    changed |= {(p.prefixAddress.addr, p.prefixLength) for p in be_ps.update_prefix(node, area, e2)}
+        rib.rebuild_routes(solver, me, als_h._impl, ps_h._impl, False, sorted(changed),
+                           policy._impl if policy else None)
+        return changed
+
+    for n in (120, 10):  # device-batched, then per-prefix host path
+        prefix_round(n)
+        assert RouteDb.from_wire(rib.route_db()).canonical() == _routes(oracle, als_o._impl, ps_o._impl, me), n
+
+    policy = RibPolicy([RibPolicyStatement("w", None, ["t"], RibRouteActionWeight(3, {A_DEF: 2}, {}))], 3600)
+    # tag every prefix advertisement so the statement matches, then rebuild
+    tagged = []
+    for node, area, e in pfx:
+        e2 = create_prefix_entry(e.prefix)
+        e2.tags = ("t",)
+        tagged.append((node, area, e2))
+        ps_h.update_prefix(node, area, e2)
+    rib.rebuild_routes(solver, me, als_h._impl, ps_h._impl, False,
+                       sorted({(e.prefix.prefixAddress.addr, e.prefix.prefixLength) for _, _, e in tagged}),
+                       policy._impl)
+    fresh = mod.DecisionRib()
+    fresh.rebuild_routes(solver, me, als_h._impl, ps_h._impl, True, [], policy._impl)
+    got = RouteDb.from_wire(rib.route_db())
+    assert got.canonical_full() == RouteDb.from_wire(fresh.route_db()).canonical_full()
+    assert any(nh.weight == 2 for r in got.unicastRoutes.values() for nh in r.nextHops)
