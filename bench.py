@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
     p.add_argument("--topologies", type=int, default=32,
                    help="what-if variants per step (--scaling whatif)")
-    p.add_argument("--lanes", type=int, default=8,
+    p.add_argument("--lanes", type=int, default=4,
                    help="stream lanes per rank: a rank's what-if variants are dealt over this many "
                         "contexts (own HIP stream each) so their sweeps overlap on the GPU")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
@@ -90,11 +90,6 @@ def median_ms(fn, reps):
 def main():
     args = parse()
     rank, world, local = dist_env()
-    # hardware queues of this process (HIP default 4): one per stream lane, so
-    # the lanes' kernels reach the GPU on separate queues (tools/lanes_probe.py:
-    # 32 sweeps on 8 lanes 11.28 M SPF-sources/s at 16 queues vs 11.02 at 4);
-    # set before the first HIP call
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     if args.rehearse_on_one_gpu:
         local = 0
     os.environ.setdefault("ORH_DEVICE", str(local))  # before the host library opens a context
