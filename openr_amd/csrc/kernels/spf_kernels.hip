@@ -1136,6 +1136,209 @@ __global__ __launch_bounds__(256) void spf_global_kernel(SpfArgs a) {
 // The far set also tracks a lower bound of its distances (LDS atomicMin on
 // every far push, recomputed exactly while promoting), so advancing the
 // threshold costs one pass over the far nodes instead of two.
+
+// Expand frontier nodes vs[0..c) of one row: the group's record, label and
+// neighbour-label loads are in flight together (one round trip per stage for
+// the group instead of per node), then merge(u, nd, cnh, cl) runs per live
+// out-edge with u's label cl as loaded.
+template <int K, int G, typename Merge>
+__device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, unsigned long long* lab,
+                                             const uint32_t (&vs)[G], int c, Merge& merge) {
+  uint2 rec[G][K];
+  unsigned long long lv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (g >= c) break;
+    load_recs<K>(a, vs[g], rec[g]);
+    lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  unsigned long long cl[G][K];
+  bool ok[G][K];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
+      if (ok[g][j])
+        cl[g][j] = __hip_atomic_load(&lab[rec[g][j].x & ORH_REC_COL_MASK], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (g >= c) break;
+    const uint32_t v = vs[g];
+    if (v != s.node && (rec[g][0].x & ORH_REC_ROW_OVL)) continue;  // no transit
+    const uint32_t dv = static_cast<uint32_t>(lv[g] >> 32);
+    const uint32_t nhv = static_cast<uint32_t>(lv[g]);
+    const bool from_src = v == s.node;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (!ok[g][j]) continue;
+      const uint2 r = rec[g][j];
+      merge(r.x & ORH_REC_COL_MASK, dv + (a.use_link_metric ? r.y : 1u),
+            from_src ? (1u << a.rank_out[v * K + j]) : nhv, cl[g][j]);
+    }
+    const uint2 last = rec[g][K - 1];
+    if (last.x & ORH_REC_CONT) {
+      const uint32_t start = last.x & ORH_REC_COL_MASK;
+      for (uint32_t q = 0; q < last.y; ++q) {
+        const uint2 r = a.recs[start + q];
+        if (!live(a, s, r, start + q)) continue;
+        const uint32_t u = r.x & ORH_REC_COL_MASK;
+        merge(u, dv + (a.use_link_metric ? r.y : 1u), from_src ? (1u << a.rank_out[start + q]) : nhv,
+              __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+    }
+  }
+}
+
+// Asynchronous twin of spf_global_nh_kernel (below): within a bucket no
+// barrier separates relaxation rounds. A thread claims the near nodes of its
+// own words (atomicExch of the word; others only set bits) as soon as they
+// appear and expands them; the bucket ends when s_work, the count of queued
+// plus claimed-but-unexpanded near nodes, reaches zero. A push counts itself
+// before its bit becomes visible and an expansion uncounts its nodes after
+// its pushes, so the count never undercounts: zero means no near work exists
+// or can appear, and every wave leaves the loop on the same condition. The
+// lattice fixpoint does not depend on the order relaxations run in, so the
+// result is the synchronous kernel's bit for bit; what goes away is the
+// per-round barrier that held every wave to the slowest one (the C4 WAN runs
+// about a hundred near rounds per search).
+template <int K>
+__global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_work;
+  __shared__ uint32_t s_min[2];
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
+  constexpr int G = K <= 4 ? 4 : 2;
+  uint32_t* near = lds;
+  uint32_t* far = lds + NB;
+  if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
+  const Src s(a, row);
+  unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
+
+  for (uint32_t i = tid; i < 2 * NB; i += nthr) lds[i] = 0u;
+  for (uint32_t i = tid; i < N; i += nthr) lab[i] = kInfLabel;
+  if (tid < 2) s_min[tid] = kInf;
+  __syncthreads();
+  if (tid == 0) {
+    lab[s.node] = 0ull;
+    near[s.node >> 5] = 1u << (s.node & 31u);
+    s_work = 1u;
+  }
+  __syncthreads();
+
+  const uint32_t delta = a.delta;
+  uint32_t T = delta;
+  uint32_t mpar = 0;
+  for (;;) {
+    uint32_t far_min = kInf;
+    auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, unsigned long long cl) {
+      for (;;) {
+        const uint32_t cd = static_cast<uint32_t>(cl >> 32);
+        if (nd > cd) return;
+        const unsigned long long nl = nd < cd
+            ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
+            : (cl | cnh);
+        if (nl == cl) return;
+        const unsigned long long old = atomicCAS(&lab[u], cl, nl);
+        if (old == cl) break;
+        cl = old;
+      }
+      const uint32_t bit = 1u << (u & 31u);
+      if (nd < T) {
+        atomicAdd(&s_work, 1u);  // counted before the bit is visible
+        const uint32_t old = atomicOr(&near[u >> 5], bit);
+        atomicAnd(&far[u >> 5], ~bit);
+        if (old & bit) atomicSub(&s_work, 1u);  // already queued
+      } else {
+        atomicOr(&far[u >> 5], bit);
+        far_min = min(far_min, nd);
+      }
+    };
+    uint32_t w = tid, bits = 0, wbase = 0;
+    for (;;) {
+      uint32_t vs[G];
+      int c = 0;
+      while (c < G) {
+        while (!bits && w < NB) {
+          bits = __hip_atomic_load(&near[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (bits) bits = atomicExch(&near[w], 0u);  // at least the bits seen: only we clear
+          wbase = w * 32;
+          w += nthr;
+        }
+        if (!bits) break;
+        vs[c++] = wbase + __builtin_ctz(bits);
+        bits &= bits - 1;
+      }
+      if (!bits && w >= NB) w = tid;  // words exhausted: rescan them next time
+      if (__builtin_amdgcn_ballot_w64(c > 0) == 0ull) {
+        // the whole wave found nothing: done once nothing is queued or claimed
+        const uint32_t pending = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&s_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (pending == 0u) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (c > 0) {
+        expand_group<K, G>(a, s, lab, vs, c, merge);
+        atomicSub(&s_work, static_cast<uint32_t>(c));
+      }
+    }
+    {
+      const uint32_t fm = wave_min(far_min);
+      if ((tid & 63u) == 0 && fm != kInf) atomicMin(&s_min[mpar], fm);
+    }
+    __syncthreads();  // bucket drained everywhere; far bound folded
+    const uint32_t m = s_min[mpar];
+    if (m == kInf) break;  // far set empty: done (every thread read the same value)
+    T = m + delta;
+    const uint32_t npar = mpar ^ 1u;
+    if (tid == 0) s_min[npar] = kInf;
+    __syncthreads();
+    uint32_t local_min = kInf, promoted = 0;
+    for (uint32_t w2 = tid; w2 < NB; w2 += nthr) {
+      uint32_t fb = far[w2], promote = 0u;
+      for (uint32_t q = fb; q; q &= q - 1) {
+        const uint32_t b = __builtin_ctz(q);
+        const uint32_t d = static_cast<uint32_t>(
+            __hip_atomic_load(&lab[w2 * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
+        if (d < T) promote |= 1u << b;
+        else local_min = min(local_min, d);
+      }
+      if (promote) {
+        far[w2] = fb & ~promote;
+        near[w2] = promote;  // the near set is empty between buckets
+        promoted += __builtin_popcount(promote);
+      }
+    }
+    if (promoted) atomicAdd(&s_work, promoted);
+    const uint32_t wm = wave_min(local_min);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
+    mpar = npar;
+    __syncthreads();
+  }
+  __syncthreads();
+  uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
+  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * a.words;
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const unsigned long long l =
+        __hip_atomic_load(&lab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_nontemporal_store(static_cast<uint32_t>(l >> 32), &od[i]);
+    if (a.words == 1) {
+      __builtin_nontemporal_store(static_cast<uint32_t>(l), &on[i]);
+    } else {
+      on[static_cast<size_t>(i) * a.words] = static_cast<uint32_t>(l);
+      for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
+    }
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1218,54 +1421,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
         bits &= bits - 1;
       }
       if (c == 0) break;
-      uint2 rec[G][K];
-      unsigned long long lv[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if (g >= c) break;
-        load_recs<K>(a, vs[g], rec[g]);
-        lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      unsigned long long cl[G][K];
-      bool ok[G][K];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
-          if (ok[g][j])
-            cl[g][j] = __hip_atomic_load(&lab[rec[g][j].x & ORH_REC_COL_MASK], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if (g >= c) break;
-        const uint32_t v = vs[g];
-        if (v != s.node && (rec[g][0].x & ORH_REC_ROW_OVL)) continue;  // no transit
-        const uint32_t dv = static_cast<uint32_t>(lv[g] >> 32);
-        const uint32_t nhv = static_cast<uint32_t>(lv[g]);
-        const bool from_src = v == s.node;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          if (!ok[g][j]) continue;
-          const uint2 r = rec[g][j];
-          merge(r.x & ORH_REC_COL_MASK, dv + (a.use_link_metric ? r.y : 1u),
-                from_src ? (1u << a.rank_out[v * K + j]) : nhv, cl[g][j]);
-        }
-        const uint2 last = rec[g][K - 1];
-        if (last.x & ORH_REC_CONT) {
-          const uint32_t start = last.x & ORH_REC_COL_MASK;
-          for (uint32_t q = 0; q < last.y; ++q) {
-            const uint2 r = a.recs[start + q];
-            if (!live(a, s, r, start + q)) continue;
-            const uint32_t u = r.x & ORH_REC_COL_MASK;
-            merge(u, dv + (a.use_link_metric ? r.y : 1u), from_src ? (1u << a.rank_out[start + q]) : nhv,
-                  __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          }
-        }
-      }
+      expand_group<K, G>(a, s, lab, vs, c, merge);
     }
     {  // the far set's lower bound: every far push folded per wave, not per push
       const uint32_t fm = wave_min(far_min);
@@ -1884,6 +2040,15 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
   (void)n_nodes;
 }
 
+// ORH_HBM_ASYNC=0 selects the round-synchronous HBM frontier kernel (A/B)
+static bool nh_async() {
+  static const bool on = [] {
+    const char* e = getenv("ORH_HBM_ASYNC");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <int K>
 static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   switch (plan.variant) {
@@ -1902,6 +2067,8 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
     case SpfVariant::kGlobal:
       return launch(spf_global_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kGlobalNh:
+      if (nh_async())
+        return launch(spf_global_nh_async_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
       return launch(spf_global_nh_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     default:
       return hipErrorInvalidValue;
