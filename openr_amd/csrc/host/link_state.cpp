@@ -6,6 +6,8 @@
 #include <set>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <stdexcept>
@@ -32,6 +34,19 @@ uint32_t toDeviceMetric(Metric m) {
   }
   return static_cast<uint32_t>(m);
 }
+
+// ORH_KSP_PROF=1: phase times of prefetchKthPaths / fillRows on stderr
+struct KspProf {
+  bool on = std::getenv("ORH_KSP_PROF") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "ksp-prof %-20s %8.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
 
 }  // namespace
 
@@ -548,7 +563,9 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
   } else {
     // rows land in the context's pinned buffer; copied out per row below
     const uint32_t *hd = nullptr, *hn = nullptr;
+    KspProf prof;
     check(ctx_, orh_spf_batch_pinned(graph_, &req, words, &hd, &hn), "orh_spf_batch_pinned");
+    prof.mark("rows: device + D2H");
     auto fill = [&](size_t, size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const size_t b = i * N;
@@ -558,6 +575,7 @@ void LinkState::fillRows(const std::vector<uint32_t>& srcIds, bool useLinkMetric
     };
     if (n > 1) WorkerPool::instance().parallelFor(n, fill);
     else fill(0, 0, n);
+    prof.mark("rows: host copies");
   }
   for (uint32_t i = 0; i < n; ++i) {
     SpfRow& row = rows[i];
@@ -651,10 +669,32 @@ void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes,
 
 void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const {
   // k = 1: traces over the memoized SPF of each source (batched)
+  KspProf prof;
   std::vector<std::string> srcs;
   for (const auto& pr : pairs) srcs.push_back(pr.first);
   prefetchSpfResults(srcs, true);
-  for (const auto& [a, b] : pairs) getKthPaths(a, b, 1);
+  prof.mark("k=1 rows");
+  // k = 1 traces over the memoized rows, independent per pair: on the pool
+  {
+    std::vector<const std::pair<std::string, std::string>*> need;
+    std::vector<const SpfRow*> rows1;
+    std::set<std::pair<std::string, std::string>> seen;
+    for (const auto& pr : pairs) {
+      if (kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{1}))) continue;
+      if (!seen.insert(pr).second) continue;
+      need.push_back(&pr);
+      rows1.push_back(&getSpfRow(pr.first, true));
+    }
+    std::vector<std::vector<Path>> traced(need.size());
+    auto trace = [&](size_t, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) traced[i] = traceKthPaths(need[i]->first, need[i]->second, *rows1[i], nullptr);
+    };
+    if (need.size() > 8) WorkerPool::instance().parallelFor(need.size(), trace);
+    else trace(0, 0, need.size());
+    for (size_t i = 0; i < need.size(); ++i)
+      kthPaths_.emplace(std::make_tuple(need[i]->first, need[i]->second, size_t{1}), std::move(traced[i]));
+  }
+  prof.mark("k=1 traces");
   // k = 2: one fresh SPF per pair with its k = 1 links ignored, all in one launch
   std::vector<uint32_t> ids;
   std::vector<std::vector<uint32_t>> ign;
@@ -675,13 +715,21 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
     ign.emplace_back(s.begin(), s.end());
     todo.push_back(&pr);
   }
+  prof.mark("k=2 ignore sets");
   auto rows = runSpfBatch(ids, true, &ign);
-  for (size_t i = 0; i < todo.size(); ++i) {
-    const auto& [src, dst] = *todo[i];
-    std::unordered_set<uint32_t> ignore(ign[i].begin(), ign[i].end());
-    kthPaths_.emplace(std::make_tuple(src, dst, size_t{2}),
-                      traceKthPaths(src, dst, rows[i], &ignore));
-  }
+  prof.mark("k=2 rows");
+  std::vector<std::vector<Path>> traced(todo.size());
+  auto trace = [&](size_t, size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const std::unordered_set<uint32_t> ignore(ign[i].begin(), ign[i].end());
+      traced[i] = traceKthPaths(todo[i]->first, todo[i]->second, rows[i], &ignore);
+    }
+  };
+  if (todo.size() > 8) WorkerPool::instance().parallelFor(todo.size(), trace);
+  else trace(0, 0, todo.size());
+  for (size_t i = 0; i < todo.size(); ++i)
+    kthPaths_.emplace(std::make_tuple(todo[i]->first, todo[i]->second, size_t{2}), std::move(traced[i]));
+  prof.mark("k=2 traces");
 }
 
 const SpfRow& LinkState::getSpfRow(const std::string& node, bool useLinkMetric) const {

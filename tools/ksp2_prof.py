@@ -23,3 +23,9 @@ for rep in range(2):
     t3 = time.perf_counter()
     print(f"rep {rep}: k=1 SPFs {1e3*(t1-t0):.2f} ms, k=1 traces {1e3*(t2-t1):.2f} ms, "
           f"k=2 SPFs + traces {1e3*(t3-t2):.2f} ms, total {1e3*(t3-t0):.2f} ms", flush=True)
+
+# device time alone for the k = 1 batch (plain rows of the same sources, no host copies)
+sw = ls.what_if_sweep([a for a, _ in kp], [[] for _ in kp])
+sw.run(); sw.sync()
+sw.run(); sw.sync()
+print(f"k=1 batch device only: {sw.last_ms():.3f} ms ({len(kp)} rows)", flush=True)
