@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <stdexcept>
+#include <string_view>
 
 namespace openr_amd {
 
@@ -453,35 +454,66 @@ void LinkState::flushMirror() const {
     }
   }
   if (structDirty_) {
+    KspProf prof;
+    // rows sized from the link sets, then filled per node on the pool (C4's
+    // 50k-node WAN: ~38 ms on one thread, mostly cache misses into links_)
     rowPtr_.assign(N + 1, 0);
-    col_.clear();
-    linkOfEntry_.clear();
-    std::vector<uint32_t> wout, win, meta;
-    entriesOfLink_.assign(links_.size(), {0u, 0u});
-    for (uint32_t v = 0; v < N; ++v) {
-      for (uint32_t id : *nodeLinks_[v]) {  // LinkSet iteration order
-        const Link& l = links_[id];
-        const uint32_t u = l.other(v);
-        const uint32_t e = static_cast<uint32_t>(col_.size());
-        col_.push_back(u);
-        linkOfEntry_.push_back(id);
-        const bool up = l.isUp();
-        wout.push_back(up ? toDeviceMetric(l.metricFrom(v)) : 1u);
-        win.push_back(up ? toDeviceMetric(l.metricFrom(u)) : 1u);
-        meta.push_back(id | (up ? 0u : ORH_META_DOWN));
-        auto& eo = entriesOfLink_[id];
-        (l.is1(v) ? eo.first : eo.second) = e;
-      }
-      rowPtr_[v + 1] = static_cast<uint32_t>(col_.size());
-    }
+    for (uint32_t v = 0; v < N; ++v)
+      rowPtr_[v + 1] = rowPtr_[v] + static_cast<uint32_t>(nodeLinks_[v]->size());
+    const uint32_t E = rowPtr_[N];
+    col_.assign(E, 0u);
+    linkOfEntry_.assign(E, 0u);
+    std::vector<uint32_t> wout(E), win(E), meta(E);
     std::vector<uint8_t> ovl(N, 0);
-    for (uint32_t v = 0; v < N; ++v) ovl[v] = isNodeOverloaded(names_[v]) ? 1 : 0;
-    // DijkstraQ ties break on the node name (LinkState.h:488-498)
-    std::vector<uint32_t> byName(N), nameRank(N);
-    for (uint32_t v = 0; v < N; ++v) byName[v] = v;
-    std::sort(byName.begin(), byName.end(),
-              [&](uint32_t a, uint32_t b) { return names_[a] < names_[b]; });
-    for (uint32_t r = 0; r < N; ++r) nameRank[byName[r]] = r;
+    entriesOfLink_.assign(links_.size(), {0u, 0u});
+    auto fillCsr = [&](size_t, size_t lo, size_t hi) {
+      for (size_t v = lo; v < hi; ++v) {
+        uint32_t e = rowPtr_[v];
+        for (uint32_t id : *nodeLinks_[v]) {  // LinkSet iteration order
+          const Link& l = links_[id];
+          const uint32_t x = static_cast<uint32_t>(v), u = l.other(x);
+          col_[e] = u;
+          linkOfEntry_[e] = id;
+          const bool up = l.isUp();
+          wout[e] = up ? toDeviceMetric(l.metricFrom(x)) : 1u;
+          win[e] = up ? toDeviceMetric(l.metricFrom(u)) : 1u;
+          meta[e] = id | (up ? 0u : ORH_META_DOWN);
+          auto& eo = entriesOfLink_[id];  // the two ends are distinct fields
+          (l.is1(x) ? eo.first : eo.second) = e;
+          ++e;
+        }
+        ovl[v] = isNodeOverloaded(names_[v]) ? 1 : 0;
+      }
+    };
+    auto& pool = WorkerPool::instance();
+    const bool par = N >= 4096 && pool.size() > 1;
+    if (par) pool.parallelFor(N, fillCsr);
+    else fillCsr(0, 0, N);
+    // DijkstraQ ties break on the node name (LinkState.h:488-498): names are
+    // unique, so chunks sorted on the pool and merged give std::sort's order
+    std::vector<std::pair<std::string_view, uint32_t>> byName(N);
+    for (uint32_t v = 0; v < N; ++v) byName[v] = {names_[v], v};
+    auto less = [](const std::pair<std::string_view, uint32_t>& a,
+                   const std::pair<std::string_view, uint32_t>& b) { return a.first < b.first; };
+    if (par) {
+      const size_t P = pool.size();
+      auto at = [&](size_t c) { return byName.begin() + static_cast<std::ptrdiff_t>(N * std::min(c, P) / P); };
+      pool.parallelFor(P, [&](size_t, size_t b, size_t e) {
+        for (size_t c = b; c < e; ++c) std::sort(at(c), at(c + 1), less);
+      });
+      for (size_t w = 1; w < P; w *= 2) {
+        const size_t groups = (P + 2 * w - 1) / (2 * w);
+        pool.parallelFor(groups, [&](size_t, size_t b, size_t e) {
+          for (size_t k = b; k < e; ++k)
+            std::inplace_merge(at(2 * w * k), at(2 * w * k + w), at(2 * w * k + 2 * w), less);
+        });
+      }
+    } else {
+      std::sort(byName.begin(), byName.end(), less);
+    }
+    std::vector<uint32_t> nameRank(N);
+    for (uint32_t r = 0; r < N; ++r) nameRank[byName[r].second] = r;
+    prof.mark("mirror: host CSR");
     orh_csr c{};
     c.n_nodes = N;
     c.name_rank = nameRank.data();
@@ -494,6 +526,7 @@ void LinkState::flushMirror() const {
     c.meta = meta.data();
     c.node_overloaded = ovl.data();
     check(ctx_, orh_graph_load(graph_, &c), "orh_graph_load");
+    prof.mark("mirror: orh_graph_load");
     ++mirrorLoads_;
     structDirty_ = false;
     rowsDirty_.clear();

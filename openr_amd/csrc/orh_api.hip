@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -657,9 +658,20 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
     for (uint32_t v = 0; v < c->n_nodes; ++v)
       if (c->name_rank[v] >= c->n_nodes)
         return fail(ctx, ORH_E_INVALID, "orh_graph_load: name_rank out of range");
+  // ORH_LOAD_PROF=1: phase times on stderr
+  static const bool prof_on = getenv("ORH_LOAD_PROF") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!prof_on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "load-prof %-14s %8.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(now - t_prev).count());
+    t_prev = now;
+  };
   ORH_HIP(ctx, hipSetDevice(ctx->device));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   free_graph_device(g);
+  mark("free");
   g->n_nodes = c->n_nodes;
   g->n_edges = c->n_edges;
   g->n_links = c->n_links;
@@ -677,17 +689,22 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
   for (uint32_t v = 0; v < c->n_nodes; ++v) g->name_rank[v] = c->name_rank ? c->name_rank[v] : v;
   g->gen = next_graph_gen();
   g->row_of.assign(g->n_nodes, -1);
+  mark("copy-in");
   recompute_bounds(g);
+  mark("bounds");
   build_neighbours(g);
+  mark("neighbours");
   for (uint32_t v = 0; v < g->n_nodes; ++v)
     if (n_distinct(g, v) > 0xFFFFu)
       return fail(ctx, ORH_E_UNSUPPORTED, "orh_graph_load: more than 65535 neighbours");
   g->ell_k = choose_ell_k(g);
   order_nodes(g);
+  mark("order");
   std::vector<uint2> recs;
   std::vector<uint32_t> link;
   std::vector<uint16_t> rank;
   build_layout(g, recs, link, rank);
+  mark("layout");
   const size_t nn = std::max<uint32_t>(g->n_nodes, 1);
   if (hipMalloc(&g->d_recs, recs.size() * sizeof(uint2)) != hipSuccess ||
       hipMalloc(&g->d_link, link.size() * sizeof(uint32_t)) != hipSuccess ||
@@ -710,6 +727,7 @@ int orh_graph_load(orh_graph* g, const orh_csr* c) {
                                 hipMemcpyHostToDevice, ctx->stream));
   }
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  mark("upload");
   return ORH_OK;
 }
 
