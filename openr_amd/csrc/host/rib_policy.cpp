@@ -37,9 +37,8 @@ bool RibPolicyStatement::match(const RibUnicastEntry& route) const {  // RibPoli
 
 bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidated) const {
   if (!match(route)) return false;  // RibPolicy.cpp:108-161
-  NextHopSet out;
-  for (const auto& nh : route.nexthops) {
-    // precedence: neighbour weight, then area weight, then default weight
+  // precedence: neighbour weight, then area weight, then default weight
+  auto weightOf = [&](const NextHopThrift& nh) {
     int32_t w = action_.defaultWeight;
     if (nh.area) {
       auto it = action_.areaToWeight.find(*nh.area);
@@ -49,15 +48,30 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidat
       auto it = action_.neighborToWeight.find(*nh.neighborNodeName);
       if (it != action_.neighborToWeight.end()) w = it->second;
     }
-    if (w > 0) {
-      NextHopThrift n = nh;
-      n.weight = w;
-      out.insert(std::move(n));
+    return w;
+  };
+  bool any = false;
+  for (const auto& nh : route.nexthops) {
+    if (weightOf(nh) > 0) {
+      any = true;
+      break;
     }
   }
-  if (out.empty()) {  // every nexthop dropped: keep the route as it was
+  if (!any) {  // every nexthop dropped: keep the route as it was
     if (invalidated) ++*invalidated;
     return false;
+  }
+  // the kept nexthops move into the new set as nodes (the weight is part of
+  // the hash, so it is set between extract and insert): no copies of their
+  // strings, no allocations
+  NextHopSet out;
+  out.reserve(route.nexthops.size());
+  while (!route.nexthops.empty()) {
+    auto node = route.nexthops.extract(route.nexthops.begin());
+    const int32_t w = weightOf(node.value());
+    if (w <= 0) continue;
+    node.value().weight = w;
+    out.insert(std::move(node));
   }
   route.nexthops = std::move(out);
   return true;
