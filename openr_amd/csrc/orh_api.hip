@@ -77,6 +77,7 @@ struct orh_ctx {
   // ORH_WHATIF_REPAIR: 0 off, 1 automatic (sources repeat, small ignore
   // sets), 2 every ignore-set batch the repair can take
   int repair_mode = 1;
+  uint32_t rep_cap_a = 0, rep_cap_e = 0;  // LDS repair caps; 0 = by graph size (ORH_REPAIR_CAPS=A,E)
 };
 
 struct orh_graph {
@@ -515,6 +516,13 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
   if (const char* e = getenv("ORH_SPF_MODE")) ctx->spf_mode = static_cast<orh::SpfMode>(atoi(e) % orh::kSpfModes);
   if (const char* e = getenv("ORH_DELTA_PCT")) ctx->delta_pct = std::max(1, atoi(e));
   if (const char* e = getenv("ORH_WHATIF_REPAIR")) ctx->repair_mode = atoi(e);
+  if (const char* e = getenv("ORH_REPAIR_CAPS")) {
+    unsigned ca = 0, ce = 0;
+    if (sscanf(e, "%u,%u", &ca, &ce) == 2 && ca >= 64 && ce >= 256) {
+      ctx->rep_cap_a = ca;
+      ctx->rep_cap_e = ce;
+    }
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
@@ -1031,7 +1039,22 @@ static int ensure_rev(orh_graph* g) {
   return ORH_OK;
 }
 
-constexpr uint32_t kRepairCapA = 1024, kRepairCapE = 4096;
+// LDS caps of the repair pass: 2,048 nodes / 8,192 edges when that state fits
+// the LDS (C4 what-if 2.05 -> 1.93 ms against 1,024 / 4,096: fewer requests
+// fall through to the global-slot pass), else 1,024 / 4,096
+static void repair_caps(const orh_ctx* ctx, uint32_t n_nodes, uint32_t* cap_a, uint32_t* cap_e) {
+  if (ctx->rep_cap_a) {
+    *cap_a = ctx->rep_cap_a;
+    *cap_e = ctx->rep_cap_e;
+  } else if (orh::repair_lds_bytes(n_nodes, 2048, 8192) <= ctx->lds_limit) {
+    *cap_a = 2048;
+    *cap_e = 8192;
+  } else {
+    *cap_a = 1024;
+    *cap_e = 4096;
+  }
+}
+
 constexpr uint32_t kRepairSlots = 64;       // second pass: whole-graph state in global memory
 constexpr size_t kRepairSlotBudget = 1ull << 30;  // bytes for all slots
 constexpr uint32_t kRepairMaxIgnore = 8;  // link-failure sets; KSP2 k = 2 sets are whole paths
@@ -1042,7 +1065,9 @@ static bool repair_eligible(const orh_graph* g, const orh_spf_request* req, uint
                             uint64_t bound, bool uniform) {
   const orh_ctx* ctx = g->ctx;
   if (ctx->repair_mode == 0 || words != 1 || !req->h_ignore_ptr) return false;
-  if (orh::repair_lds_bytes(g->n_nodes, kRepairCapA, kRepairCapE) > ctx->lds_limit) return false;
+  uint32_t cap_a = 0, cap_e = 0;
+  repair_caps(ctx, g->n_nodes, &cap_a, &cap_e);
+  if (orh::repair_lds_bytes(g->n_nodes, cap_a, cap_e) > ctx->lds_limit) return false;
   const orh::SpfPlan fp = orh::plan_spf(g->n_nodes, uniform, bound, g->ell_k, ctx->lds_limit, false,
                                         orh::SpfMode::kGlobal);
   if (fp.variant == orh::SpfVariant::kUnsupported) return false;
@@ -1172,8 +1197,7 @@ static int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist
   ra.n_nodes = N;
   ra.n_req = n_src;
   ra.use_link_metric = req->use_link_metric;
-  ra.cap_a = kRepairCapA;
-  ra.cap_e = kRepairCapE;
+  repair_caps(ctx, g->n_nodes, &ra.cap_a, &ra.cap_e);
   ra.recs = g->d_recs;
   ra.link = g->d_link;
   ra.rank_out = g->d_rank_out;
