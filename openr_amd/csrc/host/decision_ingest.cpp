@@ -29,15 +29,15 @@ KvValue readValue(Reader& r) {  // Types.thrift:555-605
   int16_t id;
   Type t;
   while (r.field(&id, &t)) {
-    switch (id) {
-      case 1: v.version = r.i64(); break;
-      case 3: v.originatorId = r.binary(); break;
-      case 2: v.value = r.binary(); break;
-      case 4: v.ttl = r.i64(); break;
-      case 5: v.ttlVersion = r.i64(); break;
-      case 6: v.hash = r.i64(); break;
-      default: r.skip(t);
-    }
+    // (id, type) must both match; a known id with another type is skipped
+    // like an unknown field
+    if (id == 1 && t == compact::kI64) v.version = r.i64();
+    else if (id == 3 && t == compact::kBinary) v.originatorId = r.binary();
+    else if (id == 2 && t == compact::kBinary) v.value = r.binary();
+    else if (id == 4 && t == compact::kI64) v.ttl = r.i64();
+    else if (id == 5 && t == compact::kI64) v.ttlVersion = r.i64();
+    else if (id == 6 && t == compact::kI64) v.hash = r.i64();
+    else r.skip(t);
   }
   r.structEnd();
   return v;
@@ -84,7 +84,6 @@ Publication publicationFromCompact(const std::string& bytes) {
       r.mapBegin(&kt, &vt, &n);
       if (n && (kt != compact::kBinary || vt != compact::kStruct))
         throw std::invalid_argument("compact: keyVals is not map<string, Value>");
-      p.keyVals.reserve(n);
       for (uint32_t i = 0; i < n; ++i) {
         std::string key = r.binary();
         p.keyVals[std::move(key)] = readValue(r);

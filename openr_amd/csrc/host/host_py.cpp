@@ -806,6 +806,16 @@ PYBIND11_MODULE(_openr_host, m) {
     }
     return py::bytes(publicationToCompact(p));
   });
+  // (area, {key: (version, originatorId, value bytes | None, ttl, ttlVersion)}, expiredKeys)
+  m.def("publication_from_compact", [](py::bytes b) {
+    const Publication p = publicationFromCompact(std::string(b));
+    py::dict kv;
+    for (const auto& [k, v] : p.keyVals)
+      kv[py::str(k)] = py::make_tuple(v.version, v.originatorId,
+                                      v.value ? py::object(py::bytes(*v.value)) : py::object(py::none()),
+                                      v.ttl, v.ttlVersion);
+    return py::make_tuple(p.area, kv, p.expiredKeys);
+  });
   m.def("parse_prefix_key", [](const std::string& key) -> py::object {  // PrefixKey::fromStr
     auto k = parsePrefixKey(key);
     if (!k) return py::none();

@@ -226,10 +226,14 @@ std::vector<std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
   // KSP2 prefixes may trace paths lazily (memo writes): one prefix at a time
   const bool hasKsp = ps.ksp2Entries() > 0;
   bool dev = false;
-  if (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64) {
+  auto& pool = WorkerPool::instance();
+  const bool parallel = !hasKsp && prefixes.size() >= 64 && pool.size() > 1;
+  // the memoized rows of `me` are filled here, on this thread: the pool's
+  // workers below only read them (a cold getSpfRow flushes the mirror and
+  // inserts into the memo, which is not synchronised)
+  if (parallel || (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64))
     for (const auto& [_, ls] : als) ls.getSpfRow(me);
-    dev = selectOnDevice(me, als, ps);
-  }
+  if (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64) dev = selectOnDevice(me, als, ps);
   auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
     auto it = staticUnicastRoutes_.find(p);
     if (it == staticUnicastRoutes_.end()) return std::nullopt;
@@ -258,8 +262,7 @@ std::vector<std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
     }
     out[i] = staticRoute(p);
   };
-  auto& pool = WorkerPool::instance();
-  if (!hasKsp && prefixes.size() >= 64 && pool.size() > 1) {
+  if (parallel) {
     pool.parallelFor(prefixes.size(), [&](size_t, size_t b, size_t e) {
       for (size_t i = b; i < e; ++i) one(i);
     });

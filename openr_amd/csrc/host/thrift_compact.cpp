@@ -64,7 +64,9 @@ void Reader::listBegin(Type* elem, uint32_t* n) {
   const uint8_t h = byte();
   *elem = static_cast<Type>(h & 0x0F);
   const uint32_t s = h >> 4;
-  *n = s == 15 ? static_cast<uint32_t>(varint()) : s;
+  const uint64_t c = s == 15 ? varint() : s;
+  if (c > remaining()) throw std::invalid_argument("compact: list size beyond the input");
+  *n = static_cast<uint32_t>(c);
 }
 
 void Reader::skip(Type t) {
@@ -85,12 +87,17 @@ void Reader::skip(Type t) {
       return;
     }
     case kMap: {
-      const uint32_t n = static_cast<uint32_t>(varint());
-      if (!n) return;
-      const uint8_t kv = byte();
+      Type k, v;
+      uint32_t n;
+      mapBegin(&k, &v, &n);
+      // a bool inside a map is a one-byte value, as in a list
+      auto elem = [this](Type e) {
+        if (e == kTrue || e == kFalse) byte();
+        else skip(e);
+      };
       for (uint32_t i = 0; i < n; ++i) {
-        skip(static_cast<Type>(kv >> 4));
-        skip(static_cast<Type>(kv & 0x0F));
+        elem(k);
+        elem(v);
       }
       return;
     }
@@ -353,8 +360,13 @@ PrefixEntry readPrefixEntry(Reader& r, std::vector<std::string>* areaStack) {  /
     }
   }
   r.structEnd();
-  // the reference keys prefixes by the masked network (folly::CIDRNetwork)
+  // toIPNetwork (folly createNetwork) throws on a malformed CIDR, and
+  // Decision counts the entry as failed to deserialise: same rule as parseCidr
   const size_t nb = p.addr.size();
+  if ((nb != 4 && nb != 16) || p.len < 0 || p.len > static_cast<int>(8 * nb))
+    throw std::invalid_argument("compact: malformed prefix (address of " + std::to_string(nb) +
+                                " bytes, length " + std::to_string(p.len) + ")");
+  // the reference keys prefixes by the masked network (folly::CIDRNetwork)
   for (size_t i = 0; i < nb; ++i) {
     const int keep = std::clamp(p.len - static_cast<int>(8 * i), 0, 8);
     p.addr[i] = static_cast<char>(static_cast<uint8_t>(p.addr[i]) & static_cast<uint8_t>(0xFF00u >> keep));
@@ -494,7 +506,6 @@ AdjacencyDatabase adjacencyDatabase(const std::string& bytes) {  // Types.thrift
         uint32_t n;
         r.listBegin(&e, &n);
         expect(e, kStruct, "adjacencies element");
-        db.adjacencies.reserve(n);
         for (uint32_t i = 0; i < n; ++i) db.adjacencies.push_back(readAdjacency(r));
         break;
       }
@@ -523,9 +534,11 @@ PrefixDatabase prefixDatabase(const std::string& bytes) {  // Types.thrift:431-4
         uint32_t n;
         r.listBegin(&e, &n);
         expect(e, kStruct, "prefixEntries element");
-        db.prefixEntries.reserve(n);
-        db.areaStacks.assign(n, {});
-        for (uint32_t i = 0; i < n; ++i) db.prefixEntries.push_back(readPrefixEntry(r, &db.areaStacks[i]));
+        // containers grow as elements parse (the count is peer-supplied)
+        for (uint32_t i = 0; i < n; ++i) {
+          db.areaStacks.emplace_back();
+          db.prefixEntries.push_back(readPrefixEntry(r, &db.areaStacks.back()));
+        }
         break;
       }
       case 5: db.deletePrefix = readBool(t); break;

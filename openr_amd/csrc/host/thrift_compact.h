@@ -84,7 +84,13 @@ class Reader {
  public:
   explicit Reader(const std::string& b) : p_(reinterpret_cast<const uint8_t*>(b.data())), e_(p_ + b.size()) {}
   Reader(const uint8_t* p, size_t n) : p_(p), e_(p + n) {}
-  void structBegin() { last_.push_back(0); }
+  // nesting bound: peer-supplied bytes must not drive skip() into unbounded
+  // recursion (fbthrift rejects such input as a deserialisation error)
+  static constexpr size_t kMaxDepth = 64;
+  void structBegin() {
+    if (last_.size() >= kMaxDepth) throw std::invalid_argument("compact: nesting too deep");
+    last_.push_back(0);
+  }
   void structEnd() { last_.pop_back(); }
   // next field header: false at the stop field; bool values arrive in the type
   bool field(int16_t* id, Type* t);
@@ -99,11 +105,15 @@ class Reader {
     return *p_++;
   }
   std::string binary();
-  // list header: element type and size
+  // list header: element type and size (every element takes at least one
+  // byte, so a count beyond the remaining input is rejected before any
+  // container is sized from it)
   void listBegin(Type* elem, uint32_t* n);
   // map header: key / value types (unset when empty) and size
   void mapBegin(Type* key, Type* val, uint32_t* n) {
-    *n = static_cast<uint32_t>(varint());
+    const uint64_t c = varint();
+    if (c > remaining()) throw std::invalid_argument("compact: map size beyond the input");
+    *n = static_cast<uint32_t>(c);
     *key = *val = kStop;
     if (*n) {
       const uint8_t kv = byte();
@@ -114,6 +124,7 @@ class Reader {
   // skip a value of type t (unknown fields)
   void skip(Type t);
   bool atEnd() const { return p_ == e_; }
+  size_t remaining() const { return static_cast<size_t>(e_ - p_); }
 
  private:
   void need(size_t n) const {

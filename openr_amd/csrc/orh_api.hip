@@ -474,6 +474,12 @@ bool wide_metrics(const orh_graph* g) {
   return g->sum_max_metric / 2 + g->max_metric >= 0xFFFFFFFFull;
 }
 
+// a staged request is reused when the stored key is this request's key
+// followed by `extra` words of staging offsets
+bool staged_key_matches(const std::vector<uint32_t>& stored, const std::vector<uint32_t>& key, size_t extra) {
+  return stored.size() == key.size() + extra && std::equal(key.begin(), key.end(), stored.begin());
+}
+
 int ensure_ms_lvl(orh_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->d_ms_lvl_cap) return ORH_OK;
   hipFree(ctx->d_ms_lvl);
@@ -1130,7 +1136,8 @@ static int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist
   key.insert(key.end(), req->h_ignore_links, req->h_ignore_links + n_ign);
   size_t off_src = n_src, off_ip = 2 * size_t{n_src}, off_ign = off_ip + n_src + 1, off_cp = 0, off_flags = 0,
          off_cuts = 0;
-  if (key != ctx->rep_key) {
+  // the stored key carries the three staging offsets after the request key
+  if (!staged_key_matches(ctx->rep_key, key, 3)) {
     std::vector<uint32_t> st(base_row);
     st.insert(st.end(), req->h_srcs, req->h_srcs + n_src);
     std::vector<uint32_t> ign_ptr(1, 0), ign, cut_ptr(1, 0), cuts;
@@ -1327,7 +1334,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // staged layout: srcs[n_rows] | ign_ptr[n_rows+1] ign[..] | nbr_ptr[n_src+1] nbr_row[..]
   uint32_t n_rows = n_src;
   size_t off_ign_ptr = 0, off_ign = 0, off_nbr_ptr = 0, off_nbr_row = 0, off_order = 0;
-  if (key != g->req_key) {
+  // the stored key carries six staging offsets after the request key
+  if (!staged_key_matches(g->req_key, key, 6)) {
     std::vector<uint32_t> srcs(req->h_srcs, req->h_srcs + n_src), nbr_ptr(n_src + 1, 0), nbr_row;
     std::vector<uint32_t> ign_ptr, ign;
     std::vector<uint32_t> row_owner;  // source index whose ignore set a row uses

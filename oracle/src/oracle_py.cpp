@@ -420,11 +420,16 @@ PYBIND11_MODULE(openr_oracle, m) {
            })
       .def("spf_tables",
            [](const LinkState& s, std::vector<std::string> srcs, std::vector<std::string> order,
-              std::vector<std::vector<std::string>> nbrs, int threads) {
+              std::vector<std::vector<std::string>> nbrs, int threads,
+              std::vector<std::vector<std::tuple<std::string, std::string, std::string>>> ignores) {
              // dist [S][N] (u32, 0xFFFFFFFF = absent) in `order`, and nexthop
              // sets as bitmasks [S][N][W] over each source's `nbrs` list;
-             // runSpf per source on per-thread LinkState copies
+             // runSpf(src, true, ignores[i]) per source on per-thread LinkState
+             // copies (ignores: per source a list of link descriptors
+             // (n1, if1, n2), or empty = no ignore sets)
              if (nbrs.size() != srcs.size()) throw std::invalid_argument("one nbr list per source");
+             if (!ignores.empty() && ignores.size() != srcs.size())
+               throw std::invalid_argument("one ignore list per source");
              const size_t S = srcs.size(), N = order.size();
              size_t W = 1;
              for (const auto& l : nbrs) W = std::max(W, (l.size() + 31) / 32);
@@ -455,7 +460,22 @@ PYBIND11_MODULE(openr_oracle, m) {
                      uint32_t* m = pn + i * N * W;
                      std::fill(d, d + N, 0xFFFFFFFFu);
                      std::fill(m, m + N * W, 0u);
-                     for (const auto& [name, r] : copies[t].runSpf(srcs[i], true)) {
+                     LinkSet ign;
+                     if (!ignores.empty()) {
+                       for (const auto& [n1, if1, n2] : ignores[i]) {
+                         bool found = false;
+                         for (const auto& link : copies[t].linksFromNode(n1))
+                           if (link->getIfaceFromNode(n1) == if1 && link->getOtherNodeName(n1) == n2) {
+                             ign.insert(link);
+                             found = true;
+                           }
+                         if (!found) {
+                           errs[t] = "ignored link " + n1 + "/" + if1 + " not found";
+                           return;
+                         }
+                       }
+                     }
+                     for (const auto& [name, r] : copies[t].runSpf(srcs[i], true, ign)) {
                        auto c = col.find(name);
                        if (c == col.end()) {
                          errs[t] = "node " + name + " not in order";
@@ -481,7 +501,8 @@ PYBIND11_MODULE(openr_oracle, m) {
              if (!err.empty()) throw std::runtime_error("spf_tables: " + err);
              return py::make_tuple(dist, nh);
            },
-           py::arg("srcs"), py::arg("order"), py::arg("nbrs"), py::arg("threads") = 8)
+           py::arg("srcs"), py::arg("order"), py::arg("nbrs"), py::arg("threads") = 8,
+           py::arg("ignores") = std::vector<std::vector<std::tuple<std::string, std::string, std::string>>>{})
       .def("time_spf_sources",
            [](const LinkState& s, std::vector<std::string> srcs, int threads) {
              // Timed all-sources SPF: one LinkState copy per thread (the memo is

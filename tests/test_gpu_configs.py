@@ -61,19 +61,32 @@ def _sweep_tables(ls_h, ls_o, names, check, threads=16):
     return info
 
 
-def test_c2_sweep_first_hops_exact(hip, oracle):
-    """The bench's own sweep (C2, all 10,000 sources in one launch), with
-    dist rows and first-hop masks of 300 sources compared in full: the four
-    corners, the edges' midpoints, the centre and 291 seeded others."""
+@pytest.mark.parametrize("variant", [0, 1, 7])
+def test_c2_sweep_first_hops_exact(hip, oracle, variant):
+    """The bench's own sweeps (C2, all 10,000 sources in one launch): the
+    grid itself (variant 0) and two of the timed what-if variants (the grid
+    with one seeded link drained, bench.drain_what_if_link: SKIP records in
+    the MS-BFS and in first_hop_lvl_kernel<16>). Dist rows and first-hop
+    masks of 300 sources compared in full: the four corners, the edges'
+    midpoints, the centre, both ends of the drained link and their
+    neighbours, and seeded others."""
+    from bench import drain_what_if_link
     n = 100
     adj_dbs, _ = bench_grid(n)
+    special = [0, n - 1, n * (n - 1), n * n - 1, n // 2, n * (n // 2), n * (n // 2) + n - 1,
+               n * (n - 1) + n // 2, n * (n // 2) + n // 2]
+    if variant:
+        drained = drain_what_if_link(adj_dbs, n, variant)
+        assert drained and all(a.isOverloaded for a in drained)
+        ends = {int(a.otherNodeName) for a in drained}
+        for e in sorted(ends):
+            special += [e] + [int(x.otherNodeName) for x in adj_dbs[e].adjacencies]
+        special = list(dict.fromkeys(special))
     als_h, _ = load_topology(hip, adj_dbs, [])
     als_o, _ = load_topology(oracle, adj_dbs, [])
     names = [str(i) for i in range(n * n)]
-    special = [0, n - 1, n * (n - 1), n * n - 1, n // 2, n * (n // 2), n * (n // 2) + n - 1,
-               n * (n - 1) + n // 2, n * (n // 2) + n // 2]
-    rng = random.Random(22)
-    check = special + rng.sample([i for i in range(n * n) if i not in special], 291)
+    rng = random.Random(22 + variant)
+    check = special + rng.sample([i for i in range(n * n) if i not in special], 300 - len(special))
     info = _sweep_tables(als_h[A], als_o[A], names, check)
     assert info["variant"] == MSBFS and info["mask_bits"] == 32, info
     assert info["batch_sources"] == 32, info

@@ -314,3 +314,38 @@ def test_rebuild_routes_incremental(hip, oracle):
     got = RouteDb.from_wire(rib.route_db())
     assert got.canonical_full() == RouteDb.from_wire(fresh.route_db()).canonical_full()
     assert any(nh.weight == 2 for r in got.unicastRoutes.values() for nh in r.nextHops)
+
+
+def test_hostile_publication_values_counted_as_errors(hip, oracle):
+    """Peer-supplied values the decoders reject (list count beyond the input,
+    201 nested structs in an unknown field, a prefix of 129 bits) are counted
+    as errors ("Failed to deserialize", Decision.cpp:1785-1788) and change
+    nothing; the valid keys of the same publication still apply."""
+    mod = hip.module
+    dbs = random_topology(6100, n=12, extra=16, max_metric=5)
+    for db in dbs:
+        db.area = AREA
+    als_h = hip.area_link_states()
+    ps_h = hip.prefix_state()
+    ingest = mod.DecisionIngest(dbs[0].thisNodeName, False)
+    kv = {f"adj:{db.thisNodeName}": (1, db.thisNodeName, mod.adj_db_to_compact(db.to_wire()), 3600000, 1)
+          for db in dbs}
+    huge = b"\xff\xff\xff\xff\x0f"
+    good = create_prefix_entry(IpPrefix.of("fd00:1::/64"))
+    bad = create_prefix_entry(IpPrefix.of("fd00:2::/64"))
+    bad.prefix = IpPrefix(bad.prefix.prefixAddress, 129)
+    node = dbs[3].thisNodeName
+    adj = mod.adj_db_to_compact(dbs[4].to_wire())
+    kv.update({
+        _prefix_key(node, good): (1, node, mod.prefix_db_to_compact(node, AREA, [good.to_wire()]), 3600000, 1),
+        f"prefix:{node}:{AREA}:[fd00:3::/64]": (1, node, b"\x18\x01a\x29\xfc" + huge, 3600000, 1),
+        f"prefix:{node}:{AREA}:[fd00:2::/64]": (1, node, mod.prefix_db_to_compact(node, AREA, [bad.to_wire()]),
+                                                3600000, 1),
+        "adj:deep": (1, "x", adj[:-1] + b"\xec" + b"\x1c" * 200 + b"\x00" * 202, 3600000, 1),
+    })
+    ingest.process_publication(mod.publication_to_compact(AREA, kv, []), als_h._impl, ps_h._impl)
+    st = ingest.stats()
+    assert st["error"] == 3 and st["adj_db_update"] == len(dbs) and st["prefix_db_update"] == 1
+    als_o, ps_o = load_topology(oracle, dbs, [(node, AREA, good)])
+    for me in sorted(db.thisNodeName for db in dbs)[:4]:
+        assert _routes(hip, als_h._impl, ps_h._impl, me) == _routes(oracle, als_o._impl, ps_o._impl, me), me

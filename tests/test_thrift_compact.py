@@ -20,7 +20,7 @@ from compact_decode import decode
 from openr_amd import host_module
 from openr_amd.facade import load_topology
 from openr_amd.topology import bench_grid
-from openr_amd.types import (IpPrefix, K_TESTING_AREA, PrefixForwardingAlgorithm,
+from openr_amd.types import (BinaryAddress, IpPrefix, K_TESTING_AREA, PrefixForwardingAlgorithm,
                              PrefixForwardingType, PrefixMetrics, create_prefix_entry)
 
 from test_gpu_parity import random_topology
@@ -208,3 +208,61 @@ def test_prefix_database_round_trip(mod):
         assert entries == [w] and got_stacks == (stacks or [[]])
     with pytest.raises(ValueError):
         mod.prefix_db_from_compact(b"\x18\x05ab")  # truncated
+
+
+# ---- hostile input (the decoders run on peer-supplied publication bytes) ----
+
+def _insert_before_stop(data, extra):
+    assert data[-1:] == b"\x00"
+    return data[:-1] + extra + b"\x00"
+
+
+def test_oversized_counts_rejected_before_allocation(mod):
+    """A list / map count beyond the remaining bytes is a decode error, not a
+    multi-GB container reservation (fbthrift rejects it the same way)."""
+    huge = b"\xff\xff\xff\xff\x0f"  # varint 2^32 - 1
+    with pytest.raises(ValueError, match="beyond the input"):
+        mod.prefix_db_from_compact(b"\x18\x01a" + b"\x29\xfc" + huge)  # prefixEntries: list<struct>
+    with pytest.raises(ValueError, match="beyond the input"):
+        mod.adj_db_from_compact(b"\x18\x01a" + b"\x29\xfc" + huge)  # adjacencies
+    db = bench_grid(2, 0)[0][0]
+    data = mod.adj_db_to_compact(db.to_wire())
+    with pytest.raises(ValueError, match="beyond the input"):  # unknown map field, huge count
+        mod.adj_db_from_compact(_insert_before_stop(data, b"\xeb" + huge + b"\x51"))
+    pub = mod.publication_to_compact("A", {"k": (1, "o", b"v", 10, 1)}, ["x"])
+    assert mod.publication_from_compact(pub) == ("A", {"k": (1, "o", b"v", 10, 1)}, ["x"])
+    with pytest.raises(ValueError):
+        mod.publication_from_compact(b"\x2b" + huge + b"\x8c")  # keyVals map<string, Value>
+
+
+def test_nesting_depth_limited(mod):
+    db = bench_grid(2, 0)[0][0]
+    data = mod.adj_db_to_compact(db.to_wire())
+    deep = b"\xec" + b"\x1c" * 200 + b"\x00" * 201  # unknown field 20: 201 nested structs
+    with pytest.raises(ValueError, match="nesting"):
+        mod.adj_db_from_compact(_insert_before_stop(data, deep))
+    shallow = b"\xec" + b"\x1c" * 8 + b"\x00" * 9
+    assert mod.adj_db_from_compact(_insert_before_stop(data, shallow)) == db.to_wire()
+
+
+def test_skip_map_of_bools(mod):
+    """An unknown map<i32, bool> field: each bool is a one-byte value, so the
+    fields after it must still decode."""
+    db = bench_grid(2, 0)[0][0]
+    w = db.to_wire()
+    data = mod.adj_db_to_compact(w)
+    m = b"\xeb" + b"\x02\x51" + b"\x02\x01" + b"\x04\x02"  # field 20 map<i32,bool>{1: true, 2: false}
+    assert mod.adj_db_from_compact(_insert_before_stop(data, m)) == w
+    # an unknown scalar field after the map
+    assert mod.adj_db_from_compact(_insert_before_stop(data, b"\xe5\x06")) == w  # field 20 i32 3
+
+
+def test_malformed_prefix_rejected(mod):
+    """toIPNetwork throws on an address that is neither 4 nor 16 bytes or a
+    length outside [0, 8 * size]; the entry is a decode error."""
+    for addr, length in ((bytes(16), 129), (bytes(4), 33), (bytes(16), -1), (bytes(5), 8)):
+        e = create_prefix_entry(IpPrefix.of("fd00::/64"))
+        e.prefix = IpPrefix(BinaryAddress(addr), length)
+        data = mod.prefix_db_to_compact("n", "A", [e.to_wire()])
+        with pytest.raises(ValueError, match="malformed prefix"):
+            mod.prefix_db_from_compact(data)
