@@ -105,55 +105,76 @@ def leg_c3(hip, cpu):
     return out
 
 
-def leg_c4(hip, cpu, n_links=64, n_srcs=16, n_ksp=256):
+def leg_c4(hip, cpu, reps=3):
+    """C4 at BASELINE.md's shape: 4,096 links x 64 sources = 262,144
+    runSpf(src, true, {link}) as one what-if job (64 plain searches, then the
+    requests in chunks of 4,096 into one device row buffer: every request's
+    full dist + first-hop row is written to HBM, chunk after chunk), and 1,024
+    KSP2 (src, dst) pairs."""
     from openr_amd.facade import load_topology
     from openr_amd.types import K_TESTING_AREA as A
-    from openr_amd.workloads import c4_ksp2_pairs, c4_wan, c4_what_if_pairs
+    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan, c4_what_if_job
     adj, _ = c4_wan()
     als, _ = load_topology(hip, adj, [])
     ls = als[A]._impl
     names = ls.node_names()
-    lids = [lid for lid, _ in ls.link_ids()]
-    pairs = c4_what_if_pairs(lids, names, n_links, n_srcs)
-    sweep = ls.what_if_sweep([s for s, _ in pairs], [[l] for _, l in pairs])
-    sweep.run()
-    sweep.sync()
-    t0 = time.perf_counter()
-    for _ in range(3):
-        sweep.run()
-    sweep.sync()
-    dt = (time.perf_counter() - t0) / 3
-    sweep.run()
-    dev_ms = sweep.last_ms()  # HIP events around the base searches + repair
-    info = sweep.info()
-    n_nodes, n_edges = sweep.nodes, sweep.edges
+    links = ls.link_ids()
+    srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
+    batch = ls.what_if_batch(srcs, idx, sets, 4096)
+    batch.run()
+    batch.sync()
+    walls, devs = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        batch.run()
+        batch.sync()
+        walls.append(time.perf_counter() - t0)
+        devs.append(batch.last_ms())
+    dt, dev_ms = statistics.median(walls), statistics.median(devs)
+    info = batch.info()
+    n_req = len(idx)
+    n_nodes, n_edges = batch.nodes, batch.edges
     # SURVEY.md §8d: per what-if SPF the same B_spf as a plain source
-    b_spf = 4 * (n_nodes + 1) + 8 * n_edges + n_nodes * (4 + 4 * sweep.words)
-    kp = c4_ksp2_pairs(names, n_ksp)
+    b_spf = 4 * (n_nodes + 1) + 8 * n_edges + n_nodes * (4 + 4)
+    out_bytes = n_req * n_nodes * 8  # the rows alone (the output floor)
+    tiers = {int(t): int((info & 7 == t).sum()) for t in range(5)}
+    aff = info >> 3
+    kp = c4_ksp2_pairs(names, C4_KSP2_PAIRS)
+    ls.prefetch_kth_paths(kp[:64])  # warm the mirror / pools
     t0 = time.perf_counter()
     ls.prefetch_kth_paths(kp)
     kdt = time.perf_counter() - t0
-    out = {"workload": f"C4 WAN N={len(names)} E={sweep.edges}, log-normal metrics",
-           "what_if_spfs_per_s": round(len(pairs) / dt, 1),
-           "what_if_batch": f"{len(pairs)} runSpf(src, true, {{link}}) = {n_links} links x {n_srcs} sources",
+    out = {"workload": f"C4 WAN N={len(names)} E={n_edges}, log-normal metrics",
+           "what_if_spfs_per_s": round(n_req / dt, 1),
+           "what_if_batch": (f"{n_req} runSpf(src, true, {{link}}) = {len(sets) // len(srcs)} links x "
+                             f"{len(srcs)} sources: one what-if job (the sources' plain searches + "
+                             f"{(n_req + 4095) // 4096} chunks of 4,096 requests into one device row buffer)"),
            "what_if_batch_ms": round(dt * 1e3, 3),
            "what_if_device_ms": round(dev_ms, 3),
-           "what_if_plan": (f"repair: {info['batch_sources']} plain SPFs, then copy + re-derive below "
-                            "the ignored link" if info["variant"] == 11 else f"variant {info['variant']}"),
+           "what_if_tiers": {"source_row": tiers[0], "lds_small": tiers[1], "lds_large": tiers[2],
+                             "global_slot": tiers[3], "full_search": tiers[4]},
+           "what_if_affected_nodes": {"mean": round(float(aff.mean()), 2), "max": int(aff.max())},
            "what_if_roofline": {"bound": "hbm", "bytes_per_spf": b_spf,
-                                "achieved_gbs": round(len(pairs) * b_spf / (dev_ms * 1e-3) / 1e9, 1),
-                                "frac": round(len(pairs) * b_spf / (dev_ms * 1e-3) / 1e9 / 8000.0, 4)},
-           "ksp2_pairs_per_s": round(n_ksp / kdt, 1),
-           "ksp2_batch": f"{n_ksp} (src, dst) getKthPaths k=1,2 (host trace + 2 device batches)"}
+                                "achieved_gbs": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9, 1),
+                                "frac": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9 / 8000.0, 4),
+                                "output_floor": {"bytes": out_bytes,
+                                                 "frac": round(out_bytes / (dev_ms * 1e-3) / 1e9 / 8000.0, 4)}},
+           "ksp2_pairs_per_s": round(len(kp) / kdt, 1),
+           "ksp2_batch": f"{len(kp)} (src, dst) getKthPaths k=1,2 (prefetchKthPaths)"}
     if cpu:
         o = _oracle()
         als_o, _ = load_topology(o, adj, [])
         k = 8
         threads = min(k, os.cpu_count() or 1)
-        sample = [s for s, _ in pairs[:k]]
-        sec, _ = als_o[A]._impl.time_spf_sources(sample, threads)
+        desc = dict(links)
+        pick = [i * (n_req // k) for i in range(k)]
+        q = [srcs[idx[i]] for i in pick]
+        t0 = time.perf_counter()
+        als_o[A]._impl.spf_tables(q, names, [ls.neighbors(s) for s in q], threads,
+                                  [[desc[sets[i][0]][:3]] for i in pick])
+        sec = time.perf_counter() - t0
         out["cpu_spfs_per_s"] = round(k / sec, 4)
-        out["cpu_sample"] = (f"{k} runSpf on the 50k-node WAN on {threads} threads "
+        out["cpu_sample"] = (f"{k} what-if runSpf(src, true, {{link}}) of the same batch on {threads} threads "
                              "(reference DijkstraQ re-heap), per-thread LinkState copies")
     return out
 

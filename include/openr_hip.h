@@ -254,6 +254,35 @@ int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words
 #define ORH_GRAPH_WIDE_METRIC 2u /* link-metric path sums can reach 2^32 - 1 */
 int orh_graph_flags(const orh_graph* g, uint32_t* flags);
 
+/* ---- what-if jobs (batched link-failure SPFs) ---------------------------
+ * runSpf(src, useLinkMetric, linksToIgnore) (LinkState.cpp:808-882) for many
+ * (source, ignore set) requests over a fixed source set - the C4 shape,
+ * "4,096 links x 64 sources" (SURVEY.md §8d). orh_whatif_create searches the
+ * plain rows of its sources once; every orh_whatif_run derives its requests'
+ * rows from them: a request's row is its source's row except below a tight
+ * ignored link, where it is re-derived (results are bit-identical to a fresh
+ * runSpf). A job is bound to the graph structure it was created on
+ * (ORH_E_STATE after a delta or reload). Everything is asynchronous on the
+ * context stream; one mask word per node (every source has <= 32 distinct
+ * neighbours), no zero-metric links (ORH_E_UNSUPPORTED otherwise). */
+typedef struct orh_whatif orh_whatif;
+int orh_whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t use_link_metric,
+                      orh_whatif** out_job);
+/* requests i < n_req: source h_srcs[h_src_idx[i]] of the job, ignored links
+ * h_ignore_links[h_ignore_ptr[i] .. h_ignore_ptr[i+1]) (orh_csr link ids);
+ * rows into d_dist [n_req*N] and d_nh [n_req*N] (one word per node). d_info
+ * (nullable, [n_req]): ORH_WHATIF_TIER(x) = how the row was made, and
+ * ORH_WHATIF_AFFECTED(x) = nodes re-derived (0: the source's row stands).
+ * Host arrays may be reused once the call returns. */
+int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, const uint32_t* h_ignore_ptr,
+                   const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info);
+#define ORH_WHATIF_TIER(x) ((x) & 7u) /* 0 source row, 1/2 LDS repair, 3 global-slot repair, 4 full search */
+#define ORH_WHATIF_AFFECTED(x) ((x) >> 3)
+/* device time from the job's creation (base searches) to the end of its last
+ * run (HIP events; waits for that run) */
+int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out);
+int orh_whatif_destroy(orh_whatif* job);
+
 /* ---- KSP2 (LinkState::getKthPaths, LinkState.cpp:762-791) --------------
  * For each dsts[i]: the k = 1 paths, traced (traceOnePath, :398-419) over
  * src's SPF with link metrics, then the k = 2 paths over a fresh SPF that
@@ -269,6 +298,20 @@ int orh_graph_flags(const orh_graph* g, uint32_t* flags);
  * getKthPaths(src, dst, 1 / 2) pair for a batch of destinations. */
 int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, uint32_t* out,
              size_t cap, size_t* n_words);
+
+/* Device form for a batch of (src, dst) pairs (the C4 shape: 1,024 pairs):
+ * the sources' SPFs, the k = 1 traces, the k = 2 searches (each pair's k = 1
+ * links ignored) and the k = 2 traces all run on the device; only the paths
+ * are copied back. *out_blocks points at n_pairs blocks of *block_words words
+ * in context-owned pinned memory, valid until the next call on the context:
+ *   [0] status: 0, or 1 = the pair outgrew the device trace's bounds (trace
+ *       it with orh_ksp2 / on the host)
+ *   [1] offset of the k = 2 section within the block
+ *   [2..] k = 1 section, then the k = 2 section, each as in orh_ksp2
+ * Graphs with zero-metric links or 64-bit path metrics: ORH_E_UNSUPPORTED
+ * (orh_ksp2 follows the exact kernel's extraction order there). */
+int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const uint32_t* h_dst,
+                   const uint32_t** out_blocks, uint32_t* block_words);
 
 /* ---- device prefix mirror (PrefixState) ------------------------------- */
 /* Replaces the per-prefix PrefixEntries map PrefixState::prefixes() hands to

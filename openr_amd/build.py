@@ -26,7 +26,8 @@ ARCH = os.environ.get("OPENR_HIP_ARCH", "gfx950")
 
 HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "spf_kernels.hip"),
             os.path.join(CSRC, "kernels", "route_kernels.hip"),
-            os.path.join(CSRC, "kernels", "whatif_kernels.hip")]
+            os.path.join(CSRC, "kernels", "whatif_kernels.hip"),
+            os.path.join(CSRC, "kernels", "ksp_kernels.hip")]
 HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "prefix_state.cpp", "spf_solver.cpp",
                                                    "rib_policy.cpp", "thrift_compact.cpp",
                                                    "decision_ingest.cpp", "host_py.cpp")]

@@ -393,6 +393,113 @@ class SpfSweep {
   uint32_t* dNh_{nullptr};
 };
 
+// batched link-failure what-if SPFs through a what-if job (orh_whatif_*):
+// requests (source index, ignored link ids) over a fixed source list, run in
+// chunks of `chunk` requests into one device row buffer (the C4 shape,
+// 4,096 links x 64 sources = 262,144 runSpf(src, true, {link}));
+// run() = the sources' plain searches + every chunk, asynchronously
+class WhatIfBatch {
+ public:
+  WhatIfBatch(const LinkState& ls, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
+              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric)
+      : useLinkMetric_(useLinkMetric) {
+    if (srcIdx.size() != ignore.size()) throw std::invalid_argument("WhatIfBatch: one ignore set per request");
+    if (chunk == 0) throw std::invalid_argument("WhatIfBatch: chunk must be positive");
+    for (const auto& s : srcs) {
+      auto id = ls.nodeId(s);
+      if (!id) throw std::invalid_argument("WhatIfBatch: unknown source " + s);
+      srcs_.push_back(*id);
+    }
+    for (uint32_t i : srcIdx)
+      if (i >= srcs_.size()) throw std::invalid_argument("WhatIfBatch: source index out of range");
+    srcIdx_ = srcIdx;
+    // per chunk: ignore CSR rebased to the chunk
+    const size_t n = srcIdx.size();
+    chunk_ = static_cast<uint32_t>(std::min<size_t>(chunk, std::max<size_t>(n, 1)));
+    for (size_t c0 = 0; c0 < n; c0 += chunk_) {
+      const size_t c1 = std::min(n, c0 + chunk_);
+      std::vector<uint32_t> ptr{0}, links;
+      for (size_t i = c0; i < c1; ++i) {
+        links.insert(links.end(), ignore[i].begin(), ignore[i].end());
+        ptr.push_back(static_cast<uint32_t>(links.size()));
+      }
+      if (links.empty()) links.push_back(0);  // non-null pointer
+      chunks_.push_back({c0, c1, std::move(ptr), std::move(links)});
+    }
+    graph_ = ls.deviceGraph();
+    ctx_ = ls.context();
+    orh_graph_info(graph_, &n_, &edges_);
+    const size_t rows = static_cast<size_t>(chunk_) * n_;
+    if (orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dDist_)) != ORH_OK ||
+        orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dNh_)) != ORH_OK ||
+        orh_device_alloc(ctx_, std::max<size_t>(n, 1) * 4, reinterpret_cast<void**>(&dInfo_)) != ORH_OK)
+      throw std::runtime_error("WhatIfBatch: device allocation failed");
+  }
+  ~WhatIfBatch() {
+    if (job_) orh_whatif_destroy(job_);
+    orh_device_free(ctx_, dDist_);
+    orh_device_free(ctx_, dNh_);
+    orh_device_free(ctx_, dInfo_);
+  }
+  void run() {  // asynchronous on the context stream
+    if (job_) orh_whatif_destroy(job_);
+    job_ = nullptr;
+    if (orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
+                          &job_) != ORH_OK)
+      throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
+    for (const auto& c : chunks_) {
+      const uint32_t nr = static_cast<uint32_t>(c.hi - c.lo);
+      if (orh_whatif_run(job_, nr, srcIdx_.data() + c.lo, c.ptr.data(), c.links.data(), dDist_, dNh_,
+                         dInfo_ + c.lo) != ORH_OK)
+        throw std::runtime_error(std::string("orh_whatif_run: ") + orh_last_error(ctx_));
+    }
+  }
+  double lastMs() {
+    double ms = 0;
+    if (!job_ || orh_whatif_elapsed_ms(job_, &ms) != ORH_OK) throw std::runtime_error("orh_whatif_elapsed_ms failed");
+    return ms;
+  }
+  void sync() {
+    if (orh_sync(ctx_) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
+  }
+  py::array_t<uint32_t> info() {
+    py::array_t<uint32_t> out(srcIdx_.size());
+    orh_memcpy_d2h(ctx_, out.mutable_data(), dInfo_, srcIdx_.size() * 4);
+    return out;
+  }
+  // rows of request i; only the last chunk's rows are still in the buffer
+  py::tuple fetch(size_t i) {
+    const auto& last = chunks_.back();
+    if (i < last.lo || i >= last.hi) throw std::out_of_range("WhatIfBatch.fetch: not in the last chunk");
+    const size_t r = i - last.lo;
+    py::array_t<uint32_t> dist(n_), nh(n_);
+    orh_memcpy_d2h(ctx_, dist.mutable_data(), dDist_ + r * n_, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_ + r * n_, n_ * 4ull);
+    return py::make_tuple(dist, nh);
+  }
+  size_t requests() const { return srcIdx_.size(); }
+  uint32_t chunk() const { return chunk_; }
+  uint32_t nodes() const { return n_; }
+  uint32_t edges() const { return edges_; }
+
+ private:
+  struct Chunk {
+    size_t lo, hi;
+    std::vector<uint32_t> ptr, links;
+  };
+  bool useLinkMetric_;
+  std::vector<uint32_t> srcs_, srcIdx_;
+  std::vector<Chunk> chunks_;
+  uint32_t chunk_{1};
+  orh_graph* graph_{nullptr};
+  orh_ctx* ctx_{nullptr};
+  orh_whatif* job_{nullptr};
+  uint32_t n_{0}, edges_{0};
+  uint32_t* dDist_{nullptr};
+  uint32_t* dNh_{nullptr};
+  uint32_t* dInfo_{nullptr};
+};
+
 // ---- canonical route-db digest --------------------------------------------
 // Per route: fields serialised in order (integers little-endian, strings and
 // lists length-prefixed, optionals with a presence byte, nexthops sorted by
@@ -703,6 +810,13 @@ PYBIND11_MODULE(_openr_host, m) {
              return new SpfSweep(s, srcs, true, &ignore);
            },
            py::keep_alive<0, 1>())
+      .def("what_if_batch",  // a what-if job over `srcs`: request i = (srcs[src_idx[i]], ignore[i])
+           [](const LinkState& s, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
+              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric) {
+             return new WhatIfBatch(s, srcs, srcIdx, ignore, chunk, useLinkMetric);
+           },
+           py::arg("srcs"), py::arg("src_idx"), py::arg("ignore"), py::arg("chunk") = 4096,
+           py::arg("use_link_metric") = true, py::return_value_policy::take_ownership, py::keep_alive<0, 1>())
       .def("run_spf_batch",
            [](const LinkState& s, const std::vector<std::string>& srcs,
               const std::vector<std::vector<uint32_t>>& ignore, bool useLinkMetric) {
@@ -727,6 +841,9 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("prefetch_spf_results", &LinkState::prefetchSpfResults, py::arg("nodes"),
            py::arg("use_link_metric") = true)
       .def("prefetch_kth_paths", &LinkState::prefetchKthPaths)
+      .def("ksp_stats", [](const LinkState& s) {  // pairs traced on the device / host
+        return py::make_tuple(s.kspDevicePairs_, s.kspHostPairs_);
+      })
       .def("spf_words",  // first-hop mask words a batch over these sources needs
            [](const LinkState& s, const std::vector<std::string>& srcs) {
              std::vector<uint32_t> ids;
@@ -759,6 +876,17 @@ PYBIND11_MODULE(_openr_host, m) {
       .def_property_readonly("nodes", &SpfSweep::nodes)
       .def_property_readonly("edges", &SpfSweep::edges)
       .def_property_readonly("sources", &SpfSweep::sources);
+
+  py::class_<WhatIfBatch>(m, "WhatIfBatch")
+      .def("run", &WhatIfBatch::run)
+      .def("last_ms", &WhatIfBatch::lastMs)
+      .def("sync", &WhatIfBatch::sync)
+      .def("info", &WhatIfBatch::info)
+      .def("fetch", &WhatIfBatch::fetch)
+      .def_property_readonly("requests", &WhatIfBatch::requests)
+      .def_property_readonly("chunk", &WhatIfBatch::chunk)
+      .def_property_readonly("nodes", &WhatIfBatch::nodes)
+      .def_property_readonly("edges", &WhatIfBatch::edges);
 
   // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
   // ---- thrift Compact wire -----------------------

@@ -277,6 +277,7 @@ void LinkState::invalidate(bool topologyChanged) {
     spfResults_.clear();
     spfMaps_.clear();
     kthPaths_.clear();
+    countedOnDevice_.clear();
   }
 }
 
@@ -701,6 +702,85 @@ void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes,
 }
 
 void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const {
+  // the whole batch on the device (orh_ksp2_batch: k = 1 rows and traces, k = 2
+  // searches and traces); only the paths come back. Graphs that need the
+  // exact kernel's extraction order, unknown nodes and pairs that outgrow the
+  // device trace's bounds take the host path below.
+  KspProf prof;
+  std::vector<const std::pair<std::string, std::string>*> dev;
+  std::vector<std::pair<std::string, std::string>> host;
+  std::vector<uint32_t> hs, hd;
+  {
+    std::set<std::pair<std::string, std::string>> seen;
+    for (const auto& pr : pairs) {
+      if (!seen.insert(pr).second) continue;
+      const bool m1 = kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{1})) != 0;
+      const bool m2 = kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{2})) != 0;
+      if (m1 && m2) continue;
+      auto s = nodeId(pr.first);
+      auto d = nodeId(pr.second);
+      if (!s || !d || m1 || m2) {  // partly memoized, or the reference's unknown-node results
+        host.push_back(pr);
+        continue;
+      }
+      dev.push_back(&pr);
+      hs.push_back(*s);
+      hd.push_back(*d);
+    }
+  }
+  // ORH_KSP_HOST=1: host traces over device rows for every pair (A/B, tests)
+  if (const char* e = getenv("ORH_KSP_HOST"); e && *e == '1') {
+    for (const auto* pr : dev) host.push_back(*pr);
+    dev.clear();
+  }
+  if (!dev.empty()) {
+    flushMirror();
+    const uint32_t* blocks = nullptr;
+    uint32_t bw = 0;
+    const int rc = orh_ksp2_batch(graph_, static_cast<uint32_t>(dev.size()), hs.data(), hd.data(), &blocks, &bw);
+    if (rc == ORH_E_UNSUPPORTED) {
+      for (const auto* pr : dev) host.push_back(*pr);
+    } else {
+      check(ctx_, rc, "orh_ksp2_batch");
+      prof.mark("device batch");
+      // spf_runs the reference's way: one per source not yet memoized
+      // (getSpfResult), one per pair with k = 1 paths (runSpf ignoring them)
+      std::unordered_set<std::string> srcCounted;
+      for (size_t i = 0; i < dev.size(); ++i) {
+        const uint32_t* b = blocks + i * static_cast<size_t>(bw);
+        if (b[0] != 0) {
+          host.push_back(*dev[i]);
+          continue;
+        }
+        ++kspDevicePairs_;
+        auto parse = [&](size_t w, std::vector<Path>& out) {
+          const uint32_t n = b[w++];
+          for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t len = b[w++];
+            out.emplace_back(b + w, b + w + len);
+            w += len;
+          }
+        };
+        std::vector<Path> k1, k2;
+        parse(2, k1);
+        parse(b[1], k2);
+        const std::string& src = dev[i]->first;
+        if (!spfResults_.count({src, true}) && !countedOnDevice_.count(src) && srcCounted.insert(src).second) {
+          ++spfRuns_;
+          countedOnDevice_.insert(src);
+        }
+        if (!k1.empty()) ++spfRuns_;
+        kthPaths_.emplace(std::make_tuple(src, dev[i]->second, size_t{1}), std::move(k1));
+        kthPaths_.emplace(std::make_tuple(src, dev[i]->second, size_t{2}), std::move(k2));
+      }
+      prof.mark("paths");
+    }
+  }
+  kspHostPairs_ += host.size();
+  if (!host.empty()) prefetchKthPathsHost(host);
+}
+
+void LinkState::prefetchKthPathsHost(const std::vector<std::pair<std::string, std::string>>& pairs) const {
   // k = 1: traces over the memoized SPF of each source (batched)
   KspProf prof;
   std::vector<std::string> srcs;
@@ -773,6 +853,7 @@ const SpfRow& LinkState::getSpfRow(const std::string& node, bool useLinkMetric) 
   SpfRow row;
   if (id) {
     row = spfOnDevice(*id, useLinkMetric, nullptr);
+    if (useLinkMetric && countedOnDevice_.erase(node)) --spfRuns_;  // counted by a KSP2 batch
   } else {
     // unknown source: the reference result holds only the source itself
     row.srcName = node;

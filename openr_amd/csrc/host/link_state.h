@@ -201,6 +201,9 @@ class LinkState {
                                   const std::vector<std::vector<uint32_t>>* ignoreSets) const;
   void prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
   void prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const;
+  // the same over host traces of device rows (exact-order graphs, pairs the
+  // device trace flags)
+  void prefetchKthPathsHost(const std::vector<std::pair<std::string, std::string>>& pairs) const;
   std::optional<Metric> getMetricFromAToB(const std::string& a, const std::string& b,
                                           bool useLinkMetric = true) const;
   Metric getMaxHopsToNode(const std::string& node) const;
@@ -290,6 +293,14 @@ class LinkState {
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMaps_;  // getSpfResult views
   mutable std::map<std::tuple<std::string, std::string, size_t>, std::vector<Path>> kthPaths_;
   mutable uint64_t spfRuns_{0};
+  // sources whose SPF a device KSP2 batch ran and counted (the reference's
+  // memoized getSpfResult, LinkState.cpp:775-776) without keeping the row on
+  // the host: a later getSpfRow of one computes the row but does not count it
+  mutable std::unordered_set<std::string> countedOnDevice_;
+
+ public:
+  // prefetchKthPaths pairs traced on the device / on the host (tests, A/B)
+  mutable uint64_t kspDevicePairs_{0}, kspHostPairs_{0};
 };
 
 }  // namespace openr_amd

@@ -11,12 +11,28 @@ namespace orh {
 // runSpf(src, useLinkMetric, ignore) for many (src, ignore set) requests from
 // the plain SPF rows of their sources: a request's row is the base row except
 // on the nodes downstream of a tight ignored link, which are re-derived.
+//
+// Requests move through tiers; each tier is a work queue drained by a fixed
+// grid of workgroups (every workgroup exits once the queue is empty):
+//   seed   one thread per request: no tight ignored link -> the base row
+//          stands (tier 0); else the request joins queue 1
+//   tier 1 small LDS state (kSmallA nodes / kSmallE edges): most repairs
+//   tier 2 large LDS state (cap_a / cap_e)
+//   tier 3 global slots sized for the whole graph (cannot overflow)
+//   tier 4 only without slots: the full HBM search (fallback flags)
+constexpr uint32_t kWhatifTierBase = 0, kWhatifTierSmall = 1, kWhatifTierLarge = 2, kWhatifTierSlot = 3,
+                   kWhatifTierSearch = 4;
+constexpr uint32_t kSmallA = 256, kSmallE = 1024;
+// counters (u32, zeroed before a run): per queue q = 0..2 its length and the
+// next index to claim
+constexpr uint32_t kWhatifCounters = 8;
+
 struct RepairArgs {
   uint32_t n_nodes;
   uint32_t n_req;
   int32_t use_link_metric;
-  uint32_t cap_a;  // affected nodes a workgroup repairs in LDS
-  uint32_t cap_e;  // predecessor edges among them
+  uint32_t cap_a;  // tier 2: affected nodes a workgroup repairs in LDS
+  uint32_t cap_e;  // tier 2: predecessor edges among them
   const uint2* recs;
   const uint32_t* link;
   const uint16_t* rank_out;
@@ -32,21 +48,23 @@ struct RepairArgs {
   const uint4* cuts;          // (tail, head, record tail -> head, 0) per ignored link end
   uint32_t* out_dist;         // [n_req][N]
   uint32_t* out_nh;           // [n_req][N], one mask word
-  uint32_t* fallback;         // [n_req] set when a request needs the full search
-  // second pass for the requests that outgrew LDS: n_slots global slots of
-  // slot_bytes each, claimed through *slot_next (zeroed beforehand)
+  uint32_t* fallback;         // [n_req] set when a request needs the full search (no slots)
+  uint32_t* info;             // [n_req] tier | affected nodes << 3 (nullable)
+  uint32_t* queues;           // [3][n_req] request ids of queues 0..2 (tiers 1..3)
+  uint32_t* counters;         // [kWhatifCounters]
+  // tier 3: n_slots global slots of slot_bytes each, one per workgroup
   uint8_t* slot_mem;
   size_t slot_bytes;
   uint32_t n_slots;
-  uint32_t* slot_next;
   uint32_t n_recs;  // device records (slot edge capacity)
+  uint32_t n_cu;    // grid sizing of the queue-draining tiers
 };
 // LDS bytes of the repair kernel for the given caps
 size_t repair_lds_bytes(uint32_t n_nodes, uint32_t cap_a, uint32_t cap_e);
 // bytes of one global repair slot (whole-graph caps)
 size_t repair_slot_bytes(uint32_t n_nodes, uint32_t n_recs);
-// copy each request's base rows, then repair; rows the repair cannot hold
-// get fallback[r] = 1 (fallback must be zeroed beforehand)
-hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, hipStream_t s);
+// seed, copy each request's base rows, then the repair tiers; with no slots
+// the requests that outgrow tier 2 get fallback[r] = 1 (zeroed beforehand)
+hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
 
 }  // namespace orh

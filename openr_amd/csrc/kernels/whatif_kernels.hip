@@ -37,13 +37,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "spf_kernels.h"  // edge record flags
 #include "whatif_kernels.h"
 
 namespace orh {
 namespace {
 
-constexpr uint32_t kRepBlock = 256;    // LDS pass: small state, several requests per CU
 constexpr uint32_t kSlotBlock = 1024;  // slot pass: few large affected sets, one per CU
 constexpr uint32_t kInfD = 0xFFFFFFFFu;
 constexpr unsigned long long kInfLab = 0xFFFFFFFF00000000ull;  // {dist = inf, mask = 0}
@@ -123,27 +124,19 @@ __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t
   }
 }
 
-// kSlot = false: state in LDS with the caps a.cap_a / a.cap_e, overflow flags
-// the request; kSlot = true: only flagged requests, state in a global slot
-// sized for the whole graph (A <= N, edges <= records), so the repair itself
-// cannot overflow; when the slots run out the flag stays for the full search
-template <int K, bool kSlot>
-__global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_kernel(RepairArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t s_cnt, s_ecnt, s_ovf, s_slot;
-  __shared__ uint32_t s_flag[3];
-  const uint32_t N = a.n_nodes, NB = (N + 31) / 32;
-  const uint32_t tid = threadIdx.x, B = blockDim.x, r = blockIdx.x;
-  if (kSlot) {
-    if (!a.fallback[r]) return;  // repaired in LDS (whole workgroup)
-    if (tid == 0) s_slot = atomicAdd(a.slot_next, 1u);
-    __syncthreads();
-    if (s_slot >= a.n_slots) return;  // no slot left: the full search takes it
-  }
-  const uint32_t cap_a = kSlot ? N : a.cap_a, cap_e = kSlot ? a.n_recs : a.cap_e;
+// One request: A (the nodes below a tight ignored link, closed under tight
+// out-records of transit nodes), boundary labels from predecessors outside
+// A, chaotic relaxation inside A, rows written. State at `base` with the
+// caps cap_a / cap_e (LDS, or a global slot with whole-graph caps). Returns
+// |A|, or ~0u when A or its edge list outgrows the caps. The membership
+// bitmap must be all zero on entry; the caller clears it afterwards.
+template <int K>
+__device__ uint32_t repair_one(const RepairArgs& a, uint32_t r, uint32_t* base, uint32_t cap_a, uint32_t cap_e,
+                               uint32_t* s_cnt, uint32_t* s_ecnt, uint32_t* s_ovf, uint32_t* s_flag) {
+  const uint32_t N = a.n_nodes;
+  const uint32_t tid = threadIdx.x, B = blockDim.x;
   // state: labels u64[cap_a] | boundary labels u64[cap_a] | edges uint2[cap_e] |
   //        edge ranges uint2[cap_a] | node list u32[cap_a] | membership bitmap u32[NB]
-  uint32_t* base = kSlot ? reinterpret_cast<uint32_t*>(a.slot_mem + s_slot * a.slot_bytes) : lds;
   unsigned long long* lab = reinterpret_cast<unsigned long long*>(base);
   unsigned long long* blab = lab + cap_a;
   uint2* edges = reinterpret_cast<uint2*>(blab + cap_a);
@@ -161,11 +154,10 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
   const uint32_t n_ign = a.ign_ptr[r + 1] - a.ign_ptr[r];
   const bool metric = a.use_link_metric != 0;
 
-  for (uint32_t i = tid; i < NB; i += B) bits[i] = 0u;
   if (tid == 0) {
-    s_cnt = 0u;
-    s_ecnt = 0u;
-    s_ovf = 0u;
+    *s_cnt = 0u;
+    *s_ecnt = 0u;
+    *s_ovf = 0u;
   }
   if (tid < 3) s_flag[tid] = 0u;
   bar();
@@ -173,9 +165,9 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
   auto add = [&](uint32_t u) {
     const uint32_t bit = 1u << (u & 31u);
     if (atomicOr(&bits[u >> 5], bit) & bit) return;
-    const uint32_t k = atomicAdd(&s_cnt, 1u);
+    const uint32_t k = atomicAdd(s_cnt, 1u);
     if (k < cap_a) alist[k] = u;
-    else s_ovf = 1u;
+    else *s_ovf = 1u;
   };
   // seeds: heads of tight ignored records whose tail is a transit node
   for (uint32_t c = a.cut_ptr[r] + tid; c < a.cut_ptr[r + 1]; c += B) {
@@ -187,13 +179,13 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
     if (static_cast<uint64_t>(dx) + (metric ? rec.y : 1u) == bd[cut.y]) add(cut.y);
   }
   bar();
-  if (s_cnt == 0u) return;  // nothing below a tight ignored link: the base row stands
+  if (*s_cnt == 0u) return 0u;  // nothing below a tight ignored link: the base row stands
 
   // A: closure under tight out-records of transit nodes, level by level
   uint32_t lo = 0;
   for (;;) {
-    const uint32_t hi = min(s_cnt, cap_a);
-    const bool ovf = s_ovf != 0u;
+    const uint32_t hi = min(*s_cnt, cap_a);
+    const bool ovf = *s_ovf != 0u;
     bar();  // everyone has read the range before it grows
     if (ovf || lo == hi) break;
     for (uint32_t k = lo + tid; k < hi; k += B) {
@@ -209,11 +201,8 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
     lo = hi;
     bar();
   }
-  const uint32_t n = min(s_cnt, cap_a);
-  if (s_ovf) {
-    if (tid == 0) a.fallback[r] = 1u;
-    return;
-  }
+  const uint32_t n = min(*s_cnt, cap_a);
+  if (*s_ovf) return ~0u;
   // the request's mask row doubles as the node -> A index map (rewritten below)
   for (uint32_t k = tid; k < n; k += B) on[alist[k]] = k;
   bar();
@@ -241,9 +230,9 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
              bl = meet(bl, static_cast<uint64_t>(dp) + w, p == s ? (1u << a.rank_out[q2]) : bn[p]);
            });
     });
-    const uint32_t e0 = cnt ? atomicAdd(&s_ecnt, cnt) : 0u;
+    const uint32_t e0 = cnt ? atomicAdd(s_ecnt, cnt) : 0u;
     if (e0 + cnt > cap_e) {
-      s_ovf = 1u;
+      *s_ovf = 1u;
       cnt = 0;
     }
     uint32_t e = e0;
@@ -257,10 +246,7 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
     lab[k] = kInfLab;
   }
   bar();
-  if (s_ovf) {
-    if (tid == 0) a.fallback[r] = 1u;
-    return;
-  }
+  if (*s_ovf) return ~0u;
 
   // chaotic relaxation inside A until no label changes (labels only descend
   // in the lattice; a sweep that writes nothing proves the fixpoint)
@@ -303,7 +289,88 @@ __global__ __launch_bounds__(kSlot ? kSlotBlock : kRepBlock) void whatif_repair_
     od[v] = static_cast<uint32_t>(l >> 32);
     on[v] = static_cast<uint32_t>(l);
   }
-  if (kSlot && tid == 0) a.fallback[r] = 0u;  // repaired: the full search skips it
+  return n;
+}
+
+// seed pass, one thread per request: a request with no tight ignored link
+// keeps the copied base row (tier 0); the others join queue 0 (wave-aggregated
+// appends: one atomic per wave)
+__global__ __launch_bounds__(256) void whatif_seed_kernel(RepairArgs a) {
+  const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+  bool hit = false;
+  if (r < a.n_req) {
+    const uint32_t N = a.n_nodes;
+    const uint32_t s = a.srcs[r];
+    const uint32_t* bd = a.base_dist + static_cast<size_t>(a.base_row[r]) * N;
+    const bool metric = a.use_link_metric != 0;
+    for (uint32_t c = a.cut_ptr[r]; c < a.cut_ptr[r + 1] && !hit; ++c) {
+      const uint4 cut = a.cuts[c];
+      const uint2 rec = a.recs[cut.z];
+      if (rec.x & ORH_REC_SKIP) continue;
+      const uint32_t dx = bd[cut.x];
+      if (dx == kInfD || (cut.x != s && a.ovl[cut.x])) continue;
+      hit = static_cast<uint64_t>(dx) + (metric ? rec.y : 1u) == bd[cut.y];
+    }
+    if (a.info) a.info[r] = kWhatifTierBase;
+  }
+  const unsigned long long m = __ballot(hit);
+  if (!m) return;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(m));
+  uint32_t at = 0;
+  if (lane == leader) at = atomicAdd(&a.counters[0], static_cast<uint32_t>(__popcll(m)));
+  at = __shfl(at, static_cast<int>(leader));
+  if (hit) a.queues[at + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)))] = r;
+}
+
+// tier kTier drains queue q into queue q + 1: LDS state (tiers 1, 2) or one global
+// slot per workgroup (tier 3); a request that outgrows the caps moves on to
+// the next queue. Every workgroup leaves once its claim passes the queue's
+// length (fixed before this launch by the previous kernel).
+template <int K, uint32_t kTier>
+__global__ __launch_bounds__(kTier == kWhatifTierSmall ? 128 : kTier == kWhatifTierLarge ? 256 : kSlotBlock)
+void whatif_repair_kernel(RepairArgs a, uint32_t cap_a, uint32_t cap_e, uint32_t q) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_cnt, s_ecnt, s_ovf, s_req;
+  __shared__ uint32_t s_flag[3];
+  constexpr bool kSlot = kTier == kWhatifTierSlot;
+  const uint32_t N = a.n_nodes, NB = (N + 31) / 32;
+  const uint32_t tid = threadIdx.x, B = blockDim.x;
+  uint32_t* base = kSlot ? reinterpret_cast<uint32_t*>(a.slot_mem + blockIdx.x * a.slot_bytes) : lds;
+  uint32_t* alist = base + 2 * 2 * cap_a + 2 * cap_e + 2 * cap_a;  // see repair_one's layout
+  uint32_t* bits = alist + cap_a;
+  for (uint32_t i = tid; i < NB; i += B) bits[i] = 0u;
+  const uint32_t len = a.counters[2 * q];
+  for (;;) {
+    if (tid == 0) {
+      const uint32_t i = atomicAdd(&a.counters[2 * q + 1], 1u);
+      s_req = i < len ? a.queues[static_cast<size_t>(q) * a.n_req + i] : ~0u;
+    }
+    bar();
+    const uint32_t r = s_req;
+    if (r == ~0u) break;
+    const uint32_t n = repair_one<K>(a, r, base, cap_a, cap_e, &s_cnt, &s_ecnt, &s_ovf, s_flag);
+    if (tid == 0) {
+      if (n != ~0u) {
+        if (a.info) a.info[r] = kTier | (n << 3);
+        if (kSlot) a.fallback[r] = 0u;
+      } else if (!kSlot) {
+        const uint32_t j = atomicAdd(&a.counters[2 * (q + 1)], 1u);
+        a.queues[static_cast<size_t>(q + 1) * a.n_req + j] = r;
+        if (kTier == kWhatifTierLarge) a.fallback[r] = 1u;  // the full search takes it without slots
+      }
+    }
+    // clear the membership bitmap: through the node list when it holds all
+    // of A, else whole
+    const uint32_t cnt = s_cnt;
+    bar();
+    if (cnt > cap_a) {
+      for (uint32_t i = tid; i < NB; i += B) bits[i] = 0u;
+    } else {
+      for (uint32_t k = tid; k < cnt; k += B) bits[alist[k] >> 5] = 0u;
+    }
+    bar();
+  }
 }
 
 }  // namespace
@@ -317,29 +384,54 @@ size_t repair_slot_bytes(uint32_t n_nodes, uint32_t n_recs) {
   return (repair_lds_bytes(n_nodes, n_nodes, n_recs) + 255) & ~static_cast<size_t>(255);
 }
 
-hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, hipStream_t s) {
+hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
   if (a.n_req == 0) return hipSuccess;
   if (ell_k != 4 && ell_k != 8) return hipErrorInvalidValue;
   const uint32_t tiles = (a.n_nodes + kCopyTile - 1) / kCopyTile;
   const uint64_t grid = static_cast<uint64_t>(tiles) * a.n_req;
   if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(whatif_seed_kernel, dim3((a.n_req + 255) / 256), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   const uint32_t vec = (a.n_nodes & 3u) == 0 && al(a.base_dist) && al(a.base_nh) && al(a.out_dist) &&
                        al(a.out_nh);
   hipLaunchKernelGGL(whatif_copy_kernel, dim3(static_cast<uint32_t>(grid)), dim3(256), 0, s, a, tiles, vec);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const size_t lds = repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // queue-draining grids: as many workgroups as the LDS lets share a CU
+  // (one request each at a time), never more than there are requests
+  auto tier_grid = [&](size_t lds, uint32_t per_cu_cap) {
+    const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(per_cu_cap, std::max<size_t>(1, lds_limit / lds)));
+    return std::max<uint32_t>(1u, std::min<uint32_t>(a.n_req, a.n_cu * per_cu));
+  };
+  const uint32_t sa = std::min(kSmallA, a.cap_a), se = std::min(kSmallE, a.cap_e);
+  const size_t lds1 = repair_lds_bytes(a.n_nodes, sa, se);
+  const size_t lds2 = repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
+  const bool small_tier = lds1 < lds2;
+  if (small_tier) {
+    if (ell_k == 8)
+      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSmall>), dim3(tier_grid(lds1, 16)), dim3(128), lds1, s,
+                         a, sa, se, 0u);
+    else
+      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSmall>), dim3(tier_grid(lds1, 16)), dim3(128), lds1, s,
+                         a, sa, se, 0u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  // without the small tier, tier 2 drains queue 0 itself
+  const uint32_t q2 = small_tier ? 1u : 0u;
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, false>), dim3(a.n_req), dim3(kRepBlock), lds, s, a);
+    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(lds2, 8)), dim3(256), lds2, s, a,
+                       a.cap_a, a.cap_e, q2);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, false>), dim3(a.n_req), dim3(kRepBlock), lds, s, a);
-  e = hipGetLastError();
-  if (e != hipSuccess || a.n_slots == 0) return e;
+    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierLarge>), dim3(tier_grid(lds2, 8)), dim3(256), lds2, s, a,
+                       a.cap_a, a.cap_e, q2);
+  if ((e = hipGetLastError()) != hipSuccess || a.n_slots == 0) return e;
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, true>), dim3(a.n_req), dim3(kSlotBlock), 0, s, a);
+    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
+                       a.n_nodes, a.n_recs, q2 + 1u);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, true>), dim3(a.n_req), dim3(kSlotBlock), 0, s, a);
+    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
+                       a.n_nodes, a.n_recs, q2 + 1u);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/openr_hip.h"
+#include "kernels/ksp_kernels.h"
 #include "kernels/route_kernels.h"
 #include "kernels/spf_kernels.h"
 #include "kernels/whatif_kernels.h"
@@ -63,13 +64,10 @@ struct orh_ctx {
   size_t d_exact_cap = 0;  // in bytes
   uint8_t* d_batch_x = nullptr;
   size_t d_batch_x_cap = 0;  // in bytes
-  // what-if repair: base rows of the batch's distinct sources, and the staged
-  // request (base row, source, ignore sets, cut records, fallback flags)
-  uint8_t* d_rep_base = nullptr;
-  size_t d_rep_base_cap = 0;  // in bytes
-  uint32_t* d_rep = nullptr;
-  size_t d_rep_cap = 0;  // in u32
-  std::vector<uint32_t> rep_key;
+  uint8_t* d_ksp = nullptr;  // orh_ksp2_batch: rows, traces' scratch and output
+  size_t d_ksp_cap = 0;
+  uint32_t* h_ksp = nullptr;  // orh_ksp2_batch's pinned output blocks
+  size_t h_ksp_cap = 0;       // in u32
   uint8_t* d_rep_slots = nullptr;  // global repair slots (requests that outgrow LDS)
   size_t d_rep_slots_cap = 0;
   uint32_t* h_pinned = nullptr;  // orh_spf_batch_pinned's host rows (hipHostMalloc)
@@ -563,9 +561,9 @@ int orh_destroy(orh_ctx* ctx) {
   hipFree(ctx->d_patch);
   hipFree(ctx->d_exact);
   hipFree(ctx->d_batch_x);
-  hipFree(ctx->d_rep_base);
-  hipFree(ctx->d_rep);
   hipFree(ctx->d_rep_slots);
+  hipFree(ctx->d_ksp);
+  if (ctx->h_ksp) hipHostFree(ctx->h_ksp);
   if (ctx->h_pinned) hipHostFree(ctx->h_pinned);
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
@@ -647,7 +645,6 @@ int orh_graph_destroy(orh_graph* g) {
   hipStreamSynchronize(g->ctx->stream);
   free_graph_device(g);
   g->ctx->req_key.clear();  // the staged request may describe this graph
-  g->ctx->rep_key.clear();
   delete g;
   return ORH_OK;
 }
@@ -1061,22 +1058,45 @@ static void repair_caps(const orh_ctx* ctx, uint32_t n_nodes, uint32_t* cap_a, u
   }
 }
 
-constexpr uint32_t kRepairSlots = 64;       // second pass: whole-graph state in global memory
+constexpr uint32_t kRepairSlots = 64;       // tier 3: whole-graph state in global memory
 constexpr size_t kRepairSlotBudget = 1ull << 30;  // bytes for all slots
 constexpr uint32_t kRepairMaxIgnore = 8;  // link-failure sets; KSP2 k = 2 sets are whole paths
 
+// What-if search plan for the graph: the repair needs one mask word per
+// source, no zero metrics (the exact kernel's extraction order decides those
+// first hops) and a full-search plan for the no-slot fallback
+static int whatif_plan(orh_graph* g, bool use_link_metric, uint64_t* bound, bool* uniform) {
+  orh_ctx* ctx = g->ctx;
+  if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "what-if: no graph loaded");
+  if (use_link_metric && g->has_zero)
+    return fail(ctx, ORH_E_UNSUPPORTED, "what-if: zero link metrics need the exact kernel");
+  const uint32_t N = g->n_nodes;
+  *uniform = !use_link_metric || g->min_out == g->max_out;
+  const uint32_t w0 = use_link_metric ? g->max_out : 1u;
+  *bound = *uniform ? static_cast<uint64_t>(N) * w0
+           : use_link_metric ? g->sum_max_metric / 2 + g->max_metric
+                             : static_cast<uint64_t>(g->n_links) + 1;
+  uint32_t cap_a = 0, cap_e = 0;
+  repair_caps(ctx, N, &cap_a, &cap_e);
+  if (orh::repair_lds_bytes(N, cap_a, cap_e) > ctx->lds_limit)
+    return fail(ctx, ORH_E_UNSUPPORTED, "what-if: repair state exceeds LDS");
+  const orh::SpfPlan fp = orh::plan_spf(N, *uniform, *bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
+  if (fp.variant == orh::SpfVariant::kUnsupported)
+    return fail(ctx, ORH_E_UNSUPPORTED, "what-if: no search plan for this graph");
+  return ORH_OK;
+}
+
 // Can run_repair take this ignore-set batch? (sources repeat, small sets,
 // one mask word, the LDS state fits, and the fallback search has a plan)
-static bool repair_eligible(const orh_graph* g, const orh_spf_request* req, uint32_t words,
-                            uint64_t bound, bool uniform) {
+static bool repair_eligible(orh_graph* g, const orh_spf_request* req, uint32_t words) {
   const orh_ctx* ctx = g->ctx;
   if (ctx->repair_mode == 0 || words != 1 || !req->h_ignore_ptr) return false;
-  uint32_t cap_a = 0, cap_e = 0;
-  repair_caps(ctx, g->n_nodes, &cap_a, &cap_e);
-  if (orh::repair_lds_bytes(g->n_nodes, cap_a, cap_e) > ctx->lds_limit) return false;
-  const orh::SpfPlan fp = orh::plan_spf(g->n_nodes, uniform, bound, g->ell_k, ctx->lds_limit, false,
-                                        orh::SpfMode::kGlobal);
-  if (fp.variant == orh::SpfVariant::kUnsupported) return false;
+  uint64_t bound = 0;
+  bool uniform = false;
+  const std::string err = g->ctx->err;
+  const int rc = whatif_plan(g, req->use_link_metric != 0, &bound, &uniform);
+  g->ctx->err = err;  // not eligible is not an error of this call
+  if (rc) return false;
   if (ctx->repair_mode >= 2) return true;
   for (uint32_t i = 0; i < req->n_src; ++i)
     if (req->h_ignore_ptr[i + 1] - req->h_ignore_ptr[i] > kRepairMaxIgnore) return false;
@@ -1086,14 +1106,258 @@ static bool repair_eligible(const orh_graph* g, const orh_spf_request* req, uint
   return 2 * m <= req->n_src;
 }
 
-// runSpf(src, useLinkMetric, ignore) for every request from the plain rows of
-// its source (one orh_spf_run over the distinct sources), then copy + repair;
-// requests the repair cannot hold in LDS are searched in full
-// (spf_global_nh_kernel with the fallback flags as row mask)
-static int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist, uint32_t* d_nh,
-                      uint64_t bound, bool uniform) {
+}  // extern "C"
+
+// A what-if job (include/openr_hip.h): the plain rows of its sources, then
+// any number of request batches repaired from them
+struct orh_whatif {
+  orh_graph* g = nullptr;
+  uint64_t gen = 0;  // graph structure the base rows belong to
+  int32_t use_link_metric = 1;
+  bool uniform = false;
+  uint64_t bound = 0;
+  std::vector<uint32_t> srcs;
+  uint32_t* d_base = nullptr;  // dist rows [m][N], then mask rows [m][N]
+  // request staging: two pinned host / device buffer pairs, alternating, so
+  // a batch's upload never waits for the previous batch's kernels
+  uint32_t* h_stage[2] = {nullptr, nullptr};
+  uint32_t* d_stage[2] = {nullptr, nullptr};
+  size_t stage_cap[2] = {0, 0};  // u32, both sides
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int cur = 0;
+  // queues [3][n] | counters | fallback flags [n] (stream-ordered reuse)
+  uint32_t* d_work = nullptr;
+  size_t work_cap = 0;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;  // create .. last run
+  uint64_t requests = 0;
+};
+
+namespace {
+
+int whatif_stage(orh_whatif* job, size_t words, uint32_t** h, uint32_t** d) {
+  orh_ctx* ctx = job->g->ctx;
+  const int c = job->cur;
+  if (job->stage_ev[c]) ORH_HIP(ctx, hipEventSynchronize(job->stage_ev[c]));  // its last upload is done
+  if (words > job->stage_cap[c]) {
+    if (job->h_stage[c]) hipHostFree(job->h_stage[c]);
+    hipFree(job->d_stage[c]);
+    job->h_stage[c] = nullptr;
+    job->d_stage[c] = nullptr;
+    job->stage_cap[c] = 0;
+    const size_t cap = std::max<size_t>(words + words / 4, 4096);
+    ORH_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&job->h_stage[c]), cap * 4, hipHostMallocDefault));
+    ORH_HIP(ctx, hipMalloc(&job->d_stage[c], cap * 4));
+    job->stage_cap[c] = cap;
+  }
+  if (!job->stage_ev[c]) ORH_HIP(ctx, hipEventCreateWithFlags(&job->stage_ev[c], hipEventDisableTiming));
+  *h = job->h_stage[c];
+  *d = job->d_stage[c];
+  return ORH_OK;
+}
+
+// one batch of requests of a job: seed, copy, repair tiers (and without
+// slots the full search for what outgrew tier 2), all on the context stream
+int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const uint32_t* ign_ptr,
+               const uint32_t* ign_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info) {
+  orh_graph* g = job->g;
   orh_ctx* ctx = g->ctx;
-  const uint32_t N = g->n_nodes, n_src = req->n_src;
+  const uint32_t N = g->n_nodes, m = static_cast<uint32_t>(job->srcs.size());
+  for (uint32_t i = 0; i < n_req; ++i)
+    if (src_idx[i] >= m) return fail(ctx, ORH_E_INVALID, "orh_whatif_run: source index out of range");
+  // staging: base_row[n] | srcs[n] | ign_ptr[n+1] | ign[..] | cut_ptr[n+1] | (pad to 16 B) cuts uint4[..]
+  const uint32_t n_ign = ign_ptr[n_req];
+  size_t n_cuts = 0;
+  for (uint32_t k = 0; k < n_ign; ++k) {
+    const uint32_t l = ign_links[k];
+    if (l < g->n_links) n_cuts += (g->link_ent[2 * static_cast<size_t>(l)] != ~0u) + (g->link_ent[2 * static_cast<size_t>(l) + 1] != ~0u);
+  }
+  const size_t off_src = n_req, off_ip = 2 * size_t{n_req}, off_ign = off_ip + n_req + 1;
+  const size_t off_cp = off_ign + n_ign;
+  const size_t off_cuts = (off_cp + n_req + 1 + 3) & ~size_t{3};
+  const size_t words = off_cuts + 4 * n_cuts + 4;
+  uint32_t *h = nullptr, *d = nullptr;
+  int rc = whatif_stage(job, words, &h, &d);
+  if (rc) return rc;
+  std::memcpy(h, src_idx, n_req * 4ull);
+  for (uint32_t i = 0; i < n_req; ++i) h[off_src + i] = job->srcs[src_idx[i]];
+  uint32_t* hp = h + off_ip;
+  uint32_t* hi = h + off_ign;
+  uint32_t* hc = h + off_cp;
+  uint4* cuts = reinterpret_cast<uint4*>(h + off_cuts);
+  size_t ni = 0, nc = 0;
+  hp[0] = 0;
+  hc[0] = 0;
+  for (uint32_t i = 0; i < n_req; ++i) {
+    uint32_t* set = hi + ni;
+    size_t len = 0;
+    for (uint32_t k = ign_ptr[i]; k < ign_ptr[i + 1]; ++k) set[len++] = ign_links[k];
+    std::sort(set, set + len);  // bsearch on device
+    len = static_cast<size_t>(std::unique(set, set + len) - set);
+    for (size_t k = 0; k < len; ++k) {
+      const uint32_t l = set[k];
+      if (l >= g->n_links) continue;
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const uint32_t e = g->link_ent[2 * static_cast<size_t>(l) + e2];
+        if (e == ~0u) continue;
+        cuts[nc++] = make_uint4(row_of(g, e), g->col[e], g->pos[e], 0u);
+      }
+    }
+    ni += len;
+    hp[i + 1] = static_cast<uint32_t>(ni);
+    hc[i + 1] = static_cast<uint32_t>(nc);
+  }
+  const int c = job->cur;
+  job->cur ^= 1;
+  ORH_HIP(ctx, hipMemcpyAsync(d, h, words * 4, hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipEventRecord(job->stage_ev[c], ctx->stream));
+
+  const size_t work = 3 * size_t{n_req} + orh::kWhatifCounters + n_req;
+  if (work > job->work_cap) {
+    hipFree(job->d_work);
+    job->d_work = nullptr;
+    job->work_cap = 0;
+    ORH_HIP(ctx, hipMalloc(&job->d_work, work * 4));
+    job->work_cap = work;
+  }
+  uint32_t* counters = job->d_work + 3 * size_t{n_req};
+  uint32_t* flags = counters + orh::kWhatifCounters;
+  ORH_HIP(ctx, hipMemsetAsync(counters, 0, (orh::kWhatifCounters + n_req) * 4ull, ctx->stream));
+  const size_t slot_bytes = orh::repair_slot_bytes(N, g->n_recs);
+  const uint32_t n_slots = static_cast<uint32_t>(std::min<size_t>(
+      std::min<size_t>(kRepairSlots, n_req), kRepairSlotBudget / std::max<size_t>(slot_bytes, 1)));
+  if (n_slots) {
+    rc = ensure_bytes(ctx, &ctx->d_rep_slots, &ctx->d_rep_slots_cap, n_slots * slot_bytes);
+    if (rc) return rc;
+  }
+  const size_t nd = static_cast<size_t>(m) * N;
+  orh::RepairArgs ra{};
+  ra.n_nodes = N;
+  ra.n_req = n_req;
+  ra.use_link_metric = job->use_link_metric;
+  repair_caps(ctx, N, &ra.cap_a, &ra.cap_e);
+  ra.recs = g->d_recs;
+  ra.link = g->d_link;
+  ra.rank_out = g->d_rank_out;
+  ra.rev = g->d_rev;
+  ra.ovl = g->d_ovl;
+  ra.base_dist = job->d_base;
+  ra.base_nh = job->d_base + nd;
+  ra.base_row = d;
+  ra.srcs = d + off_src;
+  ra.ign_ptr = d + off_ip;
+  ra.ign = d + off_ign;
+  ra.cut_ptr = d + off_cp;
+  ra.cuts = reinterpret_cast<const uint4*>(d + off_cuts);
+  ra.out_dist = d_dist;
+  ra.out_nh = d_nh;
+  ra.fallback = flags;
+  ra.info = d_info;
+  ra.queues = job->d_work;
+  ra.counters = counters;
+  ra.slot_mem = ctx->d_rep_slots;
+  ra.slot_bytes = slot_bytes;
+  ra.n_slots = n_slots;
+  ra.n_recs = g->n_recs;
+  ra.n_cu = ctx->n_cu;
+  hipError_t e = orh::launch_repair(ra, g->ell_k, ctx->lds_limit, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch");
+  if (n_slots == 0) {
+    // no slot fits the budget: the requests that outgrew tier 2 are searched
+    // in full (spf_global_nh_kernel with the flags as its row mask)
+    orh::SpfPlan fp = orh::plan_spf(N, job->uniform, job->bound, g->ell_k, ctx->lds_limit, false,
+                                    orh::SpfMode::kGlobal);
+    fp.variant = orh::SpfVariant::kGlobalNh;
+    fp.block = 1024;  // only the flagged rows search; the rest exit at once
+    rc = ensure_labels(ctx, static_cast<size_t>(n_req) * N);
+    if (rc) return rc;
+    orh::SpfArgs a{};
+    a.n_nodes = N;
+    a.n_out = n_req;
+    a.recs = g->d_recs;
+    a.link = g->d_link;
+    a.srcs = ra.srcs;
+    a.ignore_ptr = ra.ign_ptr;
+    a.ignore_links = ra.ign;
+    a.use_link_metric = job->use_link_metric;
+    a.w0 = job->use_link_metric ? g->max_out : 1u;
+    a.delta = job->uniform ? a.w0
+                           : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                        static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+    a.out_dist = d_dist;
+    a.scratch = ctx->d_scratch;
+    a.labels = ctx->d_labels;
+    a.out_nh = d_nh;
+    a.words = 1;
+    a.rank_out = g->d_rank_out;
+    a.row_mask = flags;
+    e = orh::launch_spf(fp, a, n_req, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "what-if fallback launch");
+  }
+  ORH_HIP(ctx, hipEventRecord(job->ev_end, ctx->stream));
+  job->requests += n_req;
+  ctx->counters.spf_runs += n_req;  // one runSpf per request (LinkState.cpp:815)
+  ctx->counters.spf_launches += 1;
+  ctx->counters.last_kernel_ms = -1.0;
+  return ORH_OK;
+}
+
+int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t use_link_metric,
+                  orh_whatif** out) {
+  orh_ctx* ctx = g->ctx;
+  uint64_t bound = 0;
+  bool uniform = false;
+  int rc = whatif_plan(g, use_link_metric != 0, &bound, &uniform);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < n_srcs; ++i) {
+    if (h_srcs[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_whatif_create: source out of range");
+    if (n_distinct(g, h_srcs[i]) > 32)
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_whatif_create: a source has more than 32 neighbours");
+  }
+  hipSetDevice(ctx->device);
+  auto* job = new (std::nothrow) orh_whatif();
+  if (!job) return fail(ctx, ORH_E_NOMEM, "orh_whatif_create");
+  job->g = g;
+  job->gen = g->gen;
+  job->use_link_metric = use_link_metric ? 1 : 0;
+  job->uniform = uniform;
+  job->bound = bound;
+  job->srcs.assign(h_srcs, h_srcs + n_srcs);
+  auto bail = [&](int code) {
+    orh_whatif_destroy(job);
+    return code;
+  };
+  if (hipEventCreate(&job->ev_begin) != hipSuccess || hipEventCreate(&job->ev_end) != hipSuccess)
+    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
+  rc = ensure_rev(g);
+  if (rc) return bail(rc);
+  const size_t nd = static_cast<size_t>(std::max<uint32_t>(n_srcs, 1)) * g->n_nodes;
+  if (hipMalloc(&job->d_base, nd * 8) != hipSuccess)
+    return bail(fail(ctx, ORH_E_NOMEM, "orh_whatif_create: base rows"));
+  if (hipEventRecord(job->ev_begin, ctx->stream) != hipSuccess)
+    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: event"));
+  if (n_srcs) {
+    // the plain SPFs of the sources (internal: spf_runs counts the requests)
+    orh_spf_request br{};
+    br.h_srcs = job->srcs.data();
+    br.n_src = n_srcs;
+    br.use_link_metric = job->use_link_metric;
+    const orh_counters c0 = ctx->counters;
+    rc = orh_spf_run(g, &br, 1, job->d_base, job->d_base + nd);
+    ctx->counters = c0;
+    if (rc) return bail(rc);
+  }
+  if (hipEventRecord(job->ev_end, ctx->stream) != hipSuccess)
+    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: event"));
+  *out = job;
+  return ORH_OK;
+}
+
+// runSpf(src, useLinkMetric, ignore) for every request of an ignore-set batch
+// from the plain rows of its distinct sources: a what-if job over those
+// sources, one run, destroyed after its kernels are queued (stream order)
+int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist, uint32_t* d_nh) {
+  orh_ctx* ctx = g->ctx;
+  const uint32_t n_src = req->n_src;
   std::vector<uint32_t> base_srcs, base_row(n_src);
   auto& ro = g->row_of;
   for (uint32_t i = 0; i < n_src; ++i) {
@@ -1105,168 +1369,84 @@ static int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist
     base_row[i] = static_cast<uint32_t>(ro[s]);
   }
   for (uint32_t s : base_srcs) ro[s] = -1;
-  const uint32_t m = static_cast<uint32_t>(base_srcs.size());
-  const size_t nd = static_cast<size_t>(m) * N;
-  int rc = ensure_bytes(ctx, &ctx->d_rep_base, &ctx->d_rep_base_cap, nd * 8);
+  orh_whatif* job = nullptr;
+  ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  int rc = whatif_create(g, base_srcs.data(), static_cast<uint32_t>(base_srcs.size()), req->use_link_metric, &job);
   if (rc) return rc;
-  uint32_t* base_dist = reinterpret_cast<uint32_t*>(ctx->d_rep_base);
-  uint32_t* base_nh = base_dist + nd;
-  rc = ensure_rev(g);
-  if (rc) return rc;
-  // the plain SPFs of the distinct sources (counted below as the batch's runs)
-  orh_spf_request br{};
-  br.h_srcs = base_srcs.data();
-  br.n_src = m;
-  br.use_link_metric = req->use_link_metric;
-  const orh_counters c0 = ctx->counters;
-  rc = orh_spf_run(g, &br, 1, base_dist, base_nh);
-  if (rc) return rc;
-  ctx->counters = c0;
-
-  // staging: base_row[n] | srcs[n] | ign_ptr[n+1] | ign[..] | cut_ptr[n+1] |
-  // flags[n] | (pad to 16 B) cuts uint4[..]
-  const uint32_t n_ign = req->h_ignore_ptr[n_src];
-  std::vector<uint32_t> key;
-  key.reserve(4 + 2 * n_src + 1 + n_ign);
-  const uint64_t gp = reinterpret_cast<uintptr_t>(g);
-  key.insert(key.end(), {static_cast<uint32_t>(gp), static_cast<uint32_t>(gp >> 32),
-                         static_cast<uint32_t>(g->gen), static_cast<uint32_t>(g->gen >> 32), n_src});
-  key.insert(key.end(), req->h_srcs, req->h_srcs + n_src);
-  key.insert(key.end(), req->h_ignore_ptr, req->h_ignore_ptr + n_src + 1);
-  key.insert(key.end(), req->h_ignore_links, req->h_ignore_links + n_ign);
-  size_t off_src = n_src, off_ip = 2 * size_t{n_src}, off_ign = off_ip + n_src + 1, off_cp = 0, off_flags = 0,
-         off_cuts = 0;
-  // the stored key carries the three staging offsets after the request key
-  if (!staged_key_matches(ctx->rep_key, key, 3)) {
-    std::vector<uint32_t> st(base_row);
-    st.insert(st.end(), req->h_srcs, req->h_srcs + n_src);
-    std::vector<uint32_t> ign_ptr(1, 0), ign, cut_ptr(1, 0), cuts;
-    for (uint32_t i = 0; i < n_src; ++i) {
-      std::vector<uint32_t> set(req->h_ignore_links + req->h_ignore_ptr[i],
-                                req->h_ignore_links + req->h_ignore_ptr[i + 1]);
-      std::sort(set.begin(), set.end());
-      set.erase(std::unique(set.begin(), set.end()), set.end());
-      ign.insert(ign.end(), set.begin(), set.end());
-      ign_ptr.push_back(static_cast<uint32_t>(ign.size()));
-      for (uint32_t l : set) {
-        if (l >= g->n_links) continue;
-        for (int k = 0; k < 2; ++k) {
-          const uint32_t e = g->link_ent[2 * static_cast<size_t>(l) + k];
-          if (e == ~0u) continue;
-          cuts.insert(cuts.end(), {row_of(g, e), g->col[e], g->pos[e], 0u});
-        }
-      }
-      cut_ptr.push_back(static_cast<uint32_t>(cuts.size() / 4));
-    }
-    st.insert(st.end(), ign_ptr.begin(), ign_ptr.end());
-    st.insert(st.end(), ign.begin(), ign.end());
-    off_cp = st.size();
-    st.insert(st.end(), cut_ptr.begin(), cut_ptr.end());
-    off_flags = st.size();
-    st.insert(st.end(), n_src + 1, 0u);  // flags, then the slot counter
-    while (st.size() % 4) st.push_back(0u);
-    off_cuts = st.size();
-    st.insert(st.end(), cuts.begin(), cuts.end());
-    st.push_back(0u);
-    while (st.size() % 4) st.push_back(0u);
-    if (st.size() > ctx->d_rep_cap) {
-      hipFree(ctx->d_rep);
-      ctx->d_rep = nullptr;
-      ctx->d_rep_cap = 0;
-      ctx->rep_key.clear();
-      ORH_HIP(ctx, hipMalloc(&ctx->d_rep, st.size() * sizeof(uint32_t)));
-      ctx->d_rep_cap = st.size();
-    }
-    ORH_HIP(ctx, hipMemcpyAsync(ctx->d_rep, st.data(), st.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // st is a local
-    key.insert(key.end(), {static_cast<uint32_t>(off_cp), static_cast<uint32_t>(off_flags),
-                           static_cast<uint32_t>(off_cuts)});
-    ctx->rep_key = std::move(key);
-  }
-  {
-    const auto& k = ctx->rep_key;
-    off_cp = k[k.size() - 3];
-    off_flags = k[k.size() - 2];
-    off_cuts = k[k.size() - 1];
-  }
-  uint32_t* flags = ctx->d_rep + off_flags;
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
-  ORH_HIP(ctx, hipMemsetAsync(flags, 0, (n_src + 1) * sizeof(uint32_t), ctx->stream));
-  // global slots for the requests whose affected set outgrows LDS
-  const size_t slot_bytes = orh::repair_slot_bytes(N, g->n_recs);
-  const uint32_t n_slots = static_cast<uint32_t>(
-      std::min<size_t>(std::min<size_t>(kRepairSlots, n_src), kRepairSlotBudget / std::max<size_t>(slot_bytes, 1)));
-  if (n_slots) {
-    rc = ensure_bytes(ctx, &ctx->d_rep_slots, &ctx->d_rep_slots_cap, n_slots * slot_bytes);
-    if (rc) return rc;
+  rc = whatif_run(job, n_src, base_row.data(), req->h_ignore_ptr, req->h_ignore_links, d_dist, d_nh, nullptr);
+  if (rc) {
+    orh_whatif_destroy(job);
+    return rc;
   }
-  orh::RepairArgs ra{};
-  ra.n_nodes = N;
-  ra.n_req = n_src;
-  ra.use_link_metric = req->use_link_metric;
-  repair_caps(ctx, g->n_nodes, &ra.cap_a, &ra.cap_e);
-  ra.recs = g->d_recs;
-  ra.link = g->d_link;
-  ra.rank_out = g->d_rank_out;
-  ra.rev = g->d_rev;
-  ra.ovl = g->d_ovl;
-  ra.base_dist = base_dist;
-  ra.base_nh = base_nh;
-  ra.base_row = ctx->d_rep;
-  ra.srcs = ctx->d_rep + off_src;
-  ra.ign_ptr = ctx->d_rep + off_ip;
-  ra.ign = ctx->d_rep + off_ign;
-  ra.cut_ptr = ctx->d_rep + off_cp;
-  ra.cuts = reinterpret_cast<const uint4*>(ctx->d_rep + off_cuts);
-  ra.out_dist = d_dist;
-  ra.out_nh = d_nh;
-  ra.fallback = flags;
-  ra.slot_mem = ctx->d_rep_slots;
-  ra.slot_bytes = slot_bytes;
-  ra.n_slots = n_slots;
-  ra.slot_next = flags + n_src;
-  ra.n_recs = g->n_recs;
-  hipError_t e = orh::launch_repair(ra, g->ell_k, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch");
-  // fallback: the full HBM search for the flagged rows only
-  orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
-  fp.variant = orh::SpfVariant::kGlobalNh;
-  fp.block = 1024;  // only the flagged rows search; the rest exit at once
-  rc = ensure_labels(ctx, static_cast<size_t>(n_src) * N);
-  if (rc) return rc;
-  orh::SpfArgs a{};
-  a.n_nodes = N;
-  a.n_out = n_src;
-  a.recs = g->d_recs;
-  a.link = g->d_link;
-  a.srcs = ra.srcs;
-  a.ignore_ptr = ra.ign_ptr;
-  a.ignore_links = ra.ign;
-  a.use_link_metric = req->use_link_metric;
-  a.w0 = req->use_link_metric ? g->max_out : 1u;
-  a.delta = uniform ? a.w0
-                    : std::max<uint32_t>(1u, static_cast<uint32_t>(
-                                                 static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
-  a.out_dist = d_dist;
-  a.scratch = ctx->d_scratch;
-  a.labels = ctx->d_labels;
-  a.out_nh = d_nh;
-  a.words = 1;
-  a.rank_out = g->d_rank_out;
-  a.row_mask = flags;
-  e = orh::launch_spf(fp, a, n_src, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "what-if fallback launch");
   ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  orh_whatif_destroy(job);
   orh_spf_info info{};
   info.variant = static_cast<int32_t>(orh::SpfVariant::kRepair);
   info.rows = n_src;
-  info.batch_sources = m;
+  info.batch_sources = static_cast<uint32_t>(base_srcs.size());
   ctx->last_info = info;
-  ctx->counters.spf_runs += n_src;
-  ctx->counters.spf_launches += 1;
-  ctx->counters.last_kernel_ms = -1.0;
   return ORH_OK;
 }
+
+}  // namespace
+
+extern "C" {
+
+int orh_whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t use_link_metric,
+                      orh_whatif** out) {
+  if (!g || !out || (n_srcs && !h_srcs)) return g ? fail(g->ctx, ORH_E_INVALID, "orh_whatif_create: null argument")
+                                                  : ORH_E_INVALID;
+  *out = nullptr;
+  return whatif_create(g, h_srcs, n_srcs, use_link_metric, out);
+}
+
+int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, const uint32_t* h_ignore_ptr,
+                   const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info) {
+  if (!job) return ORH_E_INVALID;
+  orh_ctx* ctx = job->g->ctx;
+  if (n_req == 0) return ORH_OK;
+  if (!h_src_idx || !h_ignore_ptr || (h_ignore_ptr[n_req] && !h_ignore_links) || !d_dist || !d_nh)
+    return fail(ctx, ORH_E_INVALID, "orh_whatif_run: null argument");
+  if (job->gen != job->g->gen)
+    return fail(ctx, ORH_E_STATE, "orh_whatif_run: the graph changed since the job was created");
+  hipSetDevice(ctx->device);
+  return whatif_run(job, n_req, h_src_idx, h_ignore_ptr, h_ignore_links, d_dist, d_nh, d_info);
+}
+
+int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out) {
+  if (!job || !ms_out) return ORH_E_INVALID;
+  orh_ctx* ctx = job->g->ctx;
+  ORH_HIP(ctx, hipEventSynchronize(job->ev_end));
+  float ms = 0.f;
+  ORH_HIP(ctx, hipEventElapsedTime(&ms, job->ev_begin, job->ev_end));
+  *ms_out = ms;
+  return ORH_OK;
+}
+
+int orh_whatif_destroy(orh_whatif* job) {
+  if (!job) return ORH_E_INVALID;
+  // device buffers may still be read by queued kernels: hipFree waits for the
+  // device; pinned staging is released after its uploads
+  for (int c = 0; c < 2; ++c) {
+    if (job->stage_ev[c]) {
+      hipEventSynchronize(job->stage_ev[c]);
+      hipEventDestroy(job->stage_ev[c]);
+    }
+    if (job->h_stage[c]) hipHostFree(job->h_stage[c]);
+    hipFree(job->d_stage[c]);
+  }
+  hipFree(job->d_work);
+  hipFree(job->d_base);
+  if (job->ev_begin) hipEventDestroy(job->ev_begin);
+  if (job->ev_end) hipEventDestroy(job->ev_end);
+  delete job;
+  return ORH_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // Phase 1 computes a distance row for every requested source and for every
 // distinct neighbour of one (the first-hop phase reads them). Without ignore
@@ -1303,10 +1483,9 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       : req->use_link_metric ? g->sum_max_metric / 2 + g->max_metric
                              : static_cast<uint64_t>(g->n_links) + 1;
   const bool has_ign = req->h_ignore_ptr != nullptr;
-  if (has_ign && ctx->spf_mode == orh::SpfMode::kAuto && max_nbr <= 32 &&
-      repair_eligible(g, req, words, bound, uniform)) {
+  if (has_ign && ctx->spf_mode == orh::SpfMode::kAuto && max_nbr <= 32 && repair_eligible(g, req, words)) {
     hipSetDevice(ctx->device);
-    return run_repair(g, req, d_dist, d_nh, bound, uniform);
+    return run_repair(g, req, d_dist, d_nh);
   }
   const orh::SpfPlan plan =
       orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, !has_ign, ctx->spf_mode);
@@ -1959,6 +2138,162 @@ int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, u
         for (uint32_t l : p) out[w++] = l;
       }
     }
+  return ORH_OK;
+}
+
+// KSP2 for a batch of (src, dst) pairs on the device: the sources' plain
+// rows, the k = 1 traces (ksp_trace_kernel), the k = 2 searches with each
+// pair's k = 1 links ignored (spf_global_nh kernel over the pairs that have
+// k = 1 paths), the k = 2 traces; only the paths leave the device
+constexpr uint32_t kKspOutCap = 1024, kKspIgnCap = 512, kKspHashCap = 2048, kKspStackCap = 1024;
+constexpr uint32_t kKspChunk = 2048;
+
+int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const uint32_t* h_dst,
+                   const uint32_t** out_blocks, uint32_t* block_words) {
+  if (!g || !out_blocks || !block_words || (n_pairs && (!h_src || !h_dst))) return ORH_E_INVALID;
+  orh_ctx* ctx = g->ctx;
+  if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_ksp2_batch: no graph loaded");
+  if (g->has_zero || wide_metrics(g))
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: zero / 64-bit path metrics need the exact kernel's order");
+  const uint32_t N = g->n_nodes;
+  for (uint32_t i = 0; i < n_pairs; ++i)
+    if (h_src[i] >= N || h_dst[i] >= N) return fail(ctx, ORH_E_INVALID, "orh_ksp2_batch: node out of range");
+  *block_words = kKspOutCap;
+  const size_t out_words = static_cast<size_t>(n_pairs) * kKspOutCap;
+  if (out_words > ctx->h_ksp_cap) {
+    if (ctx->h_ksp) hipHostFree(ctx->h_ksp);
+    ctx->h_ksp = nullptr;
+    ctx->h_ksp_cap = 0;
+    ORH_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_ksp), std::max<size_t>(out_words, 1) * 4,
+                               hipHostMallocDefault));
+    ctx->h_ksp_cap = std::max<size_t>(out_words, 1);
+  }
+  *out_blocks = ctx->h_ksp;
+  if (n_pairs == 0) return ORH_OK;
+  hipSetDevice(ctx->device);
+  int rc = ensure_rev(g);
+  if (rc) return rc;
+  const uint64_t bound = g->sum_max_metric / 2 + g->max_metric;
+  const bool uniform = g->min_out == g->max_out;
+  for (uint32_t c0 = 0; c0 < n_pairs; c0 += kKspChunk) {
+    const uint32_t P = std::min(kKspChunk, n_pairs - c0);
+    // distinct sources of the chunk, and each pair's row among them
+    std::vector<uint32_t> srcs, row1(P), rowp(P);
+    auto& ro = g->row_of;
+    for (uint32_t i = 0; i < P; ++i) {
+      const uint32_t x = h_src[c0 + i];
+      if (ro[x] < 0) {
+        ro[x] = static_cast<int32_t>(srcs.size());
+        srcs.push_back(x);
+      }
+      row1[i] = static_cast<uint32_t>(ro[x]);
+      rowp[i] = i;
+    }
+    for (uint32_t x : srcs) ro[x] = -1;
+    const uint32_t S = static_cast<uint32_t>(srcs.size());
+    uint32_t words = 1;
+    rc = orh_spf_words(g, srcs.data(), S, &words);
+    if (rc) return rc;
+    // device layout (u32 words): dist1 [S][N] | nh1 [S][N][words] | dist2 [P][N] | nh2 [P][N] |
+    // src | dst | row1 | rowp | ign_ptr [P+1] | ign [P][cap] | need2 | out | visited | stack
+    const size_t nd1 = static_cast<size_t>(S) * N, nd2 = static_cast<size_t>(P) * N;
+    size_t off = 0;
+    auto take = [&](size_t words_) {
+      const size_t o = off;
+      off += (words_ + 63) & ~size_t{63};  // 256-byte aligned pieces
+      return o;
+    };
+    const size_t o_d1 = take(nd1), o_n1 = take(nd1 * words), o_d2 = take(nd2), o_n2 = take(nd2);
+    const size_t o_src = take(P), o_dst = take(P), o_r1 = take(P), o_rp = take(P), o_ip = take(P + 1);
+    const size_t o_ign = take(size_t{P} * kKspIgnCap), o_need = take(P), o_out = take(size_t{P} * kKspOutCap);
+    const size_t o_vis = take(size_t{P} * kKspHashCap);
+    const size_t o_st = take(size_t{P} * kKspStackCap * (sizeof(orh::KspFrame) / 4));
+    rc = ensure_bytes(ctx, &ctx->d_ksp, &ctx->d_ksp_cap, off * 4);
+    if (rc) return rc;
+    uint32_t* D = reinterpret_cast<uint32_t*>(ctx->d_ksp);
+    // staged request: src | dst | row1 | rowp | ign_ptr (fixed stride)
+    std::vector<uint32_t> ip(P + 1);
+    for (uint32_t i = 0; i <= P; ++i) ip[i] = i * kKspIgnCap;
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_src, h_src + c0, P * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_dst, h_dst + c0, P * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_r1, row1.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_rp, rowp.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_ip, ip.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
+    // k = 1 rows: the sources' plain SPFs (LinkState::getSpfResult)
+    orh_spf_request br{};
+    br.h_srcs = srcs.data();
+    br.n_src = S;
+    br.use_link_metric = 1;
+    const orh_counters c_before = ctx->counters;
+    rc = orh_spf_run(g, &br, words, D + o_d1, D + o_n1);
+    if (rc) return rc;
+    orh::KspArgs ka{};
+    ka.n_nodes = N;
+    ka.n_pairs = P;
+    ka.recs = g->d_recs;
+    ka.link = g->d_link;
+    ka.rev = g->d_rev;
+    ka.name_rank = g->d_name_rank;
+    ka.src = D + o_src;
+    ka.dst = D + o_dst;
+    ka.ign = D + o_ign;
+    ka.ign_cap = kKspIgnCap;
+    ka.need2 = D + o_need;
+    ka.out = D + o_out;
+    ka.out_cap = kKspOutCap;
+    ka.visited = D + o_vis;
+    ka.hash_cap = kKspHashCap;
+    ka.stack = reinterpret_cast<orh::KspFrame*>(D + o_st);
+    ka.stack_cap = kKspStackCap;
+    ka.k = 1;
+    ka.row = D + o_r1;
+    ka.dist = D + o_d1;
+    hipError_t e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=1 trace launch");
+    // k = 2 searches: every pair with k = 1 paths, its k = 1 links ignored
+    // (row mask = need2; one fused first-hop row per pair)
+    orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
+    if (fp.variant == orh::SpfVariant::kUnsupported)
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: no search plan for this graph");
+    fp.variant = orh::SpfVariant::kGlobalNh;
+    fp.block = P <= ctx->n_cu ? 1024u : P <= 2 * ctx->n_cu ? 512u : 256u;
+    rc = ensure_labels(ctx, nd2);
+    if (rc) return rc;
+    orh::SpfArgs a{};
+    a.n_nodes = N;
+    a.n_out = P;
+    a.recs = g->d_recs;
+    a.link = g->d_link;
+    a.srcs = D + o_src;
+    a.ignore_ptr = D + o_ip;
+    a.ignore_links = D + o_ign;
+    a.use_link_metric = 1;
+    a.w0 = g->max_out;
+    a.delta = uniform ? a.w0
+                      : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                   static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+    a.out_dist = D + o_d2;
+    a.scratch = ctx->d_scratch;
+    a.labels = ctx->d_labels;
+    a.out_nh = D + o_n2;
+    a.words = 1;
+    a.rank_out = g->d_rank_out;
+    a.row_mask = D + o_need;
+    e = orh::launch_spf(fp, a, P, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
+    ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
+    ka.k = 2;
+    ka.row = D + o_rp;
+    ka.dist = D + o_d2;
+    e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 trace launch");
+    ORH_HIP(ctx, hipMemcpyAsync(ctx->h_ksp + size_t{c0} * kKspOutCap, D + o_out, size_t{P} * kKspOutCap * 4,
+                                hipMemcpyDeviceToHost, ctx->stream));
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->counters = c_before;  // the caller counts runs the reference's way (memo)
+    ctx->counters.spf_launches += 3;
+  }
   return ORH_OK;
 }
 

@@ -22,6 +22,9 @@ from .types import (K_TESTING_AREA, Adjacency, BinaryAddress, IpPrefix, PrefixEn
                     PrefixMetrics, PrefixType, create_adj_db)
 
 C3_SEED, C4_SEED, C5_SEED = 3003, 4004, 5005
+# C4 batch shape (SURVEY.md §8d / BASELINE.md): 4,096 sampled links x 64
+# sources of runSpf(src, true, {link}), and 1,024 KSP2 (src, dst) pairs
+C4_WHATIF_LINKS, C4_WHATIF_SRCS, C4_KSP2_PAIRS = 4096, 64, 1024
 
 
 def _metrics(rng):
@@ -60,6 +63,18 @@ def c4_what_if_pairs(link_ids: List[int], node_names: List[str], n_links: int, n
     links = rng.sample(link_ids, min(n_links, len(link_ids)))
     srcs = rng.sample(node_names, min(n_srcs, len(node_names)))
     return [(s, l) for l in links for s in srcs]
+
+
+def c4_what_if_job(link_ids: List[int], node_names: List[str], n_links: int = C4_WHATIF_LINKS,
+                   n_srcs: int = C4_WHATIF_SRCS, seed: int = C4_SEED):
+    """The same (source, link) requests as c4_what_if_pairs, as a what-if job:
+    (sources, per request its source index, per request its ignore set)."""
+    rng = random.Random(seed + 1)
+    links = rng.sample(link_ids, min(n_links, len(link_ids)))
+    srcs = rng.sample(node_names, min(n_srcs, len(node_names)))
+    idx = [i for _ in links for i in range(len(srcs))]
+    sets = [[l] for l in links for _ in srcs]
+    return srcs, idx, sets
 
 
 def c4_ksp2_pairs(node_names: List[str], n_pairs: int, seed: int = C4_SEED):

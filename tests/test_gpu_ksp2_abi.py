@@ -74,3 +74,57 @@ def test_ksp2_prefetch_wan_50k(hip, oracle):
     for s, d in pairs:
         for k in (1, 2):
             assert als_h[A].get_kth_paths(s, d, k) == als_o[A].get_kth_paths(s, d, k), (s, d, k)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_ksp2_device_batch_random(hip, oracle, seed):
+    """prefetchKthPaths through orh_ksp2_batch (k = 1 traces, k = 2 searches
+    and k = 2 traces on the device) over every (src, dst) pair of random
+    graphs with parallel links (LinkSet tie order), drained nodes and
+    adjacencies: every pair's k = 1 and k = 2 paths equal the oracle's
+    getKthPaths (LinkState.cpp:762-791), link by link, and spf_runs counts
+    the reference's runs (one per source, one per pair with k = 1 paths)."""
+    dbs = random_topology(2100 + seed, n=20, extra=34, max_metric=4, parallel=0.4, overload=0.1,
+                          link_overload=0.06)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    pairs = [(s, d) for s in names for d in names]
+    ls = als_h[A]._impl
+    runs0 = ls.spf_runs
+    ls.prefetch_kth_paths(pairs)
+    dev, host = ls.ksp_stats()
+    assert dev == len(pairs) and host == 0
+    runs_o0 = als_o[A]._impl.spf_runs
+    for s, d in pairs:
+        for k in (1, 2):
+            assert als_h[A].get_kth_paths(s, d, k) == als_o[A].get_kth_paths(s, d, k), (s, d, k)
+    assert ls.spf_runs - runs0 == als_o[A]._impl.spf_runs - runs_o0
+
+
+def test_ksp2_device_batch_c4(hip, oracle, monkeypatch):
+    """The C4 KSP2 batch as bench_legs.leg_c4 runs it: c4_wan() (seed 4004),
+    1,024 seeded (src, dst) pairs through the device batch. All 1,024 pairs'
+    paths equal the product's host traces over device rows (ORH_KSP_HOST=1,
+    the traceOnePath restatement checked against the oracle above), and
+    three sampled pairs equal the oracle's getKthPaths at full size."""
+    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan
+    adj, _ = c4_wan()
+    als_h, _ = load_topology(hip, adj, [])
+    ls = als_h[A]._impl
+    pairs = c4_ksp2_pairs(ls.node_names(), C4_KSP2_PAIRS)
+    ls.prefetch_kth_paths(pairs)
+    dev, host = ls.ksp_stats()
+    assert dev == len(set(pairs)) and host == 0
+    got = {(s, d, k): als_h[A].get_kth_paths(s, d, k) for s, d in pairs for k in (1, 2)}
+    assert sum(len(v) for v in got.values()) > len(pairs)
+    monkeypatch.setenv("ORH_KSP_HOST", "1")
+    als_r, _ = load_topology(hip, adj, [])
+    als_r[A]._impl.prefetch_kth_paths(pairs)
+    assert als_r[A]._impl.ksp_stats()[0] == 0
+    for (s, d, k), v in got.items():
+        assert v == als_r[A].get_kth_paths(s, d, k), (s, d, k)
+    als_o, _ = load_topology(oracle, adj, [])
+    for s, d in random.Random(7).sample(pairs, 3):
+        for k in (1, 2):
+            assert got[(s, d, k)] == als_o[A].get_kth_paths(s, d, k), (s, d, k)

@@ -203,3 +203,65 @@ def test_repair_wan_50k(hip, oracle, repair_mode):
         m = int(nh[v])
         got[names[v]] = (int(dist[v]), sorted(nbrs[b] for b in range(32) if m >> b & 1))
     assert got == ref
+
+
+def _oracle_rows(ls_o, order, nbrs, srcs, ignores, threads=16):
+    dist, nh = ls_o._impl.spf_tables(srcs, order, nbrs, threads, ignores)
+    return dist, nh[:, :, 0]
+
+
+def test_c4_bench_batch_vs_oracle(hip, oracle):
+    """The C4 what-if batch exactly as bench_legs.leg_c4 runs it: c4_wan()
+    (seed 4004), 4,096 links x 64 sources = 262,144 runSpf(src, true, {link})
+    through one what-if job in chunks of 4,096. Every request's tier and
+    affected-node count come back from the product; then, against the
+    oracle's runSpf (LinkState.cpp:808-882) in full (dist + first hops of all
+    50k nodes): all 64 base rows, the 24 requests with the largest affected
+    sets, 24 seeded repaired ones and 8 seeded ones whose source row stands."""
+    from openr_amd.workloads import c4_wan, c4_what_if_job
+    adj, _ = c4_wan()
+    als_h, _ = load_topology(hip, adj, [])
+    ls = als_h[A]._impl
+    names = ls.node_names()
+    links = ls.link_ids()
+    desc = dict(links)
+    srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
+    assert len(srcs) == 64 and len(idx) == 4096 * 64
+    big = ls.what_if_batch(srcs, idx, sets, 4096)
+    big.run()
+    big.sync()
+    info = big.info()
+    tier, affected = info & 7, info >> 3
+    assert int(tier.max()) <= 3, "a request took the full-search fallback although slots exist"
+    assert np.array_equal(tier == 0, affected == 0)
+    repaired = np.nonzero(affected)[0]
+    assert 0 < len(repaired) < len(idx)
+    rng = random.Random(44)
+    top = [int(i) for i in repaired[np.argsort(-affected[repaired], kind="stable")[:24]]]
+    rest = sorted(set(int(i) for i in repaired) - set(top))
+    pick = top + rng.sample(rest, 24) + rng.sample([int(i) for i in np.nonzero(affected == 0)[0]], 8)
+    sub = ls.what_if_batch(srcs, [idx[i] for i in pick], [sets[i] for i in pick], len(pick))
+    sub.run()
+    sub.sync()
+    assert np.array_equal(sub.info(), info[pick])
+    got = [sub.fetch(k) for k in range(len(pick))]
+
+    als_o, _ = load_topology(oracle, adj, [])
+    nbrs = {s: ls.neighbors(s) for s in srcs}
+    base = ls.sweep(srcs, True)
+    base.run()
+    base.sync()
+    q_srcs = srcs + [srcs[idx[i]] for i in pick]
+    q_ign = [[] for _ in srcs] + [[desc[sets[i][0]][:3]] for i in pick]
+    dist_o, nh_o = _oracle_rows(als_o[A], names, [nbrs[s] for s in q_srcs], q_srcs, q_ign)
+    for k, s in enumerate(srcs):
+        d, m = base.fetch(k)
+        np.testing.assert_array_equal(d, dist_o[k], err_msg=f"base dist {s}")
+        np.testing.assert_array_equal(m, nh_o[k], err_msg=f"base nh {s}")
+    for k, i in enumerate(pick):
+        d, m = got[k]
+        np.testing.assert_array_equal(d, dist_o[len(srcs) + k], err_msg=f"request {i} dist")
+        np.testing.assert_array_equal(m, nh_o[len(srcs) + k], err_msg=f"request {i} nh")
+        changed = int(np.sum((d != dist_o[idx[i]]) | (m != nh_o[idx[i]])))
+        assert changed <= affected[i], (i, changed, affected[i])
+    assert affected[top[0]] > 100  # the largest sets leave the small LDS tier
