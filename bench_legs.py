@@ -105,22 +105,23 @@ def leg_c3(hip, cpu):
     return out
 
 
-def leg_c4(hip, cpu, reps=3):
+def leg_c4(hip, cpu, reps=3, chunk=None):
     """C4 at BASELINE.md's shape: 4,096 links x 64 sources = 262,144
     runSpf(src, true, {link}) as one what-if job (64 plain searches, then the
-    requests in chunks of 4,096 into one device row buffer: every request's
+    requests in chunks of C4_WHATIF_CHUNK into one device row buffer: every request's
     full dist + first-hop row is written to HBM, chunk after chunk), and 1,024
     KSP2 (src, dst) pairs."""
     from openr_amd.facade import load_topology
     from openr_amd.types import K_TESTING_AREA as A
-    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan, c4_what_if_job
+    from openr_amd.workloads import C4_KSP2_PAIRS, C4_WHATIF_CHUNK, c4_ksp2_pairs, c4_wan, c4_what_if_job
     adj, _ = c4_wan()
     als, _ = load_topology(hip, adj, [])
     ls = als[A]._impl
     names = ls.node_names()
     links = ls.link_ids()
     srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
-    batch = ls.what_if_batch(srcs, idx, sets, 4096)
+    chunk = chunk or C4_WHATIF_CHUNK
+    batch = ls.what_if_batch(srcs, idx, sets, chunk)
     batch.run()
     batch.sync()
     walls, devs = [], []
@@ -148,7 +149,7 @@ def leg_c4(hip, cpu, reps=3):
            "what_if_spfs_per_s": round(n_req / dt, 1),
            "what_if_batch": (f"{n_req} runSpf(src, true, {{link}}) = {len(sets) // len(srcs)} links x "
                              f"{len(srcs)} sources: one what-if job (the sources' plain searches + "
-                             f"{(n_req + 4095) // 4096} chunks of 4,096 requests into one device row buffer)"),
+                             f"{(n_req + chunk - 1) // chunk} chunks of {chunk:,} requests into one device row buffer)"),
            "what_if_batch_ms": round(dt * 1e3, 3),
            "what_if_device_ms": round(dev_ms, 3),
            "what_if_tiers": {"source_row": tiers[0], "lds_small": tiers[1], "lds_large": tiers[2],

@@ -278,8 +278,13 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
                    const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info);
 #define ORH_WHATIF_TIER(x) ((x) & 7u) /* 0 source row, 1/2 LDS repair, 3 global-slot repair, 4 full search */
 #define ORH_WHATIF_AFFECTED(x) ((x) >> 3)
+/* A run's few large repairs may still be in flight on the job's internal
+ * second stream when later work is queued on the context stream; after
+ * orh_whatif_flush every row of every run so far is complete in stream order
+ * (a later run waits by itself before it overwrites rows of an earlier one). */
+int orh_whatif_flush(orh_whatif* job);
 /* device time from the job's creation (base searches) to the end of its last
- * run (HIP events; waits for that run) */
+ * run (flushes; HIP events; waits for that run) */
 int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out);
 int orh_whatif_destroy(orh_whatif* job);
 

@@ -429,16 +429,27 @@ class WhatIfBatch {
     graph_ = ls.deviceGraph();
     ctx_ = ls.context();
     orh_graph_info(graph_, &n_, &edges_);
+    // two row buffers, alternating between chunks, so a chunk's large repairs
+    // overlap the next chunk's copy and small repairs
     const size_t rows = static_cast<size_t>(chunk_) * n_;
-    if (orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dDist_)) != ORH_OK ||
-        orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dNh_)) != ORH_OK ||
-        orh_device_alloc(ctx_, std::max<size_t>(n, 1) * 4, reinterpret_cast<void**>(&dInfo_)) != ORH_OK)
+    nBuf_ = chunks_.size() > 1 ? 2 : 1;
+    for (int b = 0; b < nBuf_; ++b)
+      if (orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dDist_[b])) != ORH_OK ||
+          orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dNh_[b])) != ORH_OK)
+        throw std::runtime_error("WhatIfBatch: device allocation failed");
+    if (nBuf_ == 1) {
+      dDist_[1] = dDist_[0];
+      dNh_[1] = dNh_[0];
+    }
+    if (orh_device_alloc(ctx_, std::max<size_t>(n, 1) * 4, reinterpret_cast<void**>(&dInfo_)) != ORH_OK)
       throw std::runtime_error("WhatIfBatch: device allocation failed");
   }
   ~WhatIfBatch() {
     if (job_) orh_whatif_destroy(job_);
-    orh_device_free(ctx_, dDist_);
-    orh_device_free(ctx_, dNh_);
+    for (int b = 0; b < nBuf_; ++b) {
+      orh_device_free(ctx_, dDist_[b]);
+      orh_device_free(ctx_, dNh_[b]);
+    }
     orh_device_free(ctx_, dInfo_);
   }
   void run() {  // asynchronous on the context stream
@@ -449,10 +460,13 @@ class WhatIfBatch {
       throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
     for (const auto& c : chunks_) {
       const uint32_t nr = static_cast<uint32_t>(c.hi - c.lo);
-      if (orh_whatif_run(job_, nr, srcIdx_.data() + c.lo, c.ptr.data(), c.links.data(), dDist_, dNh_,
+      const int b = static_cast<int>((&c - chunks_.data()) & 1);  // alternate row buffers
+      if (orh_whatif_run(job_, nr, srcIdx_.data() + c.lo, c.ptr.data(), c.links.data(), dDist_[b], dNh_[b],
                          dInfo_ + c.lo) != ORH_OK)
         throw std::runtime_error(std::string("orh_whatif_run: ") + orh_last_error(ctx_));
     }
+    if (orh_whatif_flush(job_) != ORH_OK)
+      throw std::runtime_error(std::string("orh_whatif_flush: ") + orh_last_error(ctx_));
   }
   double lastMs() {
     double ms = 0;
@@ -472,9 +486,10 @@ class WhatIfBatch {
     const auto& last = chunks_.back();
     if (i < last.lo || i >= last.hi) throw std::out_of_range("WhatIfBatch.fetch: not in the last chunk");
     const size_t r = i - last.lo;
+    const int b = static_cast<int>((chunks_.size() - 1) & 1);
     py::array_t<uint32_t> dist(n_), nh(n_);
-    orh_memcpy_d2h(ctx_, dist.mutable_data(), dDist_ + r * n_, n_ * 4ull);
-    orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_ + r * n_, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, dist.mutable_data(), dDist_[b] + r * n_, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_[b] + r * n_, n_ * 4ull);
     return py::make_tuple(dist, nh);
   }
   size_t requests() const { return srcIdx_.size(); }
@@ -495,8 +510,9 @@ class WhatIfBatch {
   orh_ctx* ctx_{nullptr};
   orh_whatif* job_{nullptr};
   uint32_t n_{0}, edges_{0};
-  uint32_t* dDist_{nullptr};
-  uint32_t* dNh_{nullptr};
+  int nBuf_{1};
+  uint32_t* dDist_[2] = {nullptr, nullptr};
+  uint32_t* dNh_[2] = {nullptr, nullptr};
   uint32_t* dInfo_{nullptr};
 };
 
@@ -682,7 +698,7 @@ PYBIND11_MODULE(_openr_host, m) {
                std::sort(nhs.begin(), nhs.end());
                py::list pls;
                for (const auto& pl : r.pathLinks())
-                 pls.append(py::make_tuple(linkDesc(s.link(pl.link)), pl.prevNode));
+                 pls.append(py::make_tuple(linkDesc(s.link(pl.link.id())), pl.prevNode));
                d[py::str(name)] = py::make_tuple(static_cast<uint64_t>(r.metric()), nhs, pls);
              }
              return d;
@@ -705,10 +721,30 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("get_kth_paths",
            [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
              py::list out;
-             for (const auto& p : s.getKthPaths(a, b, k)) {
+             for (const auto& p : s.getKthPathIds(a, b, k)) {
                py::list path;
                for (uint32_t lid : p) path.append(linkDesc(s.link(lid)));
                out.append(path);
+             }
+             return out;
+           })
+      .def("walk_kth_paths",  // the reference-typed getKthPaths (LinkRef handles) walked
+                              // as selectBestPathsKsp2 does (Decision.cpp:1035-1076):
+                              // per link from `src` (metric from the near end, near
+                              // interface, far node, nhV6 from src on the first link)
+           [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
+             py::list out;
+             for (const auto& path : s.getKthPaths(a, b, k)) {
+               py::list hops;
+               std::string cur = a;
+               for (auto& link : path) {
+                 hops.append(py::make_tuple(link->getMetricFromNode(cur), link->getIfaceFromNode(cur),
+                                            link->getOtherNodeName(cur), link->getArea(), link->isUp()));
+                 cur = link->getOtherNodeName(cur);
+               }
+               const auto& first = path.front();
+               out.append(py::make_tuple(hops, pyBytes(first->getNhV6FromNode(a).addr),
+                                         first->getIfaceFromNode(a)));
              }
              return out;
            })

@@ -7,6 +7,8 @@
 // observable (folly pair hash for PrefixEntries / Link, see hash.h).
 #pragma once
 
+#include "parallel.h"
+
 #include <array>
 #include <cstdint>
 #include <iterator>
@@ -227,6 +229,27 @@ class ShardedMap {
   static constexpr size_t kShards = 64;
   using Shard = std::unordered_map<K, V, H>;
   using value_type = typename Shard::value_type;
+  // maps at least this large are freed on the Reclaimer thread
+  static constexpr size_t kAsyncFree = 1u << 16;
+
+  ShardedMap() = default;
+  ShardedMap(const ShardedMap&) = default;
+  ShardedMap(ShardedMap&&) noexcept = default;
+  ShardedMap& operator=(const ShardedMap& o) {
+    if (this != &o) {
+      reclaim();
+      s_ = o.s_;
+    }
+    return *this;
+  }
+  ShardedMap& operator=(ShardedMap&& o) noexcept {
+    if (this != &o) {
+      reclaim();
+      s_ = std::move(o.s_);
+    }
+    return *this;
+  }
+  ~ShardedMap() { reclaim(); }
 
   static size_t shardOf(const K& k) {
     return static_cast<size_t>((static_cast<uint64_t>(H{}(k)) * 0x9E3779B97F4A7C15ull) >> 58);
@@ -315,6 +338,13 @@ class ShardedMap {
   const Shard& shard(size_t i) const { return s_[i]; }
 
  private:
+  // hands a large map's nodes to the Reclaimer thread (this map is left empty)
+  void reclaim() {
+    if (size() < kAsyncFree || !Reclaimer::usable()) return;
+    auto* held = new std::array<Shard, kShards>(std::move(s_));
+    for (auto& sh : s_) sh = Shard();
+    if (!Reclaimer::instance().post([held] { delete held; })) delete held;
+  }
   std::array<Shard, kShards> s_;
 };
 

@@ -277,6 +277,7 @@ void LinkState::invalidate(bool topologyChanged) {
     spfResults_.clear();
     spfMaps_.clear();
     kthPaths_.clear();
+    kthLinkPaths_.clear();
     countedOnDevice_.clear();
   }
 }
@@ -817,11 +818,11 @@ void LinkState::prefetchKthPathsHost(const std::vector<std::pair<std::string, st
     if (kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{2}))) continue;
     if (!queued.insert(pr).second) continue;
     std::unordered_set<uint32_t> s;
-    for (const auto& p : getKthPaths(pr.first, pr.second, 1))
+    for (const auto& p : getKthPathIds(pr.first, pr.second, 1))
       for (uint32_t lid : p) s.insert(lid);
     auto id = nodeId(pr.first);
     if (s.empty() || !id) {
-      getKthPaths(pr.first, pr.second, 2);  // no re-run needed (memoized row)
+      getKthPathIds(pr.first, pr.second, 2);  // no re-run needed (memoized row)
       continue;
     }
     ids.push_back(*id);
@@ -878,7 +879,7 @@ const SpfResult& LinkState::getSpfResult(const std::string& node, bool useLinkMe
       if (!row.reachable(v)) continue;
       NodeSpfResult r(row.metric(v));
       row.forEachNextHop(v, [&](uint32_t nb) { r.addNextHop(names_[nb]); });
-      for (const auto& [lid, prev] : pathLinks(row, v)) r.addPath(lid, names_[prev]);
+      for (const auto& [lid, prev] : pathLinks(row, v)) r.addPath(LinkRef(this, lid), names_[prev]);
       res.emplace(names_[v], std::move(r));
     }
   }
@@ -976,8 +977,23 @@ std::optional<Path> LinkState::traceOnePath(uint32_t src, uint32_t dst, const Sp
   return std::nullopt;
 }
 
-const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
-                                                size_t k) const {
+const std::vector<LinkPath>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
+                                                    size_t k) const {
+  auto key = std::make_tuple(src, dst, k);
+  auto it = kthLinkPaths_.find(key);
+  if (it != kthLinkPaths_.end()) return it->second;
+  std::vector<LinkPath> out;
+  for (const auto& p : getKthPathIds(src, dst, k)) {
+    LinkPath lp;
+    lp.reserve(p.size());
+    for (uint32_t lid : p) lp.emplace_back(this, lid);
+    out.push_back(std::move(lp));
+  }
+  return kthLinkPaths_.emplace(key, std::move(out)).first->second;
+}
+
+const std::vector<Path>& LinkState::getKthPathIds(const std::string& src, const std::string& dst,
+                                                  size_t k) const {
   if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");
   auto key = std::make_tuple(src, dst, k);
   auto it = kthPaths_.find(key);
@@ -985,7 +1001,7 @@ const std::vector<Path>& LinkState::getKthPaths(const std::string& src, const st
 
   std::unordered_set<uint32_t> ignore;
   for (size_t i = 1; i < k; ++i)
-    for (const auto& p : getKthPaths(src, dst, i))
+    for (const auto& p : getKthPathIds(src, dst, i))
       for (uint32_t lid : p) ignore.insert(lid);
 
   std::vector<Path> paths;
@@ -1020,6 +1036,64 @@ std::vector<Path> LinkState::traceKthPaths(const std::string& src, const std::st
   }
   return paths;
 }
+
+bool LinkState::pathAInPathB(const LinkPath& a, const LinkPath& b) {  // LinkState.h:395-410
+  if (a.size() > b.size()) return false;
+  for (size_t i = 0; i + a.size() <= b.size(); ++i) {
+    size_t k = 0;
+    while (k < a.size() && a[k] == b[i + k]) ++k;
+    if (k == a.size()) return true;
+  }
+  return false;
+}
+
+// ---- LinkRef (LinkState.cpp:163-260, :347-360) -------------------------------
+const Link& LinkRef::raw() const { return ls_->link(id_); }
+bool LinkRef::end1(const std::string& nodeName) const {
+  const Link& l = raw();
+  if (ls_->nodeName(l.n1) == nodeName) return true;
+  if (ls_->nodeName(l.n2) == nodeName) return false;
+  throw std::invalid_argument(nodeName);
+}
+const std::string& LinkRef::getArea() const { return raw().area; }
+const std::string& LinkRef::getOtherNodeName(const std::string& nodeName) const {
+  return ls_->nodeName(end1(nodeName) ? raw().n2 : raw().n1);
+}
+const std::string& LinkRef::firstNodeName() const { return raw().on1; }
+const std::string& LinkRef::secondNodeName() const { return raw().on2; }
+const std::string& LinkRef::getIfaceFromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().if1 : raw().if2;
+}
+Metric LinkRef::getMetricFromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().metric1.value() : raw().metric2.value();
+}
+int32_t LinkRef::getAdjLabelFromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().adjLabel1 : raw().adjLabel2;
+}
+bool LinkRef::getOverloadFromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().overload1.value() : raw().overload2.value();
+}
+const BinaryAddress& LinkRef::getNhV4FromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().nhV41 : raw().nhV42;
+}
+const BinaryAddress& LinkRef::getNhV6FromNode(const std::string& nodeName) const {
+  return end1(nodeName) ? raw().nhV61 : raw().nhV62;
+}
+bool LinkRef::isUp() const { return raw().isUp(); }
+bool LinkRef::hasHolds() const {
+  const Link& l = raw();
+  return l.holdUpTtl != 0 || l.metric1.hasHold() || l.metric2.hasHold() || l.overload1.hasHold() ||
+         l.overload2.hasHold();
+}
+std::string LinkRef::toString() const {  // LinkState.cpp:363-366
+  const Link& l = raw();
+  return l.area + " - " + ls_->nodeName(l.n1) + "%" + l.if1 + " <---> " + ls_->nodeName(l.n2) + "%" + l.if2;
+}
+std::string LinkRef::directionalToString(const std::string& fromNode) const {  // :368-377
+  return getArea() + " - " + fromNode + "%" + getIfaceFromNode(fromNode) + " ---> " +
+         getOtherNodeName(fromNode) + "%" + getIfaceFromNode(getOtherNodeName(fromNode));
+}
+bool LinkRef::operator<(const LinkRef& o) const { return raw().less(o.raw()); }
 
 bool LinkState::pathAInPathB(const Path& a, const Path& b) {  // LinkState.h:395-410
   if (a.size() > b.size()) return false;

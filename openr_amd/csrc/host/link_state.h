@@ -103,6 +103,49 @@ struct Link {
 
 using Path = std::vector<uint32_t>;  // link ids, src -> dst
 
+class LinkState;
+
+// A link of a LinkState in the shape the reference's callers use its
+// std::shared_ptr<Link> (LinkState.h:82-175, getters LinkState.cpp:163-260):
+// `link->getMetricFromNode(name)`, `link->getOtherNodeName(name)`, ... so
+// code such as selectBestPathsKsp2's label / nexthop loop
+// (Decision.cpp:1035-1076) compiles unchanged over getKthPaths' paths and
+// NodeSpfResult::pathLinks. A node that is not an end of the link throws
+// std::invalid_argument (LinkState.cpp:171). Valid while the LinkState
+// lives; the id is the LinkState's link id (LinkState::link).
+class LinkRef {
+ public:
+  LinkRef() = default;
+  LinkRef(const LinkState* ls, uint32_t id) : ls_(ls), id_(id) {}
+  const LinkRef* operator->() const { return this; }
+  uint32_t id() const { return id_; }
+  const Link& raw() const;
+
+  const std::string& getArea() const;
+  const std::string& getOtherNodeName(const std::string& nodeName) const;
+  const std::string& firstNodeName() const;
+  const std::string& secondNodeName() const;
+  const std::string& getIfaceFromNode(const std::string& nodeName) const;
+  Metric getMetricFromNode(const std::string& nodeName) const;
+  int32_t getAdjLabelFromNode(const std::string& nodeName) const;
+  bool getOverloadFromNode(const std::string& nodeName) const;
+  const BinaryAddress& getNhV4FromNode(const std::string& nodeName) const;
+  const BinaryAddress& getNhV6FromNode(const std::string& nodeName) const;
+  bool isUp() const;
+  bool hasHolds() const;
+  std::string toString() const;
+  std::string directionalToString(const std::string& fromNode) const;
+  bool operator==(const LinkRef& o) const { return ls_ == o.ls_ && id_ == o.id_; }
+  bool operator!=(const LinkRef& o) const { return !(*this == o); }
+  bool operator<(const LinkRef& o) const;  // Link::operator< (hash, ordered names)
+
+ private:
+  bool end1(const std::string& nodeName) const;  // true: end 1, false: end 2, else throws
+  const LinkState* ls_{nullptr};
+  uint32_t id_{0};
+};
+using LinkPath = std::vector<LinkRef>;  // the reference's LinkState::Path (links src -> dst)
+
 // One source's SPF result as produced by the device: dist row + first-hop
 // bitmask row over the source's distinct neighbours (orh_graph_neighbors).
 // Rows of the exact kernel (zero-metric links, or path metrics that can reach
@@ -145,15 +188,15 @@ struct SpfRow {
 // (LinkState::link(id)) instead of a shared_ptr<Link>
 class NodeSpfResult {
  public:
-  struct PathLink {
-    uint32_t link;
+  struct PathLink {  // LinkState.h:205-210
+    LinkRef link;
     std::string prevNode;
   };
   explicit NodeSpfResult(Metric m) : metric_(m) {}
   Metric metric() const { return metric_; }
   const std::vector<PathLink>& pathLinks() const { return pathLinks_; }
   const std::unordered_set<std::string>& nextHops() const { return nextHops_; }
-  void addPath(uint32_t link, const std::string& prevNode) { pathLinks_.push_back({link, prevNode}); }
+  void addPath(LinkRef link, const std::string& prevNode) { pathLinks_.push_back({link, prevNode}); }
   void addNextHop(const std::string& nh) { nextHops_.insert(nh); }
 
  private:
@@ -188,8 +231,13 @@ class LinkState {
   // fresh SPF with links ignored (runSpf(src, true, linksToIgnore))
   SpfRow runSpf(const std::string& node, bool useLinkMetric,
                 const std::vector<uint32_t>& ignoreLinks) const;
-  const std::vector<Path>& getKthPaths(const std::string& src, const std::string& dst,
-                                       size_t k) const;
+  // getKthPaths (LinkState.cpp:762-791) as link ids (what the route build
+  // reads) and in the reference's type, links as LinkRef handles
+  // (LinkState.h:293-294); both memoized per (src, dst, k)
+  const std::vector<Path>& getKthPathIds(const std::string& src, const std::string& dst,
+                                         size_t k) const;
+  const std::vector<LinkPath>& getKthPaths(const std::string& src, const std::string& dst,
+                                           size_t k) const;
 
   // batched forms: one device launch for many SPFs (the reference runs them
   // one by one). runSpfBatch: sources by node id, optional per-source ignore
@@ -212,6 +260,7 @@ class LinkState {
   std::vector<std::pair<uint32_t, uint32_t>> pathLinks(
       const SpfRow& row, uint32_t v, const std::unordered_set<uint32_t>* ignore = nullptr) const;
   static bool pathAInPathB(const Path& a, const Path& b);
+  static bool pathAInPathB(const LinkPath& a, const LinkPath& b);
 
   bool hasNode(const std::string& n) const { return adjacencyDatabases_.count(n) != 0; }
   bool isNodeOverloaded(const std::string& n) const;
@@ -292,6 +341,7 @@ class LinkState {
   mutable std::map<std::pair<std::string, bool>, SpfRow> spfResults_;
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMaps_;  // getSpfResult views
   mutable std::map<std::tuple<std::string, std::string, size_t>, std::vector<Path>> kthPaths_;
+  mutable std::map<std::tuple<std::string, std::string, size_t>, std::vector<LinkPath>> kthLinkPaths_;
   mutable uint64_t spfRuns_{0};
   // sources whose SPF a device KSP2 batch ran and counted (the reference's
   // memoized getSpfResult, LinkState.cpp:775-776) without keeping the row on

@@ -61,9 +61,30 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidat
     if (invalidated) ++*invalidated;
     return false;
   }
-  // the kept nexthops move into the new set as nodes (the weight is part of
-  // the hash, so it is set between extract and insert): no copies of their
-  // strings, no allocations
+  // NextHopHash leaves the weight out, so with one weight across the set (no
+  // two nexthops differ only by weight, e.g. every route fresh from
+  // buildRouteDb) the weights are set in place and dropped nexthops erased:
+  // bucket positions stay valid and no two elements can become equal
+  bool sameWeight = true;
+  for (const auto& nh : route.nexthops)
+    if (nh.weight != route.nexthops.begin()->weight) {
+      sameWeight = false;
+      break;
+    }
+  if (sameWeight) {
+    for (auto it = route.nexthops.begin(); it != route.nexthops.end();) {
+      const int32_t w = weightOf(*it);
+      if (w <= 0) {
+        it = route.nexthops.erase(it);
+      } else {
+        const_cast<NextHopThrift&>(*it).weight = w;  // not part of the hash
+        ++it;
+      }
+    }
+    return true;
+  }
+  // otherwise the kept nexthops move into a new set as nodes: no copies of
+  // their strings, no allocations
   NextHopSet out;
   out.reserve(route.nexthops.size());
   while (!route.nexthops.empty()) {

@@ -588,12 +588,12 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsKsp2(
   for (const auto& [area, ls] : als) {
     for (const auto& [node, bestArea] : r.allNodeAreas) {
       if (node == me && bestArea == area) continue;
-      for (const auto& p : ls.getKthPaths(me, node, 1)) paths.push_back({&ls, p});
+      for (const auto& p : ls.getKthPathIds(me, node, 1)) paths.push_back({&ls, p});
     }
     const size_t firstPaths = paths.size();
     for (const auto& [node, bestArea] : r.allNodeAreas) {
       if (area != bestArea) continue;
-      for (const auto& sp : ls.getKthPaths(me, node, 2)) {
+      for (const auto& sp : ls.getKthPathIds(me, node, 2)) {
         bool add = true;
         for (size_t i = 0; i < firstPaths; ++i) {
           // link identity is per LinkState; paths of other areas never match

@@ -384,7 +384,24 @@ size_t repair_slot_bytes(uint32_t n_nodes, uint32_t n_recs) {
   return (repair_lds_bytes(n_nodes, n_nodes, n_recs) + 255) & ~static_cast<size_t>(255);
 }
 
-hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
+namespace {
+
+size_t tier1_lds(const RepairArgs& a, uint32_t* sa, uint32_t* se) {
+  *sa = std::min(kSmallA, a.cap_a);
+  *se = std::min(kSmallE, a.cap_e);
+  return repair_lds_bytes(a.n_nodes, *sa, *se);
+}
+
+// queue-draining grids: as many workgroups as the LDS lets share a CU (one
+// request each at a time), never more than there are requests
+uint32_t tier_grid(const RepairArgs& a, size_t lds_limit, size_t lds, uint32_t per_cu_cap) {
+  const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(per_cu_cap, std::max<size_t>(1, lds_limit / lds)));
+  return std::max<uint32_t>(1u, std::min<uint32_t>(a.n_req, a.n_cu * per_cu));
+}
+
+}  // namespace
+
+hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
   if (a.n_req == 0) return hipSuccess;
   if (ell_k != 4 && ell_k != 8) return hipErrorInvalidValue;
   const uint32_t tiles = (a.n_nodes + kCopyTile - 1) / kCopyTile;
@@ -398,34 +415,35 @@ hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, 
                        al(a.out_nh);
   hipLaunchKernelGGL(whatif_copy_kernel, dim3(static_cast<uint32_t>(grid)), dim3(256), 0, s, a, tiles, vec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // queue-draining grids: as many workgroups as the LDS lets share a CU
-  // (one request each at a time), never more than there are requests
-  auto tier_grid = [&](size_t lds, uint32_t per_cu_cap) {
-    const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(per_cu_cap, std::max<size_t>(1, lds_limit / lds)));
-    return std::max<uint32_t>(1u, std::min<uint32_t>(a.n_req, a.n_cu * per_cu));
-  };
-  const uint32_t sa = std::min(kSmallA, a.cap_a), se = std::min(kSmallE, a.cap_e);
-  const size_t lds1 = repair_lds_bytes(a.n_nodes, sa, se);
-  const size_t lds2 = repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
-  const bool small_tier = lds1 < lds2;
-  if (small_tier) {
+  uint32_t sa = 0, se = 0;
+  const size_t lds1 = tier1_lds(a, &sa, &se);
+  if (lds1 < repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e)) {
     if (ell_k == 8)
-      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSmall>), dim3(tier_grid(lds1, 16)), dim3(128), lds1, s,
-                         a, sa, se, 0u);
+      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
+                         dim3(128), lds1, s, a, sa, se, 0u);
     else
-      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSmall>), dim3(tier_grid(lds1, 16)), dim3(128), lds1, s,
-                         a, sa, se, 0u);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
+                         dim3(128), lds1, s, a, sa, se, 0u);
+    e = hipGetLastError();
   }
+  return e;
+}
+
+hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
+  if (a.n_req == 0) return hipSuccess;
+  if (ell_k != 4 && ell_k != 8) return hipErrorInvalidValue;
+  uint32_t sa = 0, se = 0;
+  const size_t lds2 = repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
   // without the small tier, tier 2 drains queue 0 itself
-  const uint32_t q2 = small_tier ? 1u : 0u;
+  const uint32_t q2 = tier1_lds(a, &sa, &se) < lds2 ? 1u : 0u;
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(lds2, 8)), dim3(256), lds2, s, a,
-                       a.cap_a, a.cap_e, q2);
+    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)), dim3(256),
+                       lds2, s, a, a.cap_a, a.cap_e, q2);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierLarge>), dim3(tier_grid(lds2, 8)), dim3(256), lds2, s, a,
-                       a.cap_a, a.cap_e, q2);
-  if ((e = hipGetLastError()) != hipSuccess || a.n_slots == 0) return e;
+    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)), dim3(256),
+                       lds2, s, a, a.cap_a, a.cap_e, q2);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || a.n_slots == 0) return e;
   if (ell_k == 8)
     hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
@@ -433,6 +451,11 @@ hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, 
     hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   return hipGetLastError();
+}
+
+hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
+  hipError_t e = launch_repair_front(a, ell_k, lds_limit, s);
+  return e != hipSuccess ? e : launch_repair_back(a, ell_k, lds_limit, s);
 }
 
 }  // namespace orh

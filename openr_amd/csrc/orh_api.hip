@@ -70,6 +70,7 @@ struct orh_ctx {
   size_t h_ksp_cap = 0;       // in u32
   uint8_t* d_rep_slots = nullptr;  // global repair slots (requests that outgrow LDS)
   size_t d_rep_slots_cap = 0;
+  const orh_whatif* slots_owner = nullptr;  // the what-if job using them (one at a time)
   uint32_t* h_pinned = nullptr;  // orh_spf_batch_pinned's host rows (hipHostMalloc)
   size_t h_pinned_cap = 0;       // in u32
   // ORH_WHATIF_REPAIR: 0 off, 1 automatic (sources repeat, small ignore
@@ -1118,18 +1119,28 @@ struct orh_whatif {
   uint64_t bound = 0;
   std::vector<uint32_t> srcs;
   uint32_t* d_base = nullptr;  // dist rows [m][N], then mask rows [m][N]
-  // request staging: two pinned host / device buffer pairs, alternating, so
-  // a batch's upload never waits for the previous batch's kernels
+  // runs alternate between two slots, each with its request staging (pinned
+  // host + device), its work queues / counters / fallback flags, and the
+  // side-stream part of its last run: the few large repairs (tiers 2, 3) of
+  // run r run on `side` while run r + 1's seed / copy / tier 1 run on the
+  // context stream
+  hipStream_t side = nullptr;
   uint32_t* h_stage[2] = {nullptr, nullptr};
   uint32_t* d_stage[2] = {nullptr, nullptr};
   size_t stage_cap[2] = {0, 0};  // u32, both sides
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};  // upload done
+  uint32_t* d_work[2] = {nullptr, nullptr};     // queues [3][n] | counters | fallback flags [n]
+  size_t work_cap[2] = {0, 0};
+  hipEvent_t front_ev[2] = {nullptr, nullptr};  // context-stream part done
+  hipEvent_t side_ev[2] = {nullptr, nullptr};   // side-stream part done
+  bool pending[2] = {false, false};             // side part not yet joined into the context stream
+  uintptr_t out_lo[2] = {0, 0}, out_hi[2] = {0, 0};  // output span of that run (hazard checks)
   int cur = 0;
-  // queues [3][n] | counters | fallback flags [n] (stream-ordered reuse)
-  uint32_t* d_work = nullptr;
-  size_t work_cap = 0;
-  hipEvent_t ev_begin = nullptr, ev_end = nullptr;  // create .. last run
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;  // create .. last flush
   uint64_t requests = 0;
+  // tier-3 slots: the context's (when no other job holds them) or the job's own
+  uint8_t* own_slots = nullptr;
+  size_t own_slots_cap = 0;
 };
 
 namespace {
@@ -1175,6 +1186,20 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   const size_t off_cp = off_ign + n_ign;
   const size_t off_cuts = (off_cp + n_req + 1 + 3) & ~size_t{3};
   const size_t words = off_cuts + 4 * n_cuts + 4;
+  {
+    // slot `cur` is reused: its previous run's side part must be done (the
+    // context stream waits); so must the other slot's when it writes rows
+    // this run overwrites
+    const int c = job->cur;
+    const uintptr_t lo = std::min(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh));
+    const uintptr_t hi = std::max(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh)) +
+                         size_t{n_req} * N * 4;
+    for (int k = 0; k < 2; ++k)
+      if (job->pending[k] && (k == c || (lo < job->out_hi[k] && job->out_lo[k] < hi))) {
+        ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[k], 0));
+        job->pending[k] = false;
+      }
+  }
   uint32_t *h = nullptr, *d = nullptr;
   int rc = whatif_stage(job, words, &h, &d);
   if (rc) return rc;
@@ -1212,22 +1237,32 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ORH_HIP(ctx, hipEventRecord(job->stage_ev[c], ctx->stream));
 
   const size_t work = 3 * size_t{n_req} + orh::kWhatifCounters + n_req;
-  if (work > job->work_cap) {
-    hipFree(job->d_work);
-    job->d_work = nullptr;
-    job->work_cap = 0;
-    ORH_HIP(ctx, hipMalloc(&job->d_work, work * 4));
-    job->work_cap = work;
+  if (work > job->work_cap[c]) {
+    if (job->pending[c]) ORH_HIP(ctx, hipStreamSynchronize(job->side));  // its old buffer may be in use
+    hipFree(job->d_work[c]);
+    job->d_work[c] = nullptr;
+    job->work_cap[c] = 0;
+    ORH_HIP(ctx, hipMalloc(&job->d_work[c], work * 4));
+    job->work_cap[c] = work;
   }
-  uint32_t* counters = job->d_work + 3 * size_t{n_req};
+  uint32_t* counters = job->d_work[c] + 3 * size_t{n_req};
   uint32_t* flags = counters + orh::kWhatifCounters;
   ORH_HIP(ctx, hipMemsetAsync(counters, 0, (orh::kWhatifCounters + n_req) * 4ull, ctx->stream));
   const size_t slot_bytes = orh::repair_slot_bytes(N, g->n_recs);
   const uint32_t n_slots = static_cast<uint32_t>(std::min<size_t>(
       std::min<size_t>(kRepairSlots, n_req), kRepairSlotBudget / std::max<size_t>(slot_bytes, 1)));
+  uint8_t* slot_mem = nullptr;
   if (n_slots) {
-    rc = ensure_bytes(ctx, &ctx->d_rep_slots, &ctx->d_rep_slots_cap, n_slots * slot_bytes);
+    // the context's slots while no other job's side stream may use them,
+    // else the job's own; grown only with the side stream idle
+    if (!ctx->slots_owner) ctx->slots_owner = job;
+    const bool borrowed = ctx->slots_owner == job;
+    uint8_t** p = borrowed ? &ctx->d_rep_slots : &job->own_slots;
+    size_t* cap = borrowed ? &ctx->d_rep_slots_cap : &job->own_slots_cap;
+    if (n_slots * slot_bytes > *cap) ORH_HIP(ctx, hipStreamSynchronize(job->side));
+    rc = ensure_bytes(ctx, p, cap, n_slots * slot_bytes);
     if (rc) return rc;
+    slot_mem = *p;
   }
   const size_t nd = static_cast<size_t>(m) * N;
   orh::RepairArgs ra{};
@@ -1252,15 +1287,21 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ra.out_nh = d_nh;
   ra.fallback = flags;
   ra.info = d_info;
-  ra.queues = job->d_work;
+  ra.queues = job->d_work[c];
   ra.counters = counters;
-  ra.slot_mem = ctx->d_rep_slots;
+  ra.slot_mem = slot_mem;
   ra.slot_bytes = slot_bytes;
   ra.n_slots = n_slots;
   ra.n_recs = g->n_recs;
   ra.n_cu = ctx->n_cu;
-  hipError_t e = orh::launch_repair(ra, g->ell_k, ctx->lds_limit, ctx->stream);
+  hipError_t e = orh::launch_repair_front(ra, g->ell_k, ctx->lds_limit, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch");
+  ORH_HIP(ctx, hipEventRecord(job->front_ev[c], ctx->stream));
+  // the large repairs on the side stream, after this run's front part; the
+  // previous side part is ordered before them on that stream
+  ORH_HIP(ctx, hipStreamWaitEvent(job->side, job->front_ev[c], 0));
+  e = orh::launch_repair_back(ra, g->ell_k, ctx->lds_limit, job->side);
+  if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch (large tiers)");
   if (n_slots == 0) {
     // no slot fits the budget: the requests that outgrew tier 2 are searched
     // in full (spf_global_nh_kernel with the flags as its row mask)
@@ -1268,6 +1309,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
                                     orh::SpfMode::kGlobal);
     fp.variant = orh::SpfVariant::kGlobalNh;
     fp.block = 1024;  // only the flagged rows search; the rest exit at once
+    ORH_HIP(ctx, hipStreamSynchronize(job->side));  // labels may be grown below
     rc = ensure_labels(ctx, static_cast<size_t>(n_req) * N);
     if (rc) return rc;
     orh::SpfArgs a{};
@@ -1290,14 +1332,31 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
     a.words = 1;
     a.rank_out = g->d_rank_out;
     a.row_mask = flags;
-    e = orh::launch_spf(fp, a, n_req, ctx->stream);
+    e = orh::launch_spf(fp, a, n_req, job->side);
     if (e != hipSuccess) return hip_fail(ctx, e, "what-if fallback launch");
   }
-  ORH_HIP(ctx, hipEventRecord(job->ev_end, ctx->stream));
+  ORH_HIP(ctx, hipEventRecord(job->side_ev[c], job->side));
+  job->pending[c] = true;
+  job->out_lo[c] = std::min(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh));
+  job->out_hi[c] = std::max(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh)) +
+                   size_t{n_req} * N * 4;
   job->requests += n_req;
   ctx->counters.spf_runs += n_req;  // one runSpf per request (LinkState.cpp:815)
   ctx->counters.spf_launches += 1;
   ctx->counters.last_kernel_ms = -1.0;
+  return ORH_OK;
+}
+
+// the side-stream parts of every run so far join the context stream: work
+// queued on it afterwards sees all of the job's rows
+int whatif_flush(orh_whatif* job) {
+  orh_ctx* ctx = job->g->ctx;
+  for (int c = 0; c < 2; ++c)
+    if (job->pending[c]) {
+      ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[c], 0));
+      job->pending[c] = false;
+    }
+  ORH_HIP(ctx, hipEventRecord(job->ev_end, ctx->stream));
   return ORH_OK;
 }
 
@@ -1326,8 +1385,13 @@ int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t
     orh_whatif_destroy(job);
     return code;
   };
-  if (hipEventCreate(&job->ev_begin) != hipSuccess || hipEventCreate(&job->ev_end) != hipSuccess)
-    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
+  if (hipEventCreate(&job->ev_begin) != hipSuccess || hipEventCreate(&job->ev_end) != hipSuccess ||
+      hipStreamCreateWithFlags(&job->side, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events / stream"));
+  for (int c = 0; c < 2; ++c)
+    if (hipEventCreateWithFlags(&job->front_ev[c], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&job->side_ev[c], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
   rc = ensure_rev(g);
   if (rc) return bail(rc);
   const size_t nd = static_cast<size_t>(std::max<uint32_t>(n_srcs, 1)) * g->n_nodes;
@@ -1375,6 +1439,7 @@ int run_repair(orh_graph* g, const orh_spf_request* req, uint32_t* d_dist, uint3
   if (rc) return rc;
   ORH_HIP(ctx, hipEventRecord(ctx->evm, ctx->stream));
   rc = whatif_run(job, n_src, base_row.data(), req->h_ignore_ptr, req->h_ignore_links, d_dist, d_nh, nullptr);
+  if (!rc) rc = whatif_flush(job);
   if (rc) {
     orh_whatif_destroy(job);
     return rc;
@@ -1414,9 +1479,17 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
   return whatif_run(job, n_req, h_src_idx, h_ignore_ptr, h_ignore_links, d_dist, d_nh, d_info);
 }
 
+int orh_whatif_flush(orh_whatif* job) {
+  if (!job) return ORH_E_INVALID;
+  hipSetDevice(job->g->ctx->device);
+  return whatif_flush(job);
+}
+
 int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out) {
   if (!job || !ms_out) return ORH_E_INVALID;
   orh_ctx* ctx = job->g->ctx;
+  int rc = whatif_flush(job);
+  if (rc) return rc;
   ORH_HIP(ctx, hipEventSynchronize(job->ev_end));
   float ms = 0.f;
   ORH_HIP(ctx, hipEventElapsedTime(&ms, job->ev_begin, job->ev_end));
@@ -1426,9 +1499,16 @@ int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out) {
 
 int orh_whatif_destroy(orh_whatif* job) {
   if (!job) return ORH_E_INVALID;
-  // device buffers may still be read by queued kernels: hipFree waits for the
-  // device; pinned staging is released after its uploads
+  // queued kernels may still read the job's buffers: drain both streams
+  if (job->side) {
+    whatif_flush(job);
+    hipStreamSynchronize(job->side);
+  }
+  hipStreamSynchronize(job->g->ctx->stream);
   for (int c = 0; c < 2; ++c) {
+    hipFree(job->d_work[c]);
+    if (job->front_ev[c]) hipEventDestroy(job->front_ev[c]);
+    if (job->side_ev[c]) hipEventDestroy(job->side_ev[c]);
     if (job->stage_ev[c]) {
       hipEventSynchronize(job->stage_ev[c]);
       hipEventDestroy(job->stage_ev[c]);
@@ -1436,8 +1516,10 @@ int orh_whatif_destroy(orh_whatif* job) {
     if (job->h_stage[c]) hipHostFree(job->h_stage[c]);
     hipFree(job->d_stage[c]);
   }
-  hipFree(job->d_work);
   hipFree(job->d_base);
+  hipFree(job->own_slots);
+  if (job->g->ctx->slots_owner == job) job->g->ctx->slots_owner = nullptr;
+  if (job->side) hipStreamDestroy(job->side);
   if (job->ev_begin) hipEventDestroy(job->ev_begin);
   if (job->ev_end) hipEventDestroy(job->ev_end);
   delete job;

@@ -25,6 +25,9 @@ C3_SEED, C4_SEED, C5_SEED = 3003, 4004, 5005
 # C4 batch shape (SURVEY.md §8d / BASELINE.md): 4,096 sampled links x 64
 # sources of runSpf(src, true, {link}), and 1,024 KSP2 (src, dst) pairs
 C4_WHATIF_LINKS, C4_WHATIF_SRCS, C4_KSP2_PAIRS = 4096, 64, 1024
+# requests per what-if run (one device row buffer of CHUNK x N x 8 bytes: 6.6 GB
+# at N = 50,000)
+C4_WHATIF_CHUNK = 16384
 
 
 def _metrics(rng):

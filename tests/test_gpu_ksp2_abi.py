@@ -128,3 +128,35 @@ def test_ksp2_device_batch_c4(hip, oracle, monkeypatch):
     for s, d in random.Random(7).sample(pairs, 3):
         for k in (1, 2):
             assert got[(s, d, k)] == als_o[A].get_kth_paths(s, d, k), (s, d, k)
+
+
+def test_kth_paths_link_handles(hip, oracle):
+    """getKthPaths in the reference's type: paths of LinkRef handles walked as
+    selectBestPathsKsp2 walks them (Decision.cpp:1035-1076:
+    link->getMetricFromNode(cur), getOtherNodeName, getIfaceFromNode,
+    getNhV6FromNode of the first link), equal to the oracle's links and
+    directional metrics."""
+    dbs = random_topology(2200, n=16, extra=26, max_metric=6, parallel=0.4, overload=0.0,
+                          link_overload=0.0)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    adj = {(db.thisNodeName, a.ifName): a for db in dbs for a in db.adjacencies}
+    walked = 0
+    for src in names[:4]:
+        for dst in names:
+            for k in (1, 2):
+                got = als_h[A]._impl.walk_kth_paths(src, dst, k)
+                want = als_o[A].get_kth_paths(src, dst, k)
+                assert len(got) == len(want), (src, dst, k)
+                for (hops, nh6, if0), path in zip(got, want):
+                    cur = src
+                    for (metric, iface, other, area, up), l in zip(hops, path):
+                        near_if, far = (l.if1, l.n2) if l.n1 == cur else (l.if2, l.n1)
+                        assert (iface, other, area, up) == (near_if, far, A, True)
+                        assert metric == als_o[A]._impl.metric_from_node(l.n1, l.if1, cur)
+                        cur = far
+                        walked += 1
+                    assert cur == dst
+                    assert nh6 == adj[(src, if0)].nextHopV6.addr
+    assert walked > 50

@@ -213,12 +213,12 @@ def _oracle_rows(ls_o, order, nbrs, srcs, ignores, threads=16):
 def test_c4_bench_batch_vs_oracle(hip, oracle):
     """The C4 what-if batch exactly as bench_legs.leg_c4 runs it: c4_wan()
     (seed 4004), 4,096 links x 64 sources = 262,144 runSpf(src, true, {link})
-    through one what-if job in chunks of 4,096. Every request's tier and
+    through one what-if job in chunks of C4_WHATIF_CHUNK. Every request's tier and
     affected-node count come back from the product; then, against the
     oracle's runSpf (LinkState.cpp:808-882) in full (dist + first hops of all
     50k nodes): all 64 base rows, the 24 requests with the largest affected
     sets, 24 seeded repaired ones and 8 seeded ones whose source row stands."""
-    from openr_amd.workloads import c4_wan, c4_what_if_job
+    from openr_amd.workloads import C4_WHATIF_CHUNK, c4_wan, c4_what_if_job
     adj, _ = c4_wan()
     als_h, _ = load_topology(hip, adj, [])
     ls = als_h[A]._impl
@@ -227,7 +227,7 @@ def test_c4_bench_batch_vs_oracle(hip, oracle):
     desc = dict(links)
     srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
     assert len(srcs) == 64 and len(idx) == 4096 * 64
-    big = ls.what_if_batch(srcs, idx, sets, 4096)
+    big = ls.what_if_batch(srcs, idx, sets, C4_WHATIF_CHUNK)
     big.run()
     big.sync()
     info = big.info()
