@@ -278,6 +278,9 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
                    const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info);
 #define ORH_WHATIF_TIER(x) ((x) & 7u) /* 0 source row, 1/2 LDS repair, 3 global-slot repair, 4 full search */
 #define ORH_WHATIF_AFFECTED(x) ((x) >> 3)
+/* search the job's sources again on the graph as it is now (after topology
+ * deltas; allocations are kept) - the next runs derive from these rows */
+int orh_whatif_refresh(orh_whatif* job);
 /* A run's few large repairs may still be in flight on the job's internal
  * second stream when later work is queued on the context stream; after
  * orh_whatif_flush every row of every run so far is complete in stream order

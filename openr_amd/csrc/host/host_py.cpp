@@ -452,12 +452,14 @@ class WhatIfBatch {
     }
     orh_device_free(ctx_, dInfo_);
   }
-  void run() {  // asynchronous on the context stream
-    if (job_) orh_whatif_destroy(job_);
-    job_ = nullptr;
-    if (orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
-                          &job_) != ORH_OK)
-      throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
+  void run() {  // asynchronous on the context stream: the base searches, then every chunk
+    if (!job_) {
+      if (orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
+                            &job_) != ORH_OK)
+        throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
+    } else if (orh_whatif_refresh(job_) != ORH_OK) {
+      throw std::runtime_error(std::string("orh_whatif_refresh: ") + orh_last_error(ctx_));
+    }
     for (const auto& c : chunks_) {
       const uint32_t nr = static_cast<uint32_t>(c.hi - c.lo);
       const int b = static_cast<int>((&c - chunks_.data()) & 1);  // alternate row buffers

@@ -66,9 +66,9 @@ size_t repair_slot_bytes(uint32_t n_nodes, uint32_t n_recs);
 // seed, copy each request's base rows, then the repair tiers; with no slots
 // the requests that outgrow tier 2 get fallback[r] = 1 (zeroed beforehand)
 hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
-// the same in two parts: seed, copy and tier 1 (nearly all requests, the
-// whole GPU), then tiers 2 and 3 (a few large repairs, a few workgroups),
-// which may run on a second stream, overlapping the next batch's front part
+// the same in two parts: seed and copy (HBM-bound, the whole GPU), then the
+// repair tiers (latency-bound, a few thousand workgroups), which may run on a
+// second stream, overlapping the next batch's copy
 hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
 hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
 

@@ -414,28 +414,27 @@ hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_l
   const uint32_t vec = (a.n_nodes & 3u) == 0 && al(a.base_dist) && al(a.base_nh) && al(a.out_dist) &&
                        al(a.out_nh);
   hipLaunchKernelGGL(whatif_copy_kernel, dim3(static_cast<uint32_t>(grid)), dim3(256), 0, s, a, tiles, vec);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  uint32_t sa = 0, se = 0;
-  const size_t lds1 = tier1_lds(a, &sa, &se);
-  if (lds1 < repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e)) {
-    if (ell_k == 8)
-      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
-                         dim3(128), lds1, s, a, sa, se, 0u);
-    else
-      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
-                         dim3(128), lds1, s, a, sa, se, 0u);
-    e = hipGetLastError();
-  }
-  return e;
+  return hipGetLastError();
 }
 
 hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
   if (a.n_req == 0) return hipSuccess;
   if (ell_k != 4 && ell_k != 8) return hipErrorInvalidValue;
   uint32_t sa = 0, se = 0;
+  const size_t lds1 = tier1_lds(a, &sa, &se);
   const size_t lds2 = repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
+  if (lds1 < lds2) {
+    if (ell_k == 8)
+      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
+                         dim3(128), lds1, s, a, sa, se, 0u);
+    else
+      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSmall>), dim3(tier_grid(a, lds_limit, lds1, 16)),
+                         dim3(128), lds1, s, a, sa, se, 0u);
+    const hipError_t e1 = hipGetLastError();
+    if (e1 != hipSuccess) return e1;
+  }
   // without the small tier, tier 2 drains queue 0 itself
-  const uint32_t q2 = tier1_lds(a, &sa, &se) < lds2 ? 1u : 0u;
+  const uint32_t q2 = lds1 < lds2 ? 1u : 0u;
   if (ell_k == 8)
     hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)), dim3(256),
                        lds2, s, a, a.cap_a, a.cap_e, q2);

@@ -305,6 +305,23 @@ void build_ms_layout(orh_graph* g, std::vector<uint2>& recs) {
       for (uint32_t j = inl; j < d; ++j) put(ovf++, dv, v, e0 + j);
     }
   }
+  // the pull OR is order-free, so each node's inline slots are sorted by
+  // neighbour id: a slot then reads the same relative neighbour (e.g. "lower
+  // anti-diagonal, left") across a wave's consecutive Cuthill-McKee nodes,
+  // consecutive frontier words instead of a mix of directions at the border
+  // rows (bank conflicts of the ds_read_b32 gathers). ORH_MS_SORT=0: CSR order.
+  const char* es = getenv("ORH_MS_SORT");
+  if (!(es && atoi(es) == 0)) {
+    for (uint32_t dv = 0; dv < N; ++dv) {
+      uint2* r = recs.data() + static_cast<size_t>(dv) * K;
+      const uint32_t n_inl = (r[K - 1].x & ORH_REC_CONT) ? K - 1 : K;
+      std::stable_sort(r, r + n_inl, [](const uint2& a, const uint2& b) {
+        const uint32_t ka = (a.x & ORH_REC_SKIP) ? ~0u : (a.x & ORH_REC_COL_MASK);
+        const uint32_t kb = (b.x & ORH_REC_SKIP) ? ~0u : (b.x & ORH_REC_COL_MASK);
+        return ka < kb;
+      });
+    }
+  }
   // interval skip (spf_msbfs_kernel<..., true>), opt-in with ORH_MS_SKIP=1:
   // it cuts a lone corner batch of the C2 grid from 0.48 to 0.32 ms, but the
   // all-sources sweep stays at 0.75-0.77 ms either way (profiles/r02/
@@ -1119,6 +1136,7 @@ struct orh_whatif {
   uint64_t bound = 0;
   std::vector<uint32_t> srcs;
   uint32_t* d_base = nullptr;  // dist rows [m][N], then mask rows [m][N]
+  size_t base_cap = 0;         // bytes
   // runs alternate between two slots, each with its request staging (pinned
   // host + device), its work queues / counters / fallback flags, and the
   // side-stream part of its last run: the few large repairs (tiers 2, 3) of
@@ -1360,6 +1378,56 @@ int whatif_flush(orh_whatif* job) {
   return ORH_OK;
 }
 
+// the plain SPFs of the job's sources into its base rows, on the graph as it
+// is now (create, and orh_whatif_refresh after topology changes); the side
+// parts of earlier runs, which read the old rows, are joined first
+int whatif_base(orh_whatif* job) {
+  orh_graph* g = job->g;
+  orh_ctx* ctx = g->ctx;
+  uint64_t bound = 0;
+  bool uniform = false;
+  int rc = whatif_plan(g, job->use_link_metric != 0, &bound, &uniform);
+  if (rc) return rc;
+  for (uint32_t s : job->srcs) {
+    if (s >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "what-if: source out of range");
+    if (n_distinct(g, s) > 32) return fail(ctx, ORH_E_UNSUPPORTED, "what-if: a source has more than 32 neighbours");
+  }
+  job->uniform = uniform;
+  job->bound = bound;
+  rc = ensure_rev(g);
+  if (rc) return rc;
+  for (int c = 0; c < 2; ++c)
+    if (job->pending[c]) {
+      ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[c], 0));
+      job->pending[c] = false;
+    }
+  const uint32_t m = static_cast<uint32_t>(job->srcs.size());
+  const size_t nd = static_cast<size_t>(std::max<uint32_t>(m, 1)) * g->n_nodes;
+  if (nd * 8 > job->base_cap) {
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    hipFree(job->d_base);
+    job->d_base = nullptr;
+    job->base_cap = 0;
+    if (hipMalloc(&job->d_base, nd * 8) != hipSuccess) return fail(ctx, ORH_E_NOMEM, "what-if: base rows");
+    job->base_cap = nd * 8;
+  }
+  ORH_HIP(ctx, hipEventRecord(job->ev_begin, ctx->stream));
+  if (m) {
+    // internal searches: spf_runs counts the requests
+    orh_spf_request br{};
+    br.h_srcs = job->srcs.data();
+    br.n_src = m;
+    br.use_link_metric = job->use_link_metric;
+    const orh_counters c0 = ctx->counters;
+    rc = orh_spf_run(g, &br, 1, job->d_base, job->d_base + static_cast<size_t>(m) * g->n_nodes);
+    ctx->counters = c0;
+    if (rc) return rc;
+  }
+  ORH_HIP(ctx, hipEventRecord(job->ev_end, ctx->stream));
+  job->gen = g->gen;
+  return ORH_OK;
+}
+
 int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t use_link_metric,
                   orh_whatif** out) {
   orh_ctx* ctx = g->ctx;
@@ -1392,26 +1460,8 @@ int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t
     if (hipEventCreateWithFlags(&job->front_ev[c], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&job->side_ev[c], hipEventDisableTiming) != hipSuccess)
       return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
-  rc = ensure_rev(g);
+  rc = whatif_base(job);
   if (rc) return bail(rc);
-  const size_t nd = static_cast<size_t>(std::max<uint32_t>(n_srcs, 1)) * g->n_nodes;
-  if (hipMalloc(&job->d_base, nd * 8) != hipSuccess)
-    return bail(fail(ctx, ORH_E_NOMEM, "orh_whatif_create: base rows"));
-  if (hipEventRecord(job->ev_begin, ctx->stream) != hipSuccess)
-    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: event"));
-  if (n_srcs) {
-    // the plain SPFs of the sources (internal: spf_runs counts the requests)
-    orh_spf_request br{};
-    br.h_srcs = job->srcs.data();
-    br.n_src = n_srcs;
-    br.use_link_metric = job->use_link_metric;
-    const orh_counters c0 = ctx->counters;
-    rc = orh_spf_run(g, &br, 1, job->d_base, job->d_base + nd);
-    ctx->counters = c0;
-    if (rc) return bail(rc);
-  }
-  if (hipEventRecord(job->ev_end, ctx->stream) != hipSuccess)
-    return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: event"));
   *out = job;
   return ORH_OK;
 }
@@ -1477,6 +1527,12 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
     return fail(ctx, ORH_E_STATE, "orh_whatif_run: the graph changed since the job was created");
   hipSetDevice(ctx->device);
   return whatif_run(job, n_req, h_src_idx, h_ignore_ptr, h_ignore_links, d_dist, d_nh, d_info);
+}
+
+int orh_whatif_refresh(orh_whatif* job) {
+  if (!job) return ORH_E_INVALID;
+  hipSetDevice(job->g->ctx->device);
+  return whatif_base(job);
 }
 
 int orh_whatif_flush(orh_whatif* job) {

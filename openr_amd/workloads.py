@@ -25,9 +25,10 @@ C3_SEED, C4_SEED, C5_SEED = 3003, 4004, 5005
 # C4 batch shape (SURVEY.md §8d / BASELINE.md): 4,096 sampled links x 64
 # sources of runSpf(src, true, {link}), and 1,024 KSP2 (src, dst) pairs
 C4_WHATIF_LINKS, C4_WHATIF_SRCS, C4_KSP2_PAIRS = 4096, 64, 1024
-# requests per what-if run (one device row buffer of CHUNK x N x 8 bytes: 6.6 GB
-# at N = 50,000)
-C4_WHATIF_CHUNK = 16384
+# requests per what-if run: two alternating device row buffers of
+# CHUNK x N x 8 bytes (2 x 26 GB at N = 50,000 of the 288 GB HBM), so the
+# large repairs of one chunk overlap the next chunk's copy
+C4_WHATIF_CHUNK = 65536
 
 
 def _metrics(rng):

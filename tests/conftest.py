@@ -59,6 +59,13 @@ def hip():
     return host_backend()
 
 
-@pytest.fixture(params=["oracle", pytest.param("hip", marks=pytest.mark.gpu)])
-def backend(request):
+@pytest.fixture(params=["oracle", pytest.param("hip", marks=pytest.mark.gpu),
+                        pytest.param("hip_default_select", marks=pytest.mark.gpu)])
+def backend(request, monkeypatch):
+    """hip runs route selection on the device at every size (as set above);
+    hip_default_select is the product's own default, where builds of fewer
+    than 1,024 prefixes - every reference-sized test - select on the host."""
+    if request.param == "hip_default_select":
+        monkeypatch.delenv("ORH_DEVICE_SELECT_MIN", raising=False)
+        return request.getfixturevalue("hip")
     return request.getfixturevalue(request.param)
