@@ -194,38 +194,22 @@ def leg_c5(hip, cpu):
            "load_s": round(load_s, 2),
            "build_route_db_ms": round(_route_ms(solver, "me", als, ps, 3), 2)}
     out.update(_select_roofline(solver, "me", als, ps))
-    # incremental stress (SURVEY.md §8d C5): 10k prefix add / withdraw
-    # advertisements plus 100 adjacency-metric changes, then one rebuild
+    policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
+        0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
+    # Decision::rebuildRoutes over Decision::routeDb_ (DecisionRib,
+    # Decision.cpp:1865-1930), RibPolicy applied: the first full rebuild
+    # builds everything; the full rebuild after the incremental stress runs as
+    # a delta against routeDb_ (device selection compared on the device with
+    # the previous snapshot; only changed routes built, policy-applied and
+    # compared); calculateUpdate semantics either way
     import random
     from openr_amd.types import PrefixEntry, PrefixMetrics
+    rib = hip.module.DecisionRib()
+    _, first_s = rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, True, [], policy._impl, wire=False)
+    # incremental stress (SURVEY.md §8d C5): 10k prefix add / withdraw
+    # advertisements plus 100 adjacency-metric changes, then one full rebuild
     rng = random.Random(55)
     t0 = time.perf_counter()
-    for i in range(10_000):
-        node, area, e = pfx[rng.randrange(len(pfx))]
-        if i % 2:
-            ps.delete_prefix(node, area, e.prefix)
-        else:
-            ps.update_prefix(node, area, PrefixEntry(e.prefix, metrics=PrefixMetrics(
-                1, rng.randint(0, 3), rng.randint(0, 3), rng.randint(0, 3)), tags=e.tags))
-    for _ in range(100):
-        a = rng.choice(C5_AREAS)
-        db = areas[a][rng.randrange(len(areas[a]) - 1)]
-        db.adjacencies[rng.randrange(len(db.adjacencies))].metric = rng.randint(1, 4)
-        als[a].update_adjacency_database(db)
-    upd_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    rebuild_s, _ = solver._impl.time_build_route_db("me", als._impl, ps._impl)
-    out["incremental"] = {"updates": "10k prefix add/withdraw + 100 adjacency metric changes",
-                          "apply_s": round(upd_s, 3),
-                          "rebuild_ms": round(rebuild_s * 1e3, 2),
-                          # + freeing the returned 1M-route DB (glibc), outside the reference's
-                          # route_build_ms too
-                          "rebuild_wall_ms": round((time.perf_counter() - t0) * 1e3, 2)}
-    # Decision::rebuildRoutes after prefix-only updates (Decision.cpp:1902-1924):
-    # only the updated prefixes are rebuilt (one device selection pass over
-    # the prefix mirror + host materialisation of those routes)
-    rib = hip.module.DecisionRib()
-    rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, True, [])
     changed = set()
     for i in range(10_000):
         node, area, e = pfx[rng.randrange(len(pfx))]
@@ -235,13 +219,47 @@ def leg_c5(hip, cpu):
             got = ps.update_prefix(node, area, PrefixEntry(e.prefix, metrics=PrefixMetrics(
                 1, rng.randint(0, 3), rng.randint(0, 3), rng.randint(0, 3)), tags=e.tags))
         changed |= {(p.prefixAddress.addr, p.prefixLength) for p in got}
-    (uu, ud, _, _), sec = rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, False, sorted(changed))
+    for _ in range(100):
+        a = rng.choice(C5_AREAS)
+        db = areas[a][rng.randrange(len(areas[a]) - 1)]
+        db.adjacencies[rng.randrange(len(db.adjacencies))].metric = rng.randint(1, 4)
+        als[a].update_adjacency_database(db)
+    upd_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    (uu, ud, mu, md), reb_s = rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, True, sorted(changed),
+                                                policy._impl, wire=False)
+    wall_s = time.perf_counter() - t0
+    # the same state built whole (buildRouteDb alone, no policy) for comparison
+    whole_s, _ = solver._impl.time_build_route_db("me", als._impl, ps._impl)
+    out["incremental"] = {"updates": "10k prefix add/withdraw + 100 adjacency metric changes",
+                          "apply_s": round(upd_s, 3),
+                          "first_full_rebuild_ms": round(first_s * 1e3, 2),
+                          "rebuild_ms": round(reb_s * 1e3, 2),
+                          "rebuild_wall_ms": round(wall_s * 1e3, 2),
+                          "ran_as": "delta" if rib.delta_rebuilds else "whole build",
+                          "routes_updated": uu, "routes_deleted": ud,
+                          "mpls_updated": mu, "mpls_deleted": md,
+                          "whole_build_route_db_ms": round(whole_s * 1e3, 2),
+                          "note": "Decision::rebuildRoutes with RibPolicy: buildRouteDb + applyPolicy + "
+                                  "calculateUpdate + routeDb_.update, the delta freed inside"}
+    # Decision::rebuildRoutes after prefix-only updates (Decision.cpp:1902-1924):
+    # only the updated prefixes are rebuilt (one device selection pass over
+    # the prefix mirror + host materialisation of those routes)
+    changed = set()
+    for i in range(10_000):
+        node, area, e = pfx[rng.randrange(len(pfx))]
+        if i % 2:
+            got = ps.delete_prefix(node, area, e.prefix)
+        else:
+            got = ps.update_prefix(node, area, PrefixEntry(e.prefix, metrics=PrefixMetrics(
+                1, rng.randint(0, 3), rng.randint(0, 3), rng.randint(0, 3)), tags=e.tags))
+        changed |= {(p.prefixAddress.addr, p.prefixLength) for p in got}
+    (uu, ud, _, _), sec = rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, False, sorted(changed),
+                                            policy._impl, wire=False)
     out["incremental_prefix_only"] = {"updates": "10k prefix add/withdraw, no topology change",
                                       "prefixes_rebuilt": len(changed),
                                       "rebuild_ms": round(sec * 1e3, 2),
-                                      "routes_updated": len(uu), "routes_deleted": len(ud)}
-    policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
-        0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
+                                      "routes_updated": uu, "routes_deleted": ud}
     build_s, policy_s, routes, updated = solver._impl.time_build_route_db_with_policy(
         "me", als._impl, ps._impl, policy._impl)
     out.update({"build_plus_policy_ms": round((build_s + policy_s) * 1e3, 2),

@@ -404,6 +404,15 @@ typedef struct orh_select_out {
 /* asynchronous on the context stream; the area table is copied */
 int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
                      const orh_select_area* h_areas, const orh_select_out* out);
+/* Keyed compare of two selection outputs of the same prefix set (the device
+ * half of DecisionRouteDb::calculateUpdate, Decision.cpp:108-143): prefix p
+ * < n_prefix whose record (status, metric, best, mask words) differs from
+ * prev's, or with p >= prev_n, is appended to d_changed as one packed record
+ * of 4 + total_words u32 {p, status, metric, best, mask...}; *d_count
+ * receives how many (d_changed must hold n_prefix records). Asynchronous on
+ * the context stream. */
+int orh_route_diff(orh_prefix_set* ps, uint32_t n_prefix, uint32_t prev_n, const orh_select_out* cur,
+                   const orh_select_out* prev, uint32_t* d_changed, uint32_t* d_count);
 /* device time of the last orh_route_select kernel (HIP events; waits for it) */
 int orh_last_select_ms(orh_prefix_set* ps, double* ms_out);
 

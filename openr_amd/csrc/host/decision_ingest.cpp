@@ -5,6 +5,7 @@
 #include <arpa/inet.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <regex>
 
 #include "thrift_compact.h"
@@ -250,9 +251,23 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
                                               RibPolicy* policy) {
   DecisionRouteUpdate update;
   if (fullRebuild) {
-    DecisionRouteDb db = solver.buildRouteDb(me, als, ps).value_or(DecisionRouteDb{});
-    if (policy) policy->applyPolicy(db.unicastRoutes);
-    update = routeDb_.calculateUpdate(std::move(db));
+    // a delta against routeDb_ when it was made from this solver's current
+    // selection snapshot, this prefix state, policy and static routes; else
+    // the reference's whole rebuild (Decision.cpp:1888-1900)
+    std::optional<DecisionRouteUpdate> delta;
+    const bool policyActive = policy && policy->isActive();
+    if (solver_ == &solver && ps_ == &ps && policy_ == policy && policyActive_ == policyActive &&
+        staticEpoch_ == solver.staticEpoch() && selGen_ != 0 && !std::getenv("ORH_WHOLE_REBUILD"))
+      delta = solver.buildRouteDelta(me, als, ps, routeDb_, selGen_, psStamp_, policy);
+    if (delta) {
+      update = std::move(*delta);
+      ++deltaRebuilds_;
+    } else {
+      DecisionRouteDb db = solver.buildRouteDb(me, als, ps).value_or(DecisionRouteDb{});
+      if (policy) policy->applyPolicy(db.unicastRoutes);
+      update = routeDb_.calculateUpdate(std::move(db));
+      ++wholeRebuilds_;
+    }
   } else {
     auto routes = solver.createRoutesForPrefixes(me, als, ps, updatedPrefixes);
     for (size_t i = 0; i < routes.size(); ++i) {
@@ -269,6 +284,13 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
     }
   }
   routeDb_.update(update);
+  solver_ = &solver;
+  ps_ = &ps;
+  selGen_ = solver.selGen();
+  psStamp_ = ps.stamp();
+  staticEpoch_ = solver.staticEpoch();
+  policy_ = policy;
+  policyActive_ = policy && policy->isActive();
   return update;
 }
 

@@ -107,9 +107,21 @@ class DecisionRib {
                                     const AreaLinkStates& als, const PrefixState& ps,
                                     DecisionPendingUpdates& pending, RibPolicy* policy);
   const DecisionRouteDb& routeDb() const { return routeDb_; }
+  // full rebuilds that ran as a delta against routeDb_ (SpfSolver::
+  // buildRouteDelta) / as a whole build (tests, A/B)
+  uint64_t deltaRebuilds() const { return deltaRebuilds_; }
+  uint64_t wholeRebuilds() const { return wholeRebuilds_; }
 
  private:
   DecisionRouteDb routeDb_;
+  // what routeDb_ was last made from: the solver and its selection snapshot,
+  // the prefix state's stamp, the policy and its state, the static routes
+  const SpfSolver* solver_{nullptr};
+  const PrefixState* ps_{nullptr};
+  uint64_t selGen_{0}, psStamp_{0}, staticEpoch_{0};
+  const RibPolicy* policy_{nullptr};
+  bool policyActive_{false};
+  uint64_t deltaRebuilds_{0}, wholeRebuilds_{0};
 };
 
 }  // namespace openr_amd

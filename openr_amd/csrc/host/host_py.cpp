@@ -1064,17 +1064,29 @@ PYBIND11_MODULE(_openr_host, m) {
       .def(py::init<>())
       .def("rebuild_routes",
            [](DecisionRib& r, SpfSolver& solver, const std::string& me, const AreaMap& als,
-              const PrefixState& ps, bool full, std::vector<py::tuple> prefixes, RibPolicy* policy) {
+              const PrefixState& ps, bool full, std::vector<py::tuple> prefixes, RibPolicy* policy,
+              bool wire) {
              std::vector<Cidr> pfx;
              pfx.reserve(prefixes.size());
              for (auto& t : prefixes) pfx.emplace_back(AddrBytes(str(t[0])), t[1].cast<int32_t>());
              const auto t0 = std::chrono::steady_clock::now();
-             auto u = r.rebuildRoutes(solver, me, als.m, ps, full, pfx, policy);
+             py::object out;
+             {
+               auto u = r.rebuildRoutes(solver, me, als.m, ps, full, pfx, policy);
+               if (wire) {
+                 out = deltaToWire(u);
+               } else {  // sizes only: (unicast updated, deleted, mpls updated, deleted)
+                 out = py::make_tuple(u.unicastRoutesToUpdate.size(), u.unicastRoutesToDelete.size(),
+                                      u.mplsRoutesToUpdate.size(), u.mplsRoutesToDelete.size());
+               }
+             }  // the delta is freed inside the timed call, as Decision's would be
              const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-             return py::make_tuple(deltaToWire(u), sec);
+             return py::make_tuple(out, sec);
            },
            py::arg("solver"), py::arg("me"), py::arg("als"), py::arg("ps"), py::arg("full"),
-           py::arg("prefixes"), py::arg("policy") = nullptr)
+           py::arg("prefixes"), py::arg("policy") = nullptr, py::arg("wire") = true)
+      .def_property_readonly("delta_rebuilds", &DecisionRib::deltaRebuilds)
+      .def_property_readonly("whole_rebuilds", &DecisionRib::wholeRebuilds)
       .def("rebuild_routes_pending",  // from a DecisionIngest's pending updates (then reset)
            [](DecisionRib& r, SpfSolver& solver, const std::string& me, const AreaMap& als,
               const PrefixState& ps, Ingest& g, RibPolicy* policy) {

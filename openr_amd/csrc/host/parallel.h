@@ -7,9 +7,7 @@
 #pragma once
 
 #include <algorithm>
-#include <atomic>
 #include <condition_variable>
-#include <deque>
 #include <cstdlib>
 #include <exception>
 #include <functional>
@@ -26,15 +24,22 @@ class WorkerPool {
     return pool;
   }
   size_t size() const { return workers_.size() + 1; }  // the caller works too
+  // true on a pool worker, and on the caller while it runs a parallelFor
+  // (a nested parallelFor would deadlock: callers check and run inline)
+  static bool busyHere() { return inJob_; }
 
   // fn(worker, begin, end) over [0, n) in size() contiguous chunks; the first
   // exception (if any) is rethrown on the caller
   void parallelFor(size_t n, const std::function<void(size_t, size_t, size_t)>& fn) {
     const size_t parts = std::min(size(), std::max<size_t>(n, 1));
-    if (parts <= 1) {
+    if (parts <= 1 || inJob_) {
       fn(0, 0, n);
       return;
     }
+    struct Mark {
+      Mark() { inJob_ = true; }
+      ~Mark() { inJob_ = false; }
+    } mark;
     std::unique_lock<std::mutex> lock(mu_);
     job_ = &fn;
     n_ = n;
@@ -87,6 +92,7 @@ class WorkerPool {
   }
 
   void loop() {
+    inJob_ = true;
     uint64_t seen = 0;
     std::unique_lock<std::mutex> lock(mu_);
     for (;;) {
@@ -111,67 +117,7 @@ class WorkerPool {
   uint64_t gen_{0};
   bool stop_{false};
   std::exception_ptr err_;
-};
-
-// Frees large containers off the caller's thread: a 1M-route DecisionRouteDb
-// is ~5M heap nodes, ~0.7 s of free() (C5), which a Decision thread holding
-// routeDb_ would otherwise pay on every full rebuild. One background thread
-// destroys what is posted, in order; at exit it drains the queue.
-class Reclaimer {
- public:
-  static Reclaimer& instance() {
-    static Reclaimer r;
-    return r;
-  }
-  // false when the reclaimer is already shut down (the caller frees inline)
-  bool post(std::function<void()> fn) {
-    std::lock_guard<std::mutex> lock(mu_);
-    if (stop_) return false;
-    q_.push_back(std::move(fn));
-    cv_.notify_one();
-    return true;
-  }
-  // waits until everything posted so far is freed (tests, memory accounting)
-  void drain() {
-    std::unique_lock<std::mutex> lock(mu_);
-    idle_.wait(lock, [&] { return q_.empty() && !busy_; });
-  }
-  // false once the reclaimer was destroyed (static destruction at exit)
-  static bool usable() { return state_.load() != 2; }
-
- private:
-  Reclaimer() : th_([this] { loop(); }) { state_ = 1; }
-  ~Reclaimer() {
-    state_ = 2;
-    {
-      std::lock_guard<std::mutex> lock(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    th_.join();
-  }
-  void loop() {
-    std::unique_lock<std::mutex> lock(mu_);
-    for (;;) {
-      cv_.wait(lock, [&] { return stop_ || !q_.empty(); });
-      if (q_.empty()) return;  // stopping, nothing left
-      auto fn = std::move(q_.front());
-      q_.pop_front();
-      busy_ = true;
-      lock.unlock();
-      fn();
-      fn = nullptr;
-      lock.lock();
-      busy_ = false;
-      if (q_.empty()) idle_.notify_all();
-    }
-  }
-  std::mutex mu_;
-  std::condition_variable cv_, idle_;
-  std::deque<std::function<void()>> q_;
-  bool stop_{false}, busy_{false};
-  static inline std::atomic<int> state_{0};  // 0 never built, 1 running, 2 destroyed
-  std::thread th_;
+  static inline thread_local bool inJob_ = false;
 };
 
 }  // namespace openr_amd

@@ -80,6 +80,7 @@ std::optional<uint32_t> PrefixState::areaId(const std::string& a) const {
 // id when its last advertisement is withdrawn) and queue it for upload
 void PrefixState::touch(const Cidr& prefix, bool erased) {
   uint32_t pid;
+  ++stamp_;
   auto it = pid_.find(prefix);
   if (it != pid_.end()) {
     pid = it->second;
@@ -87,6 +88,12 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
       pid_.erase(it);
       live_[pid] = 0;
       freePids_.push_back(pid);
+      // the prefix's id may go to another prefix: its key is logged
+      deleted_.emplace_back(stamp_, prefix);
+      if (deleted_.size() > kDeletedLog) {
+        deletedFloor_ = deleted_.front().first;
+        deleted_.pop_front();
+      }
     }
   } else {
     if (erased) return;
@@ -99,11 +106,13 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
       cidrOf_.push_back(prefix);
       live_.push_back(0);
       isDirty_.push_back(0);
+      pidStamp_.push_back(0);
       run_.emplace_back(0u, 0u);
     }
     pid_.emplace(prefix, pid);
     live_[pid] = 1;
   }
+  pidStamp_[pid] = stamp_;
   if (!isDirty_[pid]) {
     isDirty_[pid] = 1;
     dirty_.push_back(pid);

@@ -68,6 +68,7 @@ class RibPolicy {
   PolicyChange applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes);
   // decision.rib_policy.invalidated_routes (RibPolicy.cpp:150-153)
   uint64_t invalidatedRoutes() const { return invalidated_; }
+  void addInvalidated(uint64_t n) { invalidated_ += n; }
 
  private:
   std::chrono::steady_clock::time_point validUntil_;

@@ -192,6 +192,8 @@ SpfSolver::~SpfSolver() {
     if (w.dRow) orh_device_free(selCtx_, w.dRow);
   }
   if (dSel_) orh_device_free(selCtx_, dSel_);
+  if (dSelPrev_) orh_device_free(selCtx_, dSelPrev_);
+  if (dDiff_) orh_device_free(selCtx_, dDiff_);
 }
 
 void SpfSolver::updateStaticUnicastRoutes(
@@ -199,11 +201,13 @@ void SpfSolver::updateStaticUnicastRoutes(
     const std::vector<Cidr>& del) {
   for (const auto& [p, nhs] : upd) staticUnicastRoutes_[p] = nhs;
   for (const auto& p : del) staticUnicastRoutes_.erase(p);
+  ++staticEpoch_;
 }
 
 void SpfSolver::updateStaticMplsRoutes(
     const std::vector<std::pair<int32_t, std::vector<NextHopThrift>>>& upd,
     const std::vector<int32_t>& del) {
+  ++staticEpoch_;
   for (const auto& [l, nhs] : upd) staticMplsRoutes_[l] = nhs;
   for (int32_t l : del) staticMplsRoutes_.erase(l);
 }
@@ -234,6 +238,9 @@ std::vector<std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
   if (parallel || (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64))
     for (const auto& [_, ls] : als) ls.getSpfRow(me);
   if (!hasKsp && shardWorld_ == 1 && prefixes.size() >= 64) dev = selectOnDevice(me, als, ps);
+  // routes built without a selection pass no longer match the snapshot a
+  // later buildRouteDelta would compare with
+  if (!dev) havePrev_ = false;
   auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
     auto it = staticUnicastRoutes_.find(p);
     if (it == staticUnicastRoutes_.end()) return std::nullopt;
@@ -678,8 +685,13 @@ std::optional<RibUnicastEntry> SpfSolver::addBestPaths(const std::string& me, co
 // reads every area's SPF, Decision.cpp:1194-1197). Returns false (all
 // prefixes on the host path) when the inputs are outside what it covers.
 bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
-                               const PrefixState& ps) {
+                               const PrefixState& ps, bool diff) {
   deviceSelected_ = hostSelected_ = 0;
+  lastDiffed_ = false;
+  // a selection that does not complete (host path) leaves no snapshot: the
+  // routes built from it do not correspond to the previous one any more
+  const bool hadPrev = havePrev_;
+  havePrev_ = false;
   if (std::getenv("ORH_HOST_SELECT")) return false;  // A/B switch: host selection
   // below ORH_DEVICE_SELECT_MIN prefixes (default 1024) the launch and the
   // row uploads cost more than selecting on the host (C1: 100 prefixes)
@@ -799,8 +811,46 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
       w.tmpl4[k].push_back(nextHop(l.nhV4From(myId), l.ifFrom(myId), 0, std::nullopt, l.area, nbrName));
     }
   }
+  // digest of everything a materialised route depends on besides its
+  // selection record: the area layout and every nexthop template
+  uint64_t layout = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const auto* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) layout = (layout ^ b[i]) * 1099511628211ull;
+  };
+  for (const AreaWork& w : areaWork_) {
+    mix(&w.words, sizeof w.words);
+    mix(&w.wordOff, sizeof w.wordOff);
+    const void* ls = w.ls;
+    mix(&ls, sizeof ls);
+    for (const auto* tm : {&w.tmpl6, &w.tmpl4}) {
+      const uint32_t nb = static_cast<uint32_t>(tm->size());
+      mix(&nb, sizeof nb);
+      for (const auto& bit : *tm) {
+        const uint32_t c = static_cast<uint32_t>(bit.size());
+        mix(&c, sizeof c);
+        for (const auto& t : bit) {
+          mix(t.address.addr.data(), t.address.addr.size());
+          if (t.address.ifName) mix(t.address.ifName->data(), t.address.ifName->size());
+          if (t.area) mix(t.area->data(), t.area->size());
+          if (t.neighborNodeName) mix(t.neighborNodeName->data(), t.neighborNodeName->size());
+          mix("|", 1);
+        }
+      }
+    }
+  }
   // outputs: status [n] | metric [n] | best [n] | mask [n][words]
   const uint32_t n = ps.numPrefixIds();
+  auto outOf = [&](uint8_t* base, uint32_t np) {
+    const size_t n4 = (static_cast<size_t>(np) + 3) & ~static_cast<size_t>(3);
+    orh_select_out o{};
+    o.d_status = base;
+    o.d_metric = reinterpret_cast<uint32_t*>(base + n4);
+    o.d_best = o.d_metric + np;
+    o.d_mask = o.d_best + np;
+    o.total_words = words;
+    return o;
+  };
   const size_t n4 = (static_cast<size_t>(n) + 3) & ~static_cast<size_t>(3);
   const size_t bytes = n4 + 8ull * n + 4ull * n * std::max(words, 1u);
   if (bytes > dSelCap_) {
@@ -810,12 +860,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     if (orh_device_alloc(ctx, dSelCap_, reinterpret_cast<void**>(&dSel_)) != ORH_OK)
       throw std::runtime_error("route select: device allocation failed");
   }
-  orh_select_out out{};
-  out.d_status = dSel_;
-  out.d_metric = reinterpret_cast<uint32_t*>(dSel_ + n4);
-  out.d_best = out.d_metric + n;
-  out.d_mask = out.d_best + n;
-  out.total_words = words;
+  orh_select_out out = outOf(dSel_, n);
   const auto meName = ps.nameId(me);
   uint32_t flags = (enableBestRouteSelection_ ? ORH_SELECT_BEST_ROUTE : 0u) |
       (enableV4_ ? ORH_SELECT_V4 : 0u);
@@ -830,17 +875,64 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     lastSelectBytes_ = 8ull * np + 20ull * live + 4ull * live * areasWithRow +
         static_cast<uint64_t>(np) * (9 + 4ull * words);
   }
-  selStatus_.resize(n);
-  selMetric_.resize(n);
-  selBest_.resize(n);
-  selMask_.resize(static_cast<size_t>(n) * words);
+  const bool canDiff = diff && hadPrev && dSelPrev_ && prevWords_ == words && prevLayout_ == layout &&
+                       prevN_ <= n && selStatus_.size() == prevN_;
+  if (canDiff) {
+    // only the records that differ from the snapshot come back
+    const size_t rec = 4 + words;
+    const size_t need = (static_cast<size_t>(n) * rec + 1) * 4;
+    if (need > dDiffCap_) {
+      if (dDiff_) orh_device_free(ctx, dDiff_);
+      dDiff_ = nullptr;
+      dDiffCap_ = std::max(need, dDiffCap_ * 2);
+      if (orh_device_alloc(ctx, dDiffCap_, reinterpret_cast<void**>(&dDiff_)) != ORH_OK)
+        throw std::runtime_error("route diff: device allocation failed");
+    }
+    const orh_select_out prev = outOf(dSelPrev_, prevN_);
+    if (orh_route_diff(set, n, prevN_, &out, &prev, dDiff_ + 1, dDiff_) != ORH_OK)
+      throw std::runtime_error(std::string("orh_route_diff: ") + orh_last_error(ctx));
+    uint32_t k = 0;
+    if (orh_memcpy_d2h(ctx, &k, dDiff_, 4) != ORH_OK)
+      throw std::runtime_error(std::string("route diff copy-out: ") + orh_last_error(ctx));
+    std::vector<uint32_t> recs(static_cast<size_t>(k) * rec);
+    if (k && orh_memcpy_d2h(ctx, recs.data(), dDiff_ + 1, recs.size() * 4) != ORH_OK)
+      throw std::runtime_error(std::string("route diff copy-out: ") + orh_last_error(ctx));
+    selStatus_.resize(n, ORH_SEL_NONE);
+    selMetric_.resize(n, 0);
+    selBest_.resize(n, 0);
+    selMask_.resize(static_cast<size_t>(n) * words, 0);
+    changedPids_.resize(k);
+    for (uint32_t i = 0; i < k; ++i) {
+      const uint32_t* r = recs.data() + static_cast<size_t>(i) * rec;
+      const uint32_t pid = r[0];
+      changedPids_[i] = pid;
+      selStatus_[pid] = static_cast<uint8_t>(r[1]);
+      selMetric_[pid] = r[2];
+      selBest_[pid] = r[3];
+      std::copy(r + 4, r + 4 + words, selMask_.begin() + static_cast<size_t>(pid) * words);
+    }
+    lastDiffed_ = true;
+  } else {
+    selStatus_.resize(n);
+    selMetric_.resize(n);
+    selBest_.resize(n);
+    selMask_.resize(static_cast<size_t>(n) * words);
+    if (orh_memcpy_d2h(ctx, selStatus_.data(), out.d_status, n) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selMetric_.data(), out.d_metric, 4ull * n) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selBest_.data(), out.d_best, 4ull * n) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
+      throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
+  }
   selWords_ = words;
-  if (orh_memcpy_d2h(ctx, selStatus_.data(), out.d_status, n) != ORH_OK ||
-      orh_memcpy_d2h(ctx, selMetric_.data(), out.d_metric, 4ull * n) != ORH_OK ||
-      orh_memcpy_d2h(ctx, selBest_.data(), out.d_best, 4ull * n) != ORH_OK ||
-      orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
-    throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
   if (orh_last_select_ms(set, &lastSelectMs_) != ORH_OK) lastSelectMs_ = -1;
+  // this selection is the snapshot the next one is compared with
+  std::swap(dSel_, dSelPrev_);
+  std::swap(dSelCap_, dSelPrevCap_);
+  havePrev_ = shardWorld_ == 1;
+  ++selGen_;
+  prevN_ = n;
+  prevWords_ = words;
+  prevLayout_ = layout;
   return true;
 }
 
@@ -880,18 +972,24 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
                                                        const AreaLinkStates& als,
                                                        const PrefixState& ps) {
-  // Decision.cpp:615-792
+  return buildRouteDbImpl(me, als, ps, false);
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me,
+                                                           const AreaLinkStates& als,
+                                                           const PrefixState& ps, bool mplsOnly) {
+  // Decision.cpp:615-792 (mplsOnly: the MPLS routes alone, for buildRouteDelta)
   bool exists = false;
   for (const auto& [_, ls] : als) exists |= ls.hasNode(me);
   if (!exists) return std::nullopt;
-  ++routeBuildRuns_;
+  if (!mplsOnly) ++routeBuildRuns_;
 
   // KSP2 prefixes need one fresh SPF per best node (getKthPaths k = 2): plan
   // them first and run them as one device batch (the memo then serves the
   // route build with the same paths and the same spf_runs count)
   RouteProf prof;
   bool hasKsp = false;
-  if (ps.ksp2Entries() > 0) {
+  if (ps.ksp2Entries() > 0 && !mplsOnly) {
     std::unordered_map<const LinkState*, std::vector<std::pair<std::string, std::string>>> plan;
     kspPlan_ = &plan;
     try {
@@ -923,7 +1021,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   // per-prefix selection on the device; the host materialises the routes it
   // selected and runs the full reference logic for the prefixes it returns
   // as ORH_SEL_HOST (BGP, SR_MPLS / KSP2, minNexthop, self-advertised)
-  const bool dev = selectOnDevice(me, als, ps);
+  const bool dev = !mplsOnly && selectOnDevice(me, als, ps);
   prof.mark("select (device)");
   bool labelsDone = false;  // node-label routes built by the pipelined path
   std::vector<const Cidr*> keys;
@@ -1047,7 +1145,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
     } else {
       for (uint32_t pid = 0; pid < n; ++pid) one(pid, db.unicastRoutes);
     }
-  } else {
+  } else if (!mplsOnly) {
     keys.reserve(ps.prefixes().size());
     const uint32_t n = ps.numPrefixIds();
     for (const auto& [prefix, _] : ps.prefixes())
@@ -1076,7 +1174,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
       }
     }
   }
-  if (!labelsDone) {
+  if (!labelsDone && !mplsOnly) {
     for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
       if (db.unicastRoutes.count(prefix)) continue;
       if (shardWorld_ > 1) {  // the shard of its prefix id, shard 0 if PrefixState lacks it
@@ -1212,6 +1310,110 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   }
   prof.mark("adj + static mpls");
   return db;
+}
+
+std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string& me,
+                                                              const AreaLinkStates& als,
+                                                              const PrefixState& ps,
+                                                              const DecisionRouteDb& current,
+                                                              uint64_t selGen, uint64_t psStamp,
+                                                              RibPolicy* policy) {
+  if (!havePrev_ || selGen != selGen_ || shardWorld_ != 1 || ps.ksp2Entries() > 0) return std::nullopt;
+  bool exists = false;
+  for (const auto& [_, ls] : als) exists |= ls.hasNode(me);
+  if (!exists) return std::nullopt;
+  std::vector<Cidr> deleted;
+  if (!ps.forEachDeletedSince(psStamp, [&](const Cidr& c) { deleted.push_back(c); })) return std::nullopt;
+  RouteProf prof;
+  for (const auto& [_, ls] : als) ls.getSpfRow(me);
+  prof.mark("spf(me)");
+  if (!selectOnDevice(me, als, ps, true) || !lastDiffed_) return std::nullopt;  // the caller builds in full
+  prof.mark("select + diff (device)");
+  ++routeBuildRuns_;
+  const uint32_t n = ps.numPrefixIds();
+  // prefixes to rebuild: changed selection records, prefixes changed since
+  // psStamp, and the host-path prefixes (their inputs are not in the record)
+  std::vector<uint8_t> want(n, 0);
+  for (uint32_t pid : changedPids_) want[pid] = 1;
+  auto& pool = WorkerPool::instance();
+  pool.parallelFor(n, [&](size_t, size_t b, size_t e) {
+    for (size_t pid = b; pid < e; ++pid)
+      if (selStatus_[pid] == ORH_SEL_HOST || ps.pidStamp(static_cast<uint32_t>(pid)) > psStamp) want[pid] = 1;
+  });
+  std::vector<uint32_t> todo;
+  for (uint32_t pid = 0; pid < n; ++pid)
+    if (want[pid] && ps.prefixLive(pid)) todo.push_back(pid);
+  uint64_t nDev = 0, nHost = 0;
+  for (uint32_t pid : todo) (selStatus_[pid] == ORH_SEL_HOST ? nHost : nDev) += 1;
+  deviceSelected_ = nDev;
+  hostSelected_ = nHost;
+  prof.mark("candidates");
+  const bool applyPolicy = policy && policy->isActive();
+  auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
+    auto it = staticUnicastRoutes_.find(p);
+    if (it == staticUnicastRoutes_.end()) return std::nullopt;
+    RibUnicastEntry e;
+    e.prefix = p;
+    e.nexthops.insert(it->second.begin(), it->second.end());
+    return e;
+  };
+  struct Part {
+    std::vector<RibUnicastEntry> upd;
+    std::vector<Cidr> del;
+    uint64_t invalidated{0};
+  };
+  std::vector<Part> parts(pool.size());
+  // the new route of one prefix (createRouteForPrefixOrGetStaticRoute, then
+  // the policy), compared with current's entry (calculateUpdate)
+  auto one = [&](const Cidr& prefix, std::optional<RibUnicastEntry> r, Part& out) {
+    if (!r) r = staticRoute(prefix);
+    if (r && applyPolicy) policy->applyAction(*r, &out.invalidated);
+    auto it = current.unicastRoutes.find(prefix);
+    if (r) {
+      if (it == current.unicastRoutes.end() || it->second != *r) out.upd.push_back(std::move(*r));
+    } else if (it != current.unicastRoutes.end()) {
+      out.del.push_back(prefix);
+    }
+  };
+  pool.parallelFor(todo.size(), [&](size_t w, size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      const uint32_t pid = todo[i];
+      const Cidr& prefix = ps.prefixOf(pid);
+      std::optional<RibUnicastEntry> r;
+      if (selStatus_[pid] == ORH_SEL_ROUTE) r = materialize(pid, ps);
+      else if (selStatus_[pid] == ORH_SEL_HOST) r = createRouteForPrefix(me, als, ps, prefix);
+      one(prefix, std::move(r), parts[w]);
+    }
+  });
+  // withdrawn prefixes that no live id carries now: their routes go (or
+  // fall back to a static route)
+  for (const Cidr& c : deleted)
+    if (!ps.pidOf(c)) one(c, std::nullopt, parts[0]);
+  prof.mark("unicast (pool)");
+  DecisionRouteUpdate delta;
+  uint64_t invalidated = 0;
+  for (auto& p : parts) {
+    for (auto& r : p.upd) {
+      Cidr k = r.prefix;
+      if (!delta.unicastRoutesToUpdate.emplace(std::move(k), std::move(r)).second)
+        throw std::logic_error("buildRouteDelta: duplicate unicast route");  // RouteUpdate.h:39 CHECK
+    }
+    for (auto& c : p.del) delta.unicastRoutesToDelete.push_back(std::move(c));
+    invalidated += p.invalidated;
+  }
+  if (policy) policy->addInvalidated(invalidated);
+  // MPLS routes: rebuilt and compared in full (node labels: one per node)
+  auto mdb = buildRouteDbImpl(me, als, ps, true);
+  if (mdb) {
+    for (auto& [label, entry] : mdb->mplsRoutes) {
+      auto it = current.mplsRoutes.find(label);
+      if (it == current.mplsRoutes.end() || it->second != entry) delta.mplsRoutesToUpdate.push_back(std::move(entry));
+    }
+  }
+  for (const auto& [label, _] : current.mplsRoutes)
+    if (!mdb || !mdb->mplsRoutes.count(label)) delta.mplsRoutesToDelete.push_back(label);
+  prof.mark("mpls");
+  return delta;
 }
 
 }  // namespace openr_amd

@@ -10,9 +10,11 @@
 // mask OR instead of string-set unions.
 #pragma once
 
+#include <deque>
 #include <set>
 
 #include "link_state.h"
+#include "rib_policy.h"
 
 namespace openr_amd {
 
@@ -62,6 +64,20 @@ class PrefixState {
     if (it == pid_.end()) return std::nullopt;
     return it->second;
   }
+  // change stamps (an incremental rebuild's "what changed since"): every
+  // updatePrefix / deletePrefix that changes a prefix advances stamp(); a
+  // prefix id carries the stamp of its last change, and withdrawn prefixes
+  // are logged with theirs (ids are reused)
+  uint64_t stamp() const { return stamp_; }
+  uint64_t pidStamp(uint32_t pid) const { return pidStamp_[pid]; }
+  // calls f(prefix) for each prefix withdrawn after `since`; false when the
+  // log no longer reaches back that far
+  template <class F>
+  bool forEachDeletedSince(uint64_t since, F&& f) const {
+    if (since < deletedFloor_) return false;
+    for (auto it = deleted_.rbegin(); it != deleted_.rend() && it->first > since; ++it) f(it->second);
+    return true;
+  }
   std::optional<uint32_t> nameId(const std::string& n) const;
   uint32_t numNames() const { return static_cast<uint32_t>(names_.size()); }
   const std::string& name(uint32_t id) const { return names_[id]; }
@@ -83,6 +99,11 @@ class PrefixState {
   std::vector<uint8_t> live_;
   std::vector<uint32_t> freePids_;
   std::vector<uint32_t> dirty_;
+  uint64_t stamp_{0};
+  std::vector<uint64_t> pidStamp_;
+  static constexpr size_t kDeletedLog = 1u << 20;
+  std::deque<std::pair<uint64_t, Cidr>> deleted_;
+  uint64_t deletedFloor_{0};
   std::vector<uint8_t> isDirty_;
   std::unordered_map<std::string, uint32_t> nameIds_, areaIds_;
   std::vector<std::string> names_, areas_;
@@ -138,6 +159,24 @@ class SpfSolver {
       const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
       const std::vector<Cidr>& prefixes);
 
+  // Decision::rebuildRoutes' full rebuild (Decision.cpp:1888-1900:
+  // buildRouteDb, RibPolicy, calculateUpdate) as a delta against `current`,
+  // the route DB built from this solver's selection snapshot `selGen` with
+  // the prefix state at `psStamp` and the same policy: the device selection
+  // runs for every prefix and is compared on the device with the snapshot
+  // (orh_route_diff); only prefixes whose selection record changed, prefixes
+  // changed since psStamp, and host-path prefixes get a route built, the
+  // policy applied and compared with current's entry. MPLS routes are rebuilt
+  // and compared in full. nullopt when a delta cannot stand for the full
+  // rebuild (no snapshot, KSP2, prefix shards, my nexthop templates changed,
+  // ...): the caller rebuilds in full. The update equals calculateUpdate's.
+  std::optional<DecisionRouteUpdate> buildRouteDelta(const std::string& me, const AreaLinkStates& als,
+                                                     const PrefixState& ps, const DecisionRouteDb& current,
+                                                     uint64_t selGen, uint64_t psStamp, RibPolicy* policy);
+  // the selection snapshot of the last device selection (0: none), and the
+  // static routes' version
+  uint64_t selGen() const { return havePrev_ ? selGen_ : 0; }
+  uint64_t staticEpoch() const { return staticEpoch_; }
   uint64_t routeBuildRuns() const { return routeBuildRuns_; }
   // prefixes of the last buildRouteDb whose selection ran on the device /
   // took the host path (BGP, SR_MPLS, KSP2, minNexthop, self-advertised)
@@ -196,7 +235,13 @@ class SpfSolver {
 
   // device route selection over the PrefixState mirror; false when the
   // inputs need the host path for every prefix
-  bool selectOnDevice(const std::string& me, const AreaLinkStates& als, const PrefixState& ps);
+  // diff = true: compare with the previous snapshot on the device and copy
+  // back only the changed records (changedPids_; lastDiffed_ says whether
+  // the compare could run)
+  bool selectOnDevice(const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+                      bool diff = false);
+  std::optional<DecisionRouteDb> buildRouteDbImpl(const std::string& me, const AreaLinkStates& als,
+                                                  const PrefixState& ps, bool mplsOnly);
   RibUnicastEntry materialize(uint32_t pid, const PrefixState& ps) const;
 
   // device selection workspace (per solver)
@@ -217,6 +262,16 @@ class SpfSolver {
   orh_ctx* selCtx_{nullptr};
   uint8_t* dSel_{nullptr};  // status | metric | best | mask
   size_t dSelCap_{0};
+  // the previous selection (snapshot selGen_, prevN_ prefixes, layout digest
+  // of the nexthop templates it was made with) and the diff output
+  uint8_t* dSelPrev_{nullptr};
+  size_t dSelPrevCap_{0};
+  uint32_t* dDiff_{nullptr};
+  size_t dDiffCap_{0};
+  bool havePrev_{false}, lastDiffed_{false};
+  uint64_t selGen_{0}, prevLayout_{0}, staticEpoch_{0};
+  uint32_t prevN_{0}, prevWords_{0};
+  std::vector<uint32_t> changedPids_;
   std::vector<uint8_t> selStatus_;
   std::vector<uint32_t> selMetric_, selBest_, selMask_;
   uint32_t selWords_{0};

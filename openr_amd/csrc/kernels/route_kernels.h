@@ -41,6 +41,22 @@ struct RouteSelectArgs {
 
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s);
 
+// keyed compare of two selection outputs (route_diff_kernel)
+struct RouteDiffArgs {
+  uint32_t n_prefix, prev_n, words;
+  const uint8_t* status;
+  const uint32_t* metric;
+  const uint32_t* best;
+  const uint32_t* mask;
+  const uint8_t* p_status;
+  const uint32_t* p_metric;
+  const uint32_t* p_best;
+  const uint32_t* p_mask;
+  uint32_t* out;    // packed records {p, status, metric, best, mask[words]}
+  uint32_t* count;  // zeroed before the launch
+};
+hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s);
+
 // hdr[ids[i]] = vals[i]
 hipError_t launch_scatter_hdr(uint2* hdr, const uint32_t* ids, const uint2* vals, uint32_t n,
                               hipStream_t s);

@@ -216,6 +216,51 @@ __global__ __launch_bounds__(kSelBlock) void scatter_hdr_kernel(uint2* hdr, cons
   if (i < n) hdr[ids[i]] = vals[i];
 }
 
+// The device half of DecisionRouteDb::calculateUpdate (Decision.cpp:108-143)
+// for a rebuild after topology changes: a route is a function of its
+// selection record (status, shortest metric, best advertisement, first-hop
+// mask) once the nexthop templates, the prefix entries and the policy are
+// unchanged, so only prefixes whose record differs from the previous build's
+// need a route built and compared on the host. One thread per prefix; the
+// changed records are appended packed (one atomic per wave).
+__global__ __launch_bounds__(kSelBlock) void route_diff_kernel(RouteDiffArgs a) {
+  const uint32_t p = blockIdx.x * kSelBlock + threadIdx.x;
+  bool diff = false;
+  if (p < a.n_prefix) {
+    if (p >= a.prev_n) {
+      diff = true;
+    } else {
+      diff = a.status[p] != a.p_status[p];
+      if (!diff && a.status[p] == ORH_SEL_ROUTE) {
+        diff = a.metric[p] != a.p_metric[p] || a.best[p] != a.p_best[p];
+        for (uint32_t k = 0; k < a.words && !diff; ++k)
+          diff = a.mask[static_cast<size_t>(p) * a.words + k] != a.p_mask[static_cast<size_t>(p) * a.words + k];
+      }
+    }
+  }
+  const unsigned long long m = __ballot(diff);
+  if (!m) return;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(m));
+  uint32_t at = 0;
+  if (lane == leader) at = atomicAdd(a.count, static_cast<uint32_t>(__popcll(m)));
+  at = __shfl(at, static_cast<int>(leader));
+  if (!diff) return;
+  const size_t rec = 4 + a.words;
+  uint32_t* o = a.out + (at + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)))) * rec;
+  o[0] = p;
+  o[1] = a.status[p];
+  o[2] = a.metric[p];
+  o[3] = a.best[p];
+  for (uint32_t k = 0; k < a.words; ++k) o[4 + k] = a.mask[static_cast<size_t>(p) * a.words + k];
+}
+
+hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s) {
+  if (a.n_prefix == 0) return hipSuccess;
+  hipLaunchKernelGGL(route_diff_kernel, dim3((a.n_prefix + kSelBlock - 1) / kSelBlock), dim3(kSelBlock), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s) {
   if (a.n_prefix == 0) return hipSuccess;
   const uint32_t grid = (a.n_prefix + kSelBlock - 1) / kSelBlock;

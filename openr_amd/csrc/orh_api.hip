@@ -2692,6 +2692,36 @@ int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint3
   return ORH_OK;
 }
 
+int orh_route_diff(orh_prefix_set* ps, uint32_t n_prefix, uint32_t prev_n, const orh_select_out* cur,
+                   const orh_select_out* prev, uint32_t* d_changed, uint32_t* d_count) {
+  if (!ps || !cur || !prev || !d_changed || !d_count) return ORH_E_INVALID;
+  orh_ctx* ctx = ps->ctx;
+  if (cur->total_words != prev->total_words)
+    return fail(ctx, ORH_E_INVALID, "orh_route_diff: different mask widths");
+  if (!cur->d_status || !cur->d_metric || !cur->d_best || !prev->d_status || !prev->d_metric || !prev->d_best ||
+      (cur->total_words && (!cur->d_mask || !prev->d_mask)))
+    return fail(ctx, ORH_E_INVALID, "orh_route_diff: null selection output");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  ORH_HIP(ctx, hipMemsetAsync(d_count, 0, sizeof(uint32_t), ctx->stream));
+  orh::RouteDiffArgs a{};
+  a.n_prefix = n_prefix;
+  a.prev_n = std::min(prev_n, n_prefix);
+  a.words = cur->total_words;
+  a.status = cur->d_status;
+  a.metric = cur->d_metric;
+  a.best = cur->d_best;
+  a.mask = cur->d_mask;
+  a.p_status = prev->d_status;
+  a.p_metric = prev->d_metric;
+  a.p_best = prev->d_best;
+  a.p_mask = prev->d_mask;
+  a.out = d_changed;
+  a.count = d_count;
+  hipError_t e = orh::launch_route_diff(a, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "route_diff launch");
+  return ORH_OK;
+}
+
 int orh_last_select_ms(orh_prefix_set* ps, double* ms_out) {
   if (!ps || !ms_out) return ORH_E_INVALID;
   if (!ps->ev1) return fail(ps->ctx, ORH_E_STATE, "orh_last_select_ms: no route_select yet");

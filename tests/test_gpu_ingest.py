@@ -349,3 +349,83 @@ def test_hostile_publication_values_counted_as_errors(hip, oracle):
     als_o, ps_o = load_topology(oracle, dbs, [(node, AREA, good)])
     for me in sorted(db.thisNodeName for db in dbs)[:4]:
         assert _routes(hip, als_h._impl, ps_h._impl, me) == _routes(oracle, als_o._impl, ps_o._impl, me), me
+
+
+@pytest.mark.parametrize("with_policy", [False, True])
+def test_full_rebuild_delta(hip, oracle, with_policy):
+    """Full rebuilds after topology changes (adjacency metric changes, a link
+    drained, a node's database deleted and restored) together with prefix
+    changes, run as deltas against the DecisionRib's database
+    (SpfSolver::buildRouteDelta: device selection compared on the device
+    with the previous snapshot, orh_route_diff). After every rebuild the
+    database equals a whole build of the same state on the oracle (with the
+    policy: a whole rebuild of the product with that policy), and the
+    returned update equals calculateUpdate(previous, rebuilt)
+    (Decision.cpp:108-143)."""
+    from openr_amd.rib_policy import RibPolicy, RibPolicyStatement, RibRouteActionWeight
+    from openr_amd.types import RouteDbDelta
+    mod = hip.module
+    dbs = random_topology(6300, n=30, extra=50, max_metric=7)
+    rng = random.Random(63)
+    pfx = []
+    for i in range(400):
+        for db in rng.sample(dbs, rng.randint(1, 3)):
+            e = create_prefix_entry(IpPrefix.of(f"fd02:{i:x}::/64"))
+            e.tags = ("t",) if i % 3 else ()
+            pfx.append((db.thisNodeName, A_DEF, e))
+    als_h, ps_h = load_topology(hip, dbs, pfx)
+    als_o, ps_o = load_topology(oracle, dbs, pfx)
+    me = sorted(db.thisNodeName for db in dbs)[5]
+    solver = hip.spf_solver(me, True)._impl
+    policy = (RibPolicy([RibPolicyStatement("w", None, ["t"], RibRouteActionWeight(1, {A_DEF: 3}, {}))],
+                        3600) if with_policy else None)
+    pol = policy._impl if policy else None
+    rib = mod.DecisionRib()
+    rib.rebuild_routes(solver, me, als_h._impl, ps_h._impl, True, [], pol)
+    assert rib.whole_rebuilds == 1
+    by_name = {db.thisNodeName: db for db in dbs}
+    # topology changes away from me: my nexthop templates (my tight links)
+    # stay, so the rebuilds can run as deltas (a template change is a whole
+    # rebuild by design)
+    near = {me} | {a.otherNodeName for a in by_name[me].adjacencies}
+    far = sorted(n for n in by_name if n not in near)
+    for rnd in range(6):
+        before = rib.route_db()
+        changed = set()
+        for _ in range(rng.randint(1, 4)):  # topology
+            db = by_name[rng.choice(far)]
+            r = rng.random()
+            if r < 0.6 and db.adjacencies:
+                db.adjacencies[rng.randrange(len(db.adjacencies))].metric = rng.randint(1, 7)
+                for als in (als_h, als_o):
+                    als[A_DEF].update_adjacency_database(db)
+            elif r < 0.8 and db.adjacencies:
+                a = db.adjacencies[rng.randrange(len(db.adjacencies))]
+                a.isOverloaded = not a.isOverloaded
+                for als in (als_h, als_o):
+                    als[A_DEF].update_adjacency_database(db)
+            else:
+                for als in (als_h, als_o):
+                    als[A_DEF].delete_adjacency_database(db.thisNodeName)
+                    als[A_DEF].update_adjacency_database(db)
+        for _ in range(rng.randint(0, 20)):  # prefixes
+            node, area, e = pfx[rng.randrange(len(pfx))]
+            if rng.random() < 0.3:
+                for ps in (ps_h, ps_o):
+                    changed |= {(p.prefixAddress.addr, p.prefixLength) for p in ps.delete_prefix(node, area, e.prefix)}
+            else:
+                e2 = create_prefix_entry(e.prefix)
+                e2.metrics = PrefixMetrics(1, rng.randint(0, 2), rng.randint(0, 2), rng.randint(0, 2))
+                e2.tags = e.tags
+                for ps in (ps_h, ps_o):
+                    changed |= {(p.prefixAddress.addr, p.prefixLength) for p in ps.update_prefix(node, area, e2)}
+        delta, _ = rib.rebuild_routes(solver, me, als_h._impl, ps_h._impl, True, sorted(changed), pol)
+        after = rib.route_db()
+        if policy is None:
+            assert RouteDb.from_wire(after).canonical() == _routes(oracle, als_o._impl, ps_o._impl, me), rnd
+        fresh = mod.DecisionRib()
+        fresh.rebuild_routes(hip.spf_solver(me, True)._impl, me, als_h._impl, ps_h._impl, True, [], pol)
+        assert RouteDb.from_wire(after).canonical_full() == RouteDb.from_wire(fresh.route_db()).canonical_full()
+        want = RouteDbDelta.from_wire(mod.calculate_update(before, after)).canonical()
+        assert RouteDbDelta.from_wire(delta).canonical() == want, rnd
+    assert rib.delta_rebuilds >= 4 and rib.delta_rebuilds + rib.whole_rebuilds == 7
