@@ -113,7 +113,8 @@ def leg_c4(hip, cpu, reps=3, chunk=None):
     KSP2 (src, dst) pairs."""
     from openr_amd.facade import load_topology
     from openr_amd.types import K_TESTING_AREA as A
-    from openr_amd.workloads import C4_KSP2_PAIRS, C4_WHATIF_CHUNK, c4_ksp2_pairs, c4_wan, c4_what_if_job
+    from openr_amd.workloads import (C4_KSP2_PAIRS, C4_SEED, C4_WHATIF_CHUNK, c4_ksp2_pairs, c4_wan,
+                                     c4_what_if_job)
     adj, _ = c4_wan()
     als, _ = load_topology(hip, adj, [])
     ls = als[A]._impl
@@ -141,7 +142,7 @@ def leg_c4(hip, cpu, reps=3, chunk=None):
     tiers = {int(t): int((info & 7 == t).sum()) for t in range(5)}
     aff = info >> 3
     kp = c4_ksp2_pairs(names, C4_KSP2_PAIRS)
-    ls.prefetch_kth_paths(kp[:64])  # warm the mirror / pools
+    ls.prefetch_kth_paths(c4_ksp2_pairs(names, 64, seed=C4_SEED + 99))  # warm-up pairs (not memoized for kp)
     t0 = time.perf_counter()
     ls.prefetch_kth_paths(kp)
     kdt = time.perf_counter() - t0
@@ -155,11 +156,14 @@ def leg_c4(hip, cpu, reps=3, chunk=None):
            "what_if_tiers": {"source_row": tiers[0], "lds_small": tiers[1], "lds_large": tiers[2],
                              "global_slot": tiers[3], "full_search": tiers[4]},
            "what_if_affected_nodes": {"mean": round(float(aff.mean()), 2), "max": int(aff.max())},
-           "what_if_roofline": {"bound": "hbm", "bytes_per_spf": b_spf,
-                                "achieved_gbs": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9, 1),
-                                "frac": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9 / 8000.0, 4),
-                                "output_floor": {"bytes": out_bytes,
-                                                 "frac": round(out_bytes / (dev_ms * 1e-3) / 1e9 / 8000.0, 4)}},
+           # the rows are the floor: 8 B/node/request must reach HBM whatever
+           # the plan; B_spf per request credits work the
+           # repair plan skips, so it is reported as an equivalent only
+           "what_if_roofline": {"bound": "hbm", "bytes": out_bytes,
+                                "achieved_gbs": round(out_bytes / (dev_ms * 1e-3) / 1e9, 1),
+                                "frac": round(out_bytes / (dev_ms * 1e-3) / 1e9 / 8000.0, 4),
+                                "b_spf_equivalent": {"bytes_per_spf": b_spf,
+                                                     "gbs": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9, 1)}},
            "ksp2_pairs_per_s": round(len(kp) / kdt, 1),
            "ksp2_batch": f"{len(kp)} (src, dst) getKthPaths k=1,2 (prefetchKthPaths)"}
     if cpu:

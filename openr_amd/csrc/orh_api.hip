@@ -2313,8 +2313,10 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
   if (rc) return rc;
   const uint64_t bound = g->sum_max_metric / 2 + g->max_metric;
   const bool uniform = g->min_out == g->max_out;
-  for (uint32_t c0 = 0; c0 < n_pairs; c0 += kKspChunk) {
-    const uint32_t P = std::min(kKspChunk, n_pairs - c0);
+  uint32_t chunk = kKspChunk;  // ORH_KSP_CHUNK: pairs per device pass (A/B)
+  if (const char* e = getenv("ORH_KSP_CHUNK")) chunk = std::max(1, atoi(e));
+  for (uint32_t c0 = 0; c0 < n_pairs; c0 += chunk) {
+    const uint32_t P = std::min(chunk, n_pairs - c0);
     // distinct sources of the chunk, and each pair's row among them
     std::vector<uint32_t> srcs, row1(P), rowp(P);
     auto& ro = g->row_of;
