@@ -1361,13 +1361,28 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     std::vector<RibUnicastEntry> upd;
     std::vector<Cidr> del;
     uint64_t invalidated{0};
+    double tBuild{0}, tPolicy{0}, tCompare{0};  // ORH_ROUTE_PROF
+    size_t n{0};
   };
+  using Clock = std::chrono::steady_clock;
+  auto since = [](Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); };
   std::vector<Part> parts(pool.size());
   // the new route of one prefix (createRouteForPrefixOrGetStaticRoute, then
   // the policy), compared with current's entry (calculateUpdate)
   auto one = [&](const Cidr& prefix, std::optional<RibUnicastEntry> r, Part& out) {
     if (!r) r = staticRoute(prefix);
+    const auto t1 = prof.on ? Clock::now() : Clock::time_point{};
     if (r && applyPolicy) policy->applyAction(*r, &out.invalidated);
+    const auto t2 = prof.on ? Clock::now() : Clock::time_point{};
+    if (prof.on) out.tPolicy += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    struct CmpTimer {
+      bool on;
+      Clock::time_point t;
+      double* acc;
+      ~CmpTimer() {
+        if (on) *acc += std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+      }
+    } cmpTimer{prof.on, t2, &out.tCompare};
     auto it = current.unicastRoutes.find(prefix);
     if (r) {
       if (it == current.unicastRoutes.end() || it->second != *r) out.upd.push_back(std::move(*r));
@@ -1379,9 +1394,14 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     for (size_t i = b; i < e; ++i) {
       const uint32_t pid = todo[i];
       const Cidr& prefix = ps.prefixOf(pid);
+      const auto t0 = prof.on ? Clock::now() : Clock::time_point{};
       std::optional<RibUnicastEntry> r;
       if (selStatus_[pid] == ORH_SEL_ROUTE) r = materialize(pid, ps);
       else if (selStatus_[pid] == ORH_SEL_HOST) r = createRouteForPrefix(me, als, ps, prefix);
+      if (prof.on) {
+        parts[w].tBuild += since(t0);
+        ++parts[w].n;
+      }
       one(prefix, std::move(r), parts[w]);
     }
   });
@@ -1389,6 +1409,19 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
   // fall back to a static route)
   for (const Cidr& c : deleted)
     if (!ps.pidOf(c)) one(c, std::nullopt, parts[0]);
+  if (prof.on) {
+    double b = 0, pl = 0, c = 0;
+    size_t nn = 0, busy = 0;
+    for (const auto& p : parts) {
+      b += p.tBuild;
+      pl += p.tPolicy;
+      c += p.tCompare;
+      nn += p.n;
+      busy += p.n > 0;
+    }
+    std::fprintf(stderr, "route-prof delta: %zu routes on %zu workers; thread-ms build %.3f policy %.3f compare %.3f\n",
+                 nn, busy, b, pl, c);
+  }
   prof.mark("unicast (pool)");
   DecisionRouteUpdate delta;
   uint64_t invalidated = 0;

@@ -1934,7 +1934,12 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
     // N + 1 entries (the last is the always-zero target of dead slots)
     // 12 waves per workgroup beat 8 and 16 on the 10k grid (one workgroup
     // per CU; per-level latency is what the search time is made of)
-    const uint32_t block = n_nodes <= 4096 ? 256 : 768;
+    uint32_t block = n_nodes <= 4096 ? 256 : 768;
+    // ORH_MS_BLOCK (A/B): threads per multi-source workgroup (multiple of 64)
+    if (const char* e = getenv("ORH_MS_BLOCK")) {
+      const int b = atoi(e);
+      if (b >= 64 && b <= 1024 && b % 64 == 0) block = static_cast<uint32_t>(b);
+    }
     const uint32_t j = (n_nodes + block - 1) / block;
     const uint32_t pitch = (n_nodes + 1 + 15) & ~15u;
     if (j <= 32) {
