@@ -262,10 +262,14 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
     if (delta) {
       update = std::move(*delta);
       ++deltaRebuilds_;
+      routeDb_.update(update);
     } else {
       DecisionRouteDb db = solver.buildRouteDb(me, als, ps).value_or(DecisionRouteDb{});
       if (policy) policy->applyPolicy(db.unicastRoutes);
-      update = routeDb_.calculateUpdate(std::move(db));
+      update = routeDb_.calculateUpdate(db);
+      // routeDb_.update(update) leaves routeDb_ equal to db: take db itself
+      // (no second copy of every changed route; the old maps free in parallel)
+      routeDb_ = std::move(db);
       ++wholeRebuilds_;
     }
   } else {
@@ -282,8 +286,8 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
       for (const auto& p : policy->applyPolicy(update.unicastRoutesToUpdate).deletedRoutes)
         update.unicastRoutesToDelete.push_back(p);
     }
+    routeDb_.update(update);
   }
-  routeDb_.update(update);
   solver_ = &solver;
   ps_ = &ps;
   selGen_ = solver.selGen();

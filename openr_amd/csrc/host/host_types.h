@@ -357,7 +357,7 @@ using MplsRouteMap = ShardedMap<int32_t, RibMplsEntry>;
 // DecisionRouteUpdate (openr/decision/RouteUpdate.h:23-41): the delta Decision
 // publishes to Fib / PrefixManager after a rebuild
 struct DecisionRouteUpdate {
-  std::unordered_map<Cidr, RibUnicastEntry, CidrHash> unicastRoutesToUpdate;
+  UnicastRouteMap unicastRoutesToUpdate;  // sharded like DecisionRouteDb's map
   std::vector<Cidr> unicastRoutesToDelete;
   std::vector<RibMplsEntry> mplsRoutesToUpdate;
   std::vector<int32_t> mplsRoutesToDelete;
@@ -368,19 +368,34 @@ struct DecisionRouteDb {
   MplsRouteMap mplsRoutes;
 
   // calculateUpdate (openr/decision/Decision.cpp:108-143): new or changed
-  // entries of newDb are updates; keys of this db missing from newDb are
-  // deletes. Lists follow newDb's / this db's iteration order, as there.
-  DecisionRouteUpdate calculateUpdate(DecisionRouteDb&& newDb) const {
+  // entries of newDb are updates (copied: the caller may keep newDb as the
+  // next state); keys of this db missing from newDb are deletes. Lists follow
+  // newDb's / this db's iteration order, as there. Shard s of every map holds
+  // the same keys, so large maps are compared shard by shard on the pool.
+  DecisionRouteUpdate calculateUpdate(const DecisionRouteDb& newDb) const {
     DecisionRouteUpdate delta;
-    for (auto& [prefix, entry] : newDb.unicastRoutes) {
-      auto it = unicastRoutes.find(prefix);
-      if (it == unicastRoutes.end() || it->second != entry) {
-        if (!delta.unicastRoutesToUpdate.emplace(prefix, std::move(entry)).second)
-          throw std::logic_error("calculateUpdate: duplicate unicast route");  // RouteUpdate.h:39 CHECK
+    constexpr size_t kS = UnicastRouteMap::kShards;
+    std::vector<std::vector<Cidr>> del(kS);
+    auto shard = [&](size_t s) {
+      const auto& mine = unicastRoutes.shard(s);
+      const auto& theirs = newDb.unicastRoutes.shard(s);
+      auto& out = delta.unicastRoutesToUpdate.shard(s);
+      for (const auto& [prefix, entry] : theirs) {
+        auto it = mine.find(prefix);
+        if (it == mine.end() || it->second != entry) out.emplace(prefix, entry);
       }
+      for (const auto& [prefix, _] : mine)
+        if (!theirs.count(prefix)) del[s].push_back(prefix);
+    };
+    auto& pool = WorkerPool::instance();
+    if (newDb.unicastRoutes.size() + unicastRoutes.size() >= 8192 && pool.size() > 1) {
+      pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
+        for (size_t s = b; s < e; ++s) shard(s);
+      });
+    } else {
+      for (size_t s = 0; s < kS; ++s) shard(s);
     }
-    for (const auto& [prefix, _] : unicastRoutes)
-      if (!newDb.unicastRoutes.count(prefix)) delta.unicastRoutesToDelete.push_back(prefix);
+    for (auto& d : del) delta.unicastRoutesToDelete.insert(delta.unicastRoutesToDelete.end(), d.begin(), d.end());
     for (const auto& [label, entry] : newDb.mplsRoutes) {
       auto it = mplsRoutes.find(label);
       if (it == mplsRoutes.end() || it->second != entry) delta.mplsRoutesToUpdate.push_back(entry);

@@ -6,6 +6,7 @@
 #include <set>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -119,8 +120,13 @@ bool Link::less(const Link& o) const {
 }
 
 // ---- construction -------------------------------------------------------
+uint64_t LinkState::nextStamp() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1, std::memory_order_relaxed);
+}
+
 LinkState::LinkState(const std::string& area, orh_ctx* ctx)
-    : area_(area), ctx_(ctx ? ctx : defaultContext()) {
+    : area_(area), stamp_(nextStamp()), ctx_(ctx ? ctx : defaultContext()) {
   check(ctx_, orh_graph_create(ctx_, &graph_), "orh_graph_create");
 }
 
@@ -287,6 +293,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, 
                                                    Metric down) {
   // LinkState.cpp:564-719
   LinkStateChange change;
+  stamp_ = nextStamp();
   const std::string& node = db.thisNodeName;
   const uint32_t v = ensureNode(node);
   AdjacencyDatabase prior = std::move(adjacencyDatabases_[node]);
@@ -358,6 +365,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, 
 
 LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
   LinkStateChange c;  // LinkState.cpp:721-738
+  stamp_ = nextStamp();
   auto it = adjacencyDatabases_.find(node);
   if (it == adjacencyDatabases_.end()) return c;
   removeNode(*nodeId(node));
@@ -369,6 +377,7 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
 
 LinkStateChange LinkState::decrementHolds() {  // LinkState.cpp:500-514
   LinkStateChange c;
+  stamp_ = nextStamp();
   for (uint32_t id = 0; id < links_.size(); ++id) {
     Link& l = links_[id];
     if (!l.alive) continue;

@@ -263,6 +263,9 @@ class LinkState {
   static bool pathAInPathB(const LinkPath& a, const LinkPath& b);
 
   bool hasNode(const std::string& n) const { return adjacencyDatabases_.count(n) != 0; }
+  // unique across LinkState instances and renewed by every mutator: equal
+  // stamps mean the same object in the same state
+  uint64_t stateStamp() const { return stamp_; }
   bool isNodeOverloaded(const std::string& n) const;
   std::optional<uint32_t> nodeId(const std::string& n) const;
   const std::string& nodeName(uint32_t id) const { return names_[id]; }
@@ -315,6 +318,8 @@ class LinkState {
                                    const std::unordered_set<uint32_t>* ignore) const;
 
   std::string area_;
+  uint64_t stamp_;
+  static uint64_t nextStamp();
   orh_ctx* ctx_;
   mutable orh_graph* graph_{nullptr};
 

@@ -1,9 +1,13 @@
 // PrefixState (openr/decision/PrefixState.cpp:17-56) and its device mirror
 // (orh_prefix_set): see spf_solver.h.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <stdexcept>
 
+#include "parallel.h"
 #include "spf_solver.h"
 
 namespace openr_amd {
@@ -119,6 +123,17 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
   }
 }
 
+// the device record of one advertisement
+orh_adv PrefixState::advRecord(const NodeAndArea& na, const PrefixEntry& e) const {
+  uint32_t meta = areaIds_.at(na.second) & ORH_ADV_AREA_MASK;
+  if (e.forwardingType == kFwdSrMpls) meta |= ORH_ADV_SR_MPLS;
+  if (e.forwardingAlgorithm == kAlgoKsp2EdEcmp) meta |= ORH_ADV_KSP2;
+  if (e.type == kPrefixTypeBgp) meta |= ORH_ADV_BGP;
+  if (e.minNexthop) meta |= ORH_ADV_MIN_NEXTHOP;
+  if (e.prependLabel) meta |= ORH_ADV_PREPEND;
+  return orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference, e.distance};
+}
+
 // pid's advertisements appended to the host pool (the numbering the device
 // reports best positions in) and as device records
 void PrefixState::buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const {
@@ -131,14 +146,7 @@ void PrefixState::buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* fla
   *flags = it->first.first.size() == 4 ? ORH_PFX_V4 : 0;
   for (const auto& [na, e] : it->second) {
     advPool_.push_back(AdvRef{&na, &e});
-    uint32_t meta = areaIds_.at(na.second) & ORH_ADV_AREA_MASK;
-    if (e.forwardingType == kFwdSrMpls) meta |= ORH_ADV_SR_MPLS;
-    if (e.forwardingAlgorithm == kAlgoKsp2EdEcmp) meta |= ORH_ADV_KSP2;
-    if (e.type == kPrefixTypeBgp) meta |= ORH_ADV_BGP;
-    if (e.minNexthop) meta |= ORH_ADV_MIN_NEXTHOP;
-    if (e.prependLabel) meta |= ORH_ADV_PREPEND;
-    out.push_back(orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference,
-                          e.distance});
+    out.push_back(advRecord(na, e));
   }
   run_[pid].second = static_cast<uint32_t>(advPool_.size()) - run_[pid].first;
   advLive_ += run_[pid].second;
@@ -161,23 +169,50 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
   // host pool mostly garbage: renumber every prefix (device reloaded too)
   if (advPool_.size() > 4096 && advPool_.size() > 2 * advLive_) devFull_ = true;
   if (devFull_) {
-    advPool_.clear();
-    advLive_ = 0;
-    std::vector<orh_adv> recs;
-    std::vector<uint32_t> ptr(cidrOf_.size() + 1, 0);
-    std::vector<uint8_t> fl(cidrOf_.size(), 0);
-    recs.reserve(prefixes_.size() + prefixes_.size() / 8);
-    advPool_.reserve(recs.capacity());
-    for (uint32_t pid = 0; pid < cidrOf_.size(); ++pid) {
-      run_[pid] = {0u, 0u};
-      buildRun(pid, recs, &fl[pid]);
-      ptr[pid + 1] = static_cast<uint32_t>(recs.size());
-    }
+    // every prefix's run, in pid order: counts, offsets, then the records,
+    // each pass on the worker pool for large states (C5: 1M prefixes)
+    const uint32_t n = static_cast<uint32_t>(cidrOf_.size());
+    std::vector<const PrefixEntries*> ents(n, nullptr);
+    std::vector<uint32_t> ptr(n + 1, 0);
+    std::vector<uint8_t> fl(n, 0);
+    auto& pool = WorkerPool::instance();
+    auto each = [&](auto&& fn) {
+      if (n >= 16384 && pool.size() > 1) {
+        pool.parallelFor(n, [&](size_t, size_t b, size_t e) {
+          for (size_t pid = b; pid < e; ++pid) fn(static_cast<uint32_t>(pid));
+        });
+      } else {
+        for (uint32_t pid = 0; pid < n; ++pid) fn(pid);
+      }
+    };
+    each([&](uint32_t pid) {
+      if (!live_[pid]) return;
+      auto it = prefixes_.find(cidrOf_[pid]);
+      if (it == prefixes_.end()) return;
+      ents[pid] = &it->second;
+      ptr[pid + 1] = static_cast<uint32_t>(it->second.size());
+      fl[pid] = it->first.first.size() == 4 ? ORH_PFX_V4 : 0;
+    });
+    for (uint32_t pid = 0; pid < n; ++pid) ptr[pid + 1] += ptr[pid];
+    std::vector<orh_adv> recs(ptr[n]);
+    advPool_.assign(ptr[n], AdvRef{});
+    advLive_ = ptr[n];
+    each([&](uint32_t pid) {
+      run_[pid] = {ptr[pid], ptr[pid + 1] - ptr[pid]};
+      if (!ents[pid]) return;
+      uint32_t k = ptr[pid];
+      for (const auto& [na, e] : *ents[pid]) {
+        advPool_[k] = AdvRef{&na, &e};
+        recs[k] = advRecord(na, e);
+        ++k;
+      }
+    });
     check(ctx, orh_prefix_load(dev_, static_cast<uint32_t>(cidrOf_.size()), ptr.data(), recs.data(),
                                fl.data()),
           "orh_prefix_load");
     devFull_ = false;
   } else if (!dirty_.empty()) {
+    const auto t0 = std::chrono::steady_clock::now();
     std::vector<orh_adv> recs;
     std::vector<uint32_t> ptr(1, 0);
     std::vector<uint8_t> fl(dirty_.size(), 0);
@@ -185,9 +220,16 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
       buildRun(dirty_[i], recs, &fl[i]);
       ptr.push_back(static_cast<uint32_t>(recs.size()));
     }
+    const auto t1 = std::chrono::steady_clock::now();
     check(ctx, orh_prefix_apply_delta(dev_, static_cast<uint32_t>(dirty_.size()), dirty_.data(),
                                       ptr.data(), recs.data(), fl.data()),
           "orh_prefix_apply_delta");
+    if (std::getenv("ORH_ROUTE_PROF")) {  // phase times (see spf_solver.cpp)
+      const auto t2 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "route-prof   sync: %zu dirty prefixes, runs %.3f ms, device delta %.3f ms\n", dirty_.size(),
+                   std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                   std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
   }
   for (uint32_t pid : dirty_) self.isDirty_[pid] = 0;
   self.dirty_.clear();

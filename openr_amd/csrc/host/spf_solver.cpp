@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <ctime>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -728,7 +729,9 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     if (!ps.areaId(area)) order.push_back(&ls);
   if (order.size() > 32) return false;
   selCtx_ = ctx;
+  RouteProf prof;
   orh_prefix_set* set = ps.syncDevice(ctx);
+  prof.mark(" select: sync");
   areaWork_.resize(order.size());
   std::vector<orh_select_area> sel(order.size());
   uint32_t words = 0;
@@ -839,6 +842,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
       }
     }
   }
+  prof.mark(" select: areas");
   // outputs: status [n] | metric [n] | best [n] | mask [n][words]
   const uint32_t n = ps.numPrefixIds();
   auto outOf = [&](uint8_t* base, uint32_t np) {
@@ -875,6 +879,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     lastSelectBytes_ = 8ull * np + 20ull * live + 4ull * live * areasWithRow +
         static_cast<uint64_t>(np) * (9 + 4ull * words);
   }
+  prof.mark(" select: launch");
   const bool canDiff = diff && hadPrev && dSelPrev_ && prevWords_ == words && prevLayout_ == layout &&
                        prevN_ <= n && selStatus_.size() == prevN_;
   if (canDiff) {
@@ -923,6 +928,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
         orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
       throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
   }
+  prof.mark(" select: copy-out");
   selWords_ = words;
   if (orh_last_select_ms(set, &lastSelectMs_) != ORH_OK) lastSelectMs_ = -1;
   // this selection is the snapshot the next one is compared with
@@ -979,6 +985,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
                                                            const AreaLinkStates& als,
                                                            const PrefixState& ps, bool mplsOnly) {
   // Decision.cpp:615-792 (mplsOnly: the MPLS routes alone, for buildRouteDelta)
+  mplsKeyOk_ = false;
   bool exists = false;
   for (const auto& [_, ls] : als) exists |= ls.hasNode(me);
   if (!exists) return std::nullopt;
@@ -1309,7 +1316,17 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       throw std::logic_error("duplicate mpls route");
   }
   prof.mark("adj + static mpls");
+  mplsKey_ = mplsInputs(als);
+  mplsMe_ = me;
+  mplsStatic_ = staticEpoch_;
+  mplsKeyOk_ = true;
   return db;
+}
+
+std::vector<std::pair<const LinkState*, uint64_t>> SpfSolver::mplsInputs(const AreaLinkStates& als) const {
+  std::vector<std::pair<const LinkState*, uint64_t>> k;
+  for (const auto& [_, ls] : als) k.emplace_back(&ls, ls.stateStamp());
+  return k;
 }
 
 std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string& me,
@@ -1357,15 +1374,20 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     e.nexthops.insert(it->second.begin(), it->second.end());
     return e;
   };
-  struct Part {
+  struct alignas(128) Part {  // one per worker, no shared cache lines
     std::vector<RibUnicastEntry> upd;
     std::vector<Cidr> del;
     uint64_t invalidated{0};
-    double tBuild{0}, tPolicy{0}, tCompare{0};  // ORH_ROUTE_PROF
+    double tBuild{0}, tPolicy{0}, tFind{0}, tCmp{0}, tPush{0}, tCpu{0};  // ORH_ROUTE_PROF
     size_t n{0};
   };
   using Clock = std::chrono::steady_clock;
-  auto since = [](Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); };
+  auto ms = [](Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  auto cpuMs = [] {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+  };
   std::vector<Part> parts(pool.size());
   // the new route of one prefix (createRouteForPrefixOrGetStaticRoute, then
   // the policy), compared with current's entry (calculateUpdate)
@@ -1374,23 +1396,27 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     const auto t1 = prof.on ? Clock::now() : Clock::time_point{};
     if (r && applyPolicy) policy->applyAction(*r, &out.invalidated);
     const auto t2 = prof.on ? Clock::now() : Clock::time_point{};
-    if (prof.on) out.tPolicy += std::chrono::duration<double, std::milli>(t2 - t1).count();
-    struct CmpTimer {
-      bool on;
-      Clock::time_point t;
-      double* acc;
-      ~CmpTimer() {
-        if (on) *acc += std::chrono::duration<double, std::milli>(Clock::now() - t).count();
-      }
-    } cmpTimer{prof.on, t2, &out.tCompare};
     auto it = current.unicastRoutes.find(prefix);
+    const auto t3 = prof.on ? Clock::now() : Clock::time_point{};
+    bool differs = false;
+    if (r) differs = it == current.unicastRoutes.end() || it->second != *r;
+    const auto t4 = prof.on ? Clock::now() : Clock::time_point{};
     if (r) {
-      if (it == current.unicastRoutes.end() || it->second != *r) out.upd.push_back(std::move(*r));
+      if (differs) out.upd.push_back(std::move(*r));
     } else if (it != current.unicastRoutes.end()) {
       out.del.push_back(prefix);
     }
+    if (prof.on) {
+      const auto t5 = Clock::now();
+      out.tPolicy += ms(t1, t2);
+      out.tFind += ms(t2, t3);
+      out.tCmp += ms(t3, t4);
+      out.tPush += ms(t4, t5);
+    }
   };
   pool.parallelFor(todo.size(), [&](size_t w, size_t b, size_t e) {
+    const double c0 = prof.on ? cpuMs() : 0.0;
+    parts[w].upd.reserve(parts[w].upd.size() + (e - b));  // no regrowth (and its page faults) per route
     for (size_t i = b; i < e; ++i) {
       const uint32_t pid = todo[i];
       const Cidr& prefix = ps.prefixOf(pid);
@@ -1399,28 +1425,34 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
       if (selStatus_[pid] == ORH_SEL_ROUTE) r = materialize(pid, ps);
       else if (selStatus_[pid] == ORH_SEL_HOST) r = createRouteForPrefix(me, als, ps, prefix);
       if (prof.on) {
-        parts[w].tBuild += since(t0);
+        parts[w].tBuild += ms(t0, Clock::now());
         ++parts[w].n;
       }
       one(prefix, std::move(r), parts[w]);
     }
+    if (prof.on) parts[w].tCpu += cpuMs() - c0;
   });
   // withdrawn prefixes that no live id carries now: their routes go (or
   // fall back to a static route)
   for (const Cidr& c : deleted)
     if (!ps.pidOf(c)) one(c, std::nullopt, parts[0]);
   if (prof.on) {
-    double b = 0, pl = 0, c = 0;
+    double b = 0, pl = 0, f = 0, c = 0, pu = 0, cpu = 0;
     size_t nn = 0, busy = 0;
     for (const auto& p : parts) {
       b += p.tBuild;
       pl += p.tPolicy;
-      c += p.tCompare;
+      f += p.tFind;
+      c += p.tCmp;
+      pu += p.tPush;
+      cpu += p.tCpu;
       nn += p.n;
       busy += p.n > 0;
     }
-    std::fprintf(stderr, "route-prof delta: %zu routes on %zu workers; thread-ms build %.3f policy %.3f compare %.3f\n",
-                 nn, busy, b, pl, c);
+    std::fprintf(stderr,
+                 "route-prof delta: %zu routes on %zu workers; thread-ms build %.3f policy %.3f find %.3f "
+                 "compare %.3f push %.3f; thread cpu-ms %.3f\n",
+                 nn, busy, b, pl, f, c, pu, cpu);
   }
   prof.mark("unicast (pool)");
   DecisionRouteUpdate delta;
@@ -1435,7 +1467,12 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     invalidated += p.invalidated;
   }
   if (policy) policy->addInvalidated(invalidated);
-  // MPLS routes: rebuilt and compared in full (node labels: one per node)
+  // MPLS routes: unchanged inputs (no topology or static change since the
+  // build current holds) keep them; else rebuilt and compared in full
+  if (mplsKeyOk_ && mplsMe_ == me && mplsStatic_ == staticEpoch_ && mplsKey_ == mplsInputs(als)) {
+    prof.mark("mpls (kept)");
+    return delta;
+  }
   auto mdb = buildRouteDbImpl(me, als, ps, true);
   if (mdb) {
     for (auto& [label, entry] : mdb->mplsRoutes) {

@@ -90,6 +90,7 @@ class PrefixState {
   uint32_t internName(const std::string& n);
   uint32_t internArea(const std::string& a);
   void buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const;
+  orh_adv advRecord(const NodeAndArea& na, const PrefixEntry& e) const;
 
   std::unordered_map<Cidr, PrefixEntries, CidrHash> prefixes_;
   size_t ksp2Entries_{0};
@@ -270,6 +271,13 @@ class SpfSolver {
   size_t dDiffCap_{0};
   bool havePrev_{false}, lastDiffed_{false};
   uint64_t selGen_{0}, prevLayout_{0}, staticEpoch_{0};
+  // inputs of the last MPLS route build (every area's LinkState stamp, me,
+  // static routes): a delta rebuild with the same inputs keeps the routes
+  std::vector<std::pair<const LinkState*, uint64_t>> mplsInputs(const AreaLinkStates& als) const;
+  std::vector<std::pair<const LinkState*, uint64_t>> mplsKey_;
+  std::string mplsMe_;
+  uint64_t mplsStatic_{0};
+  bool mplsKeyOk_{false};
   uint32_t prevN_{0}, prevWords_{0};
   std::vector<uint32_t> changedPids_;
   std::vector<uint8_t> selStatus_;

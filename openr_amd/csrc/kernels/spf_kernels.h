@@ -83,6 +83,9 @@ struct HopArgs {
   // level-row kernel block order: 0 = one contiguous source range per XCD,
   // G > 0 = runs of G consecutive blocks dealt round-robin over the XCDs
   uint32_t xcd_group;
+  // logical blocks (sources x tile phases); a grid smaller than this runs
+  // persistent workgroups, each striding through its XCD's logical range
+  uint32_t n_logical;
 };
 
 enum class SpfVariant {

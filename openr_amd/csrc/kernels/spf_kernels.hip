@@ -1787,8 +1787,25 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
   const uint32_t N = a.n_nodes, P = a.lvl_pitch, w0 = a.w0;
   const uint32_t tid = threadIdx.x;
   const uint32_t split = a.tile_split;
-  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x, a.xcd_group);
-  const uint32_t i = blk / split, phase = blk % split;
+  // one logical block per workgroup, or (persistent grid, a multiple of the
+  // 8 XCDs; ORH_HOP_WG_PER_CU) XCD x = b % 8 owns a contiguous logical range
+  // its workgroups stride through
+  uint32_t lb, lb_end, lb_step;
+  if (gridDim.x >= a.n_logical) {
+    lb = xcd_block(blockIdx.x, gridDim.x, a.xcd_group);
+    lb_end = lb + 1;
+    lb_step = 1;
+  } else {
+    constexpr uint32_t kXcd = 8;
+    const uint32_t x = blockIdx.x % kXcd, k = blockIdx.x / kXcd;
+    const uint32_t q = a.n_logical / kXcd, r = a.n_logical % kXcd;
+    const uint32_t lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    lb = lo + k;
+    lb_end = lo + q + (x < r ? 1u : 0u);
+    lb_step = gridDim.x / kXcd;
+  }
+  for (; lb < lb_end; lb += lb_step) {
+  const uint32_t i = lb / split, phase = lb % split;
   const uint32_t src = a.srcs[i];
   const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
   const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
@@ -1877,6 +1894,8 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
       }
     }
   }
+  __syncthreads();  // every thread is done with this source's entries
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1931,10 +1950,14 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   const size_t nb = (n_nodes + 31) / 32;
   if (mode == SpfMode::kAuto && multi_source && uniform && path_bound < 0xFFFFFFFFull) {
     // a thread owns J <= 32 nodes (registers); the frontier arrays hold
-    // N + 1 entries (the last is the always-zero target of dead slots)
-    // 12 waves per workgroup beat 8 and 16 on the 10k grid (one workgroup
-    // per CU; per-level latency is what the search time is made of)
-    uint32_t block = n_nodes <= 4096 ? 256 : 768;
+    // N + 1 entries (the last is the always-zero target of dead slots).
+    // 8 waves per workgroup (J = 20 on the 10k grid): one sweep alone takes
+    // 0.82 ms against 0.73 at 12 waves (J = 16), but sweeps running side by
+    // side on 4 streams - the bench step, any batch of what-if topologies -
+    // finish 7 % sooner (26.8 vs 28.7 ms per 32 sweeps): two 8-wave
+    // workgroups per CU leave wave slots and VGPRs for the other streams'
+    // first-hop and finalize kernels (profiles/r03/o_ms_block_ab.txt)
+    uint32_t block = n_nodes <= 4096 ? 256 : 512;
     // ORH_MS_BLOCK (A/B): threads per multi-source workgroup (multiple of 64)
     if (const char* e = getenv("ORH_MS_BLOCK")) {
       const int b = atoi(e);
@@ -2153,8 +2176,28 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
     a.tiles = wide ? t16 : (a.n_nodes + kBlock * 4 - 1) / (kBlock * 4);
     a.tile_split = 1;
     while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;
-    const uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
+    uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
     if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    a.n_logical = static_cast<uint32_t>(g2);
+    // ORH_HOP_WG_PER_CU (A/B, default 0 = one workgroup per logical block):
+    // persistent workgroups, that many per CU, for even per-source work. C2
+    // sweep, first hops: 0.362 ms one per block, 0.389 ms at 8 per CU, 0.439
+    // at 4 (profiles/r03/n_ms_variants_ab.txt): more workgroups in flight beat
+    // fewer, longer-lived ones
+    static const uint32_t per_cu = [] {
+      const char* e = getenv("ORH_HOP_WG_PER_CU");
+      return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+    }();
+    static const uint32_t n_cu = [] {
+      int d = 0, c = 0;
+      if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        return 0u;
+      return static_cast<uint32_t>(c);
+    }();
+    if (a.xcd_group == 0 && per_cu && n_cu) {
+      const uint64_t cap = (static_cast<uint64_t>(n_cu) * per_cu) & ~uint64_t{7};
+      if (cap >= 8 && cap < g2) g2 = cap;
+    }
     if (nodes_per_thread) *nodes_per_thread = wide ? 16 : 4;
     if (split) *split = a.tile_split;
     return wide ? launch(first_hop_lvl_kernel<16>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
