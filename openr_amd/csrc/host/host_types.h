@@ -405,10 +405,26 @@ struct DecisionRouteDb {
     return delta;
   }
 
-  // update (openr/decision/Decision.cpp:146-160): deletes first, then updates
+  // update (openr/decision/Decision.cpp:146-160): deletes first, then
+  // updates; every key stays in its shard, so large updates run shard by
+  // shard on the pool
   void update(const DecisionRouteUpdate& u) {
-    for (const auto& p : u.unicastRoutesToDelete) unicastRoutes.erase(p);
-    for (const auto& [_, e] : u.unicastRoutesToUpdate) unicastRoutes.insert_or_assign(e.prefix, e);
+    constexpr size_t kS = UnicastRouteMap::kShards;
+    auto& pool = WorkerPool::instance();
+    if (u.unicastRoutesToDelete.size() + u.unicastRoutesToUpdate.size() >= 4096 && pool.size() > 1) {
+      std::vector<std::vector<const Cidr*>> del(kS);
+      for (const auto& p : u.unicastRoutesToDelete) del[UnicastRouteMap::shardOf(p)].push_back(&p);
+      pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
+        for (size_t s = b; s < e; ++s) {
+          auto& dst = unicastRoutes.shard(s);
+          for (const Cidr* p : del[s]) dst.erase(*p);
+          for (const auto& [_, r] : u.unicastRoutesToUpdate.shard(s)) dst.insert_or_assign(r.prefix, r);
+        }
+      });
+    } else {
+      for (const auto& p : u.unicastRoutesToDelete) unicastRoutes.erase(p);
+      for (const auto& [_, e] : u.unicastRoutesToUpdate) unicastRoutes.insert_or_assign(e.prefix, e);
+    }
     for (auto l : u.mplsRoutesToDelete) mplsRoutes.erase(l);
     for (const auto& e : u.mplsRoutesToUpdate) mplsRoutes.insert_or_assign(e.label, e);
   }

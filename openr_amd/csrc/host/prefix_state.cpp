@@ -195,6 +195,7 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
     });
     for (uint32_t pid = 0; pid < n; ++pid) ptr[pid + 1] += ptr[pid];
     std::vector<orh_adv> recs(ptr[n]);
+    advPool_.reserve(ptr[n] + ptr[n] / 4 + 1024);  // later deltas append without regrowth
     advPool_.assign(ptr[n], AdvRef{});
     advLive_ = ptr[n];
     each([&](uint32_t pid) {

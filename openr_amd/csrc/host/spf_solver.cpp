@@ -1474,14 +1474,28 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     return delta;
   }
   auto mdb = buildRouteDbImpl(me, als, ps, true);
-  if (mdb) {
-    for (auto& [label, entry] : mdb->mplsRoutes) {
-      auto it = current.mplsRoutes.find(label);
-      if (it == current.mplsRoutes.end() || it->second != entry) delta.mplsRoutesToUpdate.push_back(std::move(entry));
+  {  // compared shard by shard (same key -> shard map); lists in iteration order
+    constexpr size_t kS = MplsRouteMap::kShards;
+    std::vector<std::vector<RibMplsEntry>> upd(kS);
+    std::vector<std::vector<int32_t>> del(kS);
+    pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
+      for (size_t sh = b; sh < e; ++sh) {
+        const auto& cur = current.mplsRoutes.shard(sh);
+        if (mdb) {
+          for (auto& [label, entry] : mdb->mplsRoutes.shard(sh)) {
+            auto it = cur.find(label);
+            if (it == cur.end() || it->second != entry) upd[sh].push_back(std::move(entry));
+          }
+        }
+        for (const auto& [label, _] : cur)
+          if (!mdb || !mdb->mplsRoutes.shard(sh).count(label)) del[sh].push_back(label);
+      }
+    });
+    for (size_t sh = 0; sh < kS; ++sh) {
+      for (auto& e : upd[sh]) delta.mplsRoutesToUpdate.push_back(std::move(e));
+      delta.mplsRoutesToDelete.insert(delta.mplsRoutesToDelete.end(), del[sh].begin(), del[sh].end());
     }
   }
-  for (const auto& [label, _] : current.mplsRoutes)
-    if (!mdb || !mdb->mplsRoutes.count(label)) delta.mplsRoutesToDelete.push_back(label);
   prof.mark("mpls");
   return delta;
 }

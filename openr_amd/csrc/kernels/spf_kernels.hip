@@ -94,7 +94,12 @@ struct Src {
   uint32_t node;
   const uint32_t* ign;
   uint32_t n_ign;
-  __device__ Src(const SpfArgs& a, uint32_t row) : node(a.srcs[row]), ign(nullptr), n_ign(0) {
+  // optional LDS filter of the ignore set (a bit per hashed link id, no
+  // false negatives): a clear bit skips the binary search in global memory
+  const uint32_t* filt;
+  uint32_t fshift;
+  __device__ Src(const SpfArgs& a, uint32_t row)
+      : node(a.srcs[row]), ign(nullptr), n_ign(0), filt(nullptr), fshift(0) {
     if (a.ignore_ptr) {
       const uint32_t b = a.ignore_ptr[row];
       ign = a.ignore_links + b;
@@ -103,10 +108,18 @@ struct Src {
   }
 };
 
+__device__ inline uint32_t ign_hash(uint32_t link, uint32_t shift) { return (link * 0x9E3779B1u) >> shift; }
+
 // a record the search may relax: up, not a continuation, not ignored
 __device__ inline bool live(const SpfArgs& a, const Src& s, const uint2& r, uint32_t q) {
-  return !(r.x & (ORH_REC_SKIP | ORH_REC_CONT)) &&
-      !(s.n_ign && ignored(s.ign, s.n_ign, a.link[q]));
+  if (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) return false;
+  if (!s.n_ign) return true;
+  const uint32_t l = a.link[q];
+  if (s.filt) {
+    const uint32_t h = ign_hash(l, s.fshift);
+    if (!((s.filt[h >> 5] >> (h & 31u)) & 1u)) return true;
+  }
+  return !ignored(s.ign, s.n_ign, l);
 }
 
 template <int K>
@@ -1216,16 +1229,40 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
   constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
   constexpr int G = K <= 4 ? 4 : 2;
+  __shared__ uint32_t s_nign;
   uint32_t* near = lds;
   uint32_t* far = lds + NB;
   if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
-  const Src s(a, row);
+  Src s(a, row);
   unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
+  // the plan's third bitmap (the synchronous kernel's second near set) holds
+  // the ignore filter: FW words, a power of two <= 256, and the set's real
+  // length (fixed-stride lists end in ~0u padding, e.g. KSP2's k = 2 rows)
+  uint32_t* filt = lds + 2 * NB;
+  uint32_t FW = 1;
+  while (2 * FW <= min(NB, 256u)) FW *= 2;
+  const uint32_t fshift = 32u - (5u + static_cast<uint32_t>(__builtin_ctz(FW)));
 
   for (uint32_t i = tid; i < 2 * NB; i += nthr) lds[i] = 0u;
+  if (s.n_ign)
+    for (uint32_t i = tid; i < FW; i += nthr) filt[i] = 0u;
   for (uint32_t i = tid; i < N; i += nthr) lab[i] = kInfLabel;
   if (tid < 2) s_min[tid] = kInf;
+  if (tid == 0) s_nign = 0u;
   __syncthreads();
+  if (s.n_ign) {
+    for (uint32_t i = tid; i < s.n_ign; i += nthr) {
+      const uint32_t l = s.ign[i];
+      if (l == 0xFFFFFFFFu) continue;
+      atomicAdd(&s_nign, 1u);
+      const uint32_t h = ign_hash(l, fshift);
+      atomicOr(&filt[h >> 5], 1u << (h & 31u));
+    }
+    __syncthreads();
+    s.n_ign = s_nign;  // sorted: the real entries come first
+    s.filt = filt;
+    s.fshift = fshift;
+  }
   if (tid == 0) {
     lab[s.node] = 0ull;
     near[s.node >> 5] = 1u << (s.node & 31u);
@@ -1847,8 +1884,19 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
         ls[k] = LvlVec<kLvlPer>::byte(own, k);
       }
     }
+    // own level bytes with the source's byte forced to "unreached" (no next
+    // hops; bytes past N are the row padding, unreached already)
+    uint32_t ot[kWords];
+#pragma unroll
+    for (uint32_t q = 0; q < kWords; ++q) ot[q] = ow[q];
+    if (src >= v0 && src < v0 + kLvlPer) {
+#pragma unroll
+      for (uint32_t q = 0; q < kWords; ++q)
+        if ((src - v0) / 4u == q) ot[q] |= 0xFFu << (((src - v0) & 3u) * 8u);
+    }
     for (uint32_t word = 0; word < W; ++word) {
       uint32_t acc[kLvlPer] = {};
+      uint32_t pk[kWords] = {};  // byte k of word q: mask bits 0..7 of node 4q + k (packed path)
       for (uint32_t e = 0; e < ne; ++e) {
         const uint4 en = ent[e];
         const uint32_t r = en.w & 0x7FFFFFFFu;
@@ -1866,7 +1914,18 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
         bool direct = own_direct || en.y != w0;
 #pragma unroll
         for (uint32_t q = 0; q < kWords; ++q) direct |= has_byte_fe(nw[q]);
-        if (!direct) {  // plain levels: tight iff L_n(v) + 1 == L_s(v)
+        if (!direct && bit < 256u) {
+          // plain levels, four nodes per word op: tight iff L_n(v) + 1 ==
+          // L_s(v), bytewise mod 256 (an unreached 255 wraps to 0, a level
+          // only the source holds, forced to 255 in ot)
+#pragma unroll
+          for (uint32_t q = 0; q < kWords; ++q) {
+            const uint32_t inc = ((nw[q] & 0x7F7F7F7Fu) + 0x01010101u) ^ (nw[q] & 0x80808080u);
+            const uint32_t z = inc ^ ot[q];
+            const uint32_t eq = ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);  // 0x80 per zero byte
+            pk[q] |= (eq >> 7) * bit;
+          }
+        } else if (!direct) {  // plain levels, a rank past 7
 #pragma unroll
           for (uint32_t k = 0; k < kLvlPer; ++k)
             if (((nw[k / 4] >> ((k & 3u) * 8u)) & 0xFFu) + 1u == ls[k]) acc[k] |= bit;
@@ -1879,6 +1938,8 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
           }
         }
       }
+#pragma unroll
+      for (uint32_t k = 0; k < kLvlPer; ++k) acc[k] |= (pk[k / 4] >> ((k & 3u) * 8u)) & 0xFFu;
       if (kLvlPer == 16 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
@@ -1957,7 +2018,8 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
     // finish 7 % sooner (26.8 vs 28.7 ms per 32 sweeps): two 8-wave
     // workgroups per CU leave wave slots and VGPRs for the other streams'
     // first-hop and finalize kernels (profiles/r03/o_ms_block_ab.txt)
-    uint32_t block = n_nodes <= 4096 ? 256 : 512;
+    // (past 16,384 nodes 512 threads would need J > 32: 12 waves)
+    uint32_t block = n_nodes <= 4096 ? 256 : n_nodes <= 16384 ? 512 : 768;
     // ORH_MS_BLOCK (A/B): threads per multi-source workgroup (multiple of 64)
     if (const char* e = getenv("ORH_MS_BLOCK")) {
       const int b = atoi(e);

@@ -2315,7 +2315,25 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
   const bool uniform = g->min_out == g->max_out;
   uint32_t chunk = kKspChunk;  // ORH_KSP_CHUNK: pairs per device pass (A/B)
   if (const char* e = getenv("ORH_KSP_CHUNK")) chunk = std::max(1, atoi(e));
+  // ORH_KSP_PROF=1: host and device (events) time of each stage on stderr
+  const bool prof = getenv("ORH_KSP_PROF") != nullptr;
+  constexpr int kStages = 7;
+  static const char* const kStageName[kStages] = {"stage", "k1 search", "k1 trace", "k2 search", "k2 trace",
+                                                  "copy-out", ""};
+  hipEvent_t ev[kStages] = {};
+  double host_ms[kStages] = {};
+  auto h_now = [] { return std::chrono::steady_clock::now(); };
+  auto t_host = h_now();
+  auto mark = [&](int k) {
+    if (!prof) return;
+    if (!ev[k]) hipEventCreate(&ev[k]);
+    hipEventRecord(ev[k], ctx->stream);
+    const auto t = h_now();
+    host_ms[k] += std::chrono::duration<double, std::milli>(t - t_host).count();
+    t_host = t;
+  };
   for (uint32_t c0 = 0; c0 < n_pairs; c0 += chunk) {
+    mark(0);
     const uint32_t P = std::min(chunk, n_pairs - c0);
     // distinct sources of the chunk, and each pair's row among them
     std::vector<uint32_t> srcs, row1(P), rowp(P);
@@ -2366,8 +2384,10 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     br.n_src = S;
     br.use_link_metric = 1;
     const orh_counters c_before = ctx->counters;
+    mark(1);
     rc = orh_spf_run(g, &br, words, D + o_d1, D + o_n1);
     if (rc) return rc;
+    mark(2);
     orh::KspArgs ka{};
     ka.n_nodes = N;
     ka.n_pairs = P;
@@ -2391,6 +2411,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     ka.dist = D + o_d1;
     hipError_t e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=1 trace launch");
+    mark(3);
     // k = 2 searches: every pair with k = 1 paths, its k = 1 links ignored
     // (row mask = need2; one fused first-hop row per pair)
     orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
@@ -2422,18 +2443,34 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.row_mask = D + o_need;
     e = orh::launch_spf(fp, a, P, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
+    mark(4);
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
     ka.k = 2;
     ka.row = D + o_rp;
     ka.dist = D + o_d2;
     e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 trace launch");
+    mark(5);
     ORH_HIP(ctx, hipMemcpyAsync(ctx->h_ksp + size_t{c0} * kKspOutCap, D + o_out, size_t{P} * kKspOutCap * 4,
                                 hipMemcpyDeviceToHost, ctx->stream));
+    mark(6);
     ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ctx->counters = c_before;  // the caller counts runs the reference's way (memo)
     ctx->counters.spf_launches += 3;
+    if (prof) {  // stage k: host time to issue it, device time between its events
+      for (int k = 0; k + 1 < kStages; ++k) {
+        float d = 0.f;
+        hipEventElapsedTime(&d, ev[k], ev[k + 1]);
+        std::fprintf(stderr, "ksp-batch %-10s host %8.3f ms  device %8.3f ms\n", kStageName[k], host_ms[k + 1], d);
+      }
+      std::fprintf(stderr, "ksp-batch after copy-out sync host %8.3f ms\n",
+                   std::chrono::duration<double, std::milli>(h_now() - t_host).count());
+      for (double& h : host_ms) h = 0;
+    }
   }
+  if (prof)
+    for (auto& e : ev)
+      if (e) hipEventDestroy(e);
   return ORH_OK;
 }
 
