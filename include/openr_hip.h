@@ -272,11 +272,13 @@ int orh_whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int
  * h_ignore_links[h_ignore_ptr[i] .. h_ignore_ptr[i+1]) (orh_csr link ids);
  * rows into d_dist [n_req*N] and d_nh [n_req*N] (one word per node). d_info
  * (nullable, [n_req]): ORH_WHATIF_TIER(x) = how the row was made, and
- * ORH_WHATIF_AFFECTED(x) = nodes re-derived (0: the source's row stands).
+ * ORH_WHATIF_AFFECTED(x) = nodes re-derived (0: the source's row stands, or a full search).
  * Host arrays may be reused once the call returns. */
 int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, const uint32_t* h_ignore_ptr,
                    const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info);
-#define ORH_WHATIF_TIER(x) ((x) & 7u) /* 0 source row, 1/2 LDS repair, 3 global-slot repair, 4 full search */
+#define ORH_WHATIF_TIER(x) ((x) & 7u) /* 0 source row, 1/2 LDS repair, 3 global-slot repair, 4 full search
+                                         (subtrees too large for LDS, up to ORH_WHATIF_FULL per run; every
+                                         such request without slots) */
 #define ORH_WHATIF_AFFECTED(x) ((x) >> 3)
 /* search the job's sources again on the graph as it is now (after topology
  * deltas; allocations are kept) - the next runs derive from these rows */

@@ -51,6 +51,11 @@ struct SpfArgs {
   // HBM kernel with fused first hops: rows whose flag is 0 are skipped (the
   // what-if repair's fallback searches only the rows it could not repair)
   const uint32_t* row_mask;  // [n_rows], nullable
+  // HBM kernel with fused first hops: workgroup b searches row row_list[b]
+  // while b < *row_count (else exits), with its labels in slot b (nullable:
+  // workgroup b searches row b)
+  const uint32_t* row_list;
+  const uint32_t* row_count;
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of

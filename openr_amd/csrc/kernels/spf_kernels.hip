@@ -1226,7 +1226,9 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   __shared__ uint32_t s_min[2];
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  if (a.row_list && blockIdx.x >= *a.row_count) return;
+  const uint32_t row = a.row_list ? a.row_list[blockIdx.x] : blockIdx.x;
   constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
   constexpr int G = K <= 4 ? 4 : 2;
   __shared__ uint32_t s_nign;
@@ -1234,7 +1236,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   uint32_t* far = lds + NB;
   if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
   Src s(a, row);
-  unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
+  unsigned long long* lab = a.labels + static_cast<size_t>(a.row_list ? blockIdx.x : row) * N;
   // the plan's third bitmap (the synchronous kernel's second near set) holds
   // the ignore filter: FW words, a power of two <= 256, and the set's real
   // length (fixed-stride lists end in ~0u padding, e.g. KSP2's k = 2 rows)
@@ -1383,7 +1385,9 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   __shared__ uint32_t s_min[2];
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, row = blockIdx.x;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  if (a.row_list && blockIdx.x >= *a.row_count) return;
+  const uint32_t row = a.row_list ? a.row_list[blockIdx.x] : blockIdx.x;
   constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
   // frontier nodes a thread expands together: their record, label and
   // neighbour-label loads are in flight at once (one round trip per stage
@@ -1394,7 +1398,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   uint32_t* far = lds + 2 * NB;
   if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
   const Src s(a, row);
-  unsigned long long* lab = a.labels + static_cast<size_t>(row) * N;
+  unsigned long long* lab = a.labels + static_cast<size_t>(a.row_list ? blockIdx.x : row) * N;
 
   for (uint32_t i = tid; i < 3 * NB; i += nthr) lds[i] = 0u;
   for (uint32_t i = tid; i < N; i += nthr) lab[i] = kInfLabel;

@@ -58,7 +58,14 @@ struct RepairArgs {
   uint32_t n_slots;
   uint32_t n_recs;  // device records (slot edge capacity)
   uint32_t n_cu;    // grid sizing of the queue-draining tiers
+  // the first full_cap entries of the slot tier's queue are searched in full
+  // instead (a separate launch over that list, repair_slot_queue): a large
+  // subtree repairs slower in a slot than the whole search runs; the slot
+  // tier takes the rest and marks those requests kWhatifTierSearch
+  uint32_t full_cap;
 };
+// queue index the slot tier drains (the full search's list)
+uint32_t repair_slot_queue(const RepairArgs& a);
 // LDS bytes of the repair kernel for the given caps
 size_t repair_lds_bytes(uint32_t n_nodes, uint32_t cap_a, uint32_t cap_e);
 // bytes of one global repair slot (whole-graph caps)

@@ -341,9 +341,13 @@ void whatif_repair_kernel(RepairArgs a, uint32_t cap_a, uint32_t cap_e, uint32_t
   uint32_t* bits = alist + cap_a;
   for (uint32_t i = tid; i < NB; i += B) bits[i] = 0u;
   const uint32_t len = a.counters[2 * q];
+  const uint32_t skip = kSlot ? min(len, a.full_cap) : 0u;  // the full search's share
+  if (kSlot && a.info)
+    for (uint32_t i = blockIdx.x * B + tid; i < skip; i += gridDim.x * B)
+      a.info[a.queues[static_cast<size_t>(q) * a.n_req + i]] = kWhatifTierSearch;
   for (;;) {
     if (tid == 0) {
-      const uint32_t i = atomicAdd(&a.counters[2 * q + 1], 1u);
+      const uint32_t i = atomicAdd(&a.counters[2 * q + 1], 1u) + skip;
       s_req = i < len ? a.queues[static_cast<size_t>(q) * a.n_req + i] : ~0u;
     }
     bar();
@@ -450,6 +454,11 @@ hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_li
     hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   return hipGetLastError();
+}
+
+uint32_t repair_slot_queue(const RepairArgs& a) {
+  uint32_t sa = 0, se = 0;
+  return tier1_lds(a, &sa, &se) < repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e) ? 2u : 1u;
 }
 
 hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {

@@ -1159,6 +1159,10 @@ struct orh_whatif {
   // tier-3 slots: the context's (when no other job holds them) or the job's own
   uint8_t* own_slots = nullptr;
   size_t own_slots_cap = 0;
+  // labels of the full searches that take the slot tier's largest repairs
+  // (side stream only, so one buffer serves both run slots)
+  void* d_full_lab = nullptr;
+  size_t full_lab_cap = 0;
 };
 
 namespace {
@@ -1312,6 +1316,29 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ra.n_slots = n_slots;
   ra.n_recs = g->n_recs;
   ra.n_cu = ctx->n_cu;
+  // ORH_WHATIF_FULL=n (A/B, default 0): the slot tier's queue goes to full
+  // searches first, up to n rows (labels within 1 GB). C4: 79 requests per
+  // job searched in full 30.7-31.2 ms against 29.6 ms in slots
+  // (profiles/r03/r_c4_full_search_ab.txt): the slots stay the default
+  if (n_slots) {
+    static const uint32_t full_env = [] {
+      const char* e = getenv("ORH_WHATIF_FULL");
+      return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+    }();
+    const size_t by_mem = (size_t{1} << 30) / (static_cast<size_t>(N) * 8);
+    ra.full_cap = static_cast<uint32_t>(std::min<size_t>({full_env, by_mem, n_req}));
+    if (ra.full_cap) {
+      const size_t need = static_cast<size_t>(ra.full_cap) * N * 8;
+      if (need > job->full_lab_cap) {
+        ORH_HIP(ctx, hipStreamSynchronize(job->side));  // the old buffer may be in use
+        hipFree(job->d_full_lab);
+        job->d_full_lab = nullptr;
+        job->full_lab_cap = 0;
+        ORH_HIP(ctx, hipMalloc(&job->d_full_lab, need));
+        job->full_lab_cap = need;
+      }
+    }
+  }
   hipError_t e = orh::launch_repair_front(ra, g->ell_k, ctx->lds_limit, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch");
   ORH_HIP(ctx, hipEventRecord(job->front_ev[c], ctx->stream));
@@ -1320,6 +1347,39 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ORH_HIP(ctx, hipStreamWaitEvent(job->side, job->front_ev[c], 0));
   e = orh::launch_repair_back(ra, g->ell_k, ctx->lds_limit, job->side);
   if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch (large tiers)");
+  if (n_slots && ra.full_cap) {
+    // workgroup b searches request queue[b] while b < the queue's length
+    const uint32_t q = orh::repair_slot_queue(ra);
+    orh::SpfPlan fp = orh::plan_spf(N, job->uniform, job->bound, g->ell_k, ctx->lds_limit, false,
+                                    orh::SpfMode::kGlobal);
+    if (fp.variant == orh::SpfVariant::kUnsupported)
+      return fail(ctx, ORH_E_UNSUPPORTED, "what-if: no search plan for this graph");
+    fp.variant = orh::SpfVariant::kGlobalNh;
+    fp.block = 1024;
+    orh::SpfArgs a{};
+    a.n_nodes = N;
+    a.n_out = n_req;
+    a.recs = g->d_recs;
+    a.link = g->d_link;
+    a.srcs = ra.srcs;
+    a.ignore_ptr = ra.ign_ptr;
+    a.ignore_links = ra.ign;
+    a.use_link_metric = job->use_link_metric;
+    a.w0 = job->use_link_metric ? g->max_out : 1u;
+    a.delta = job->uniform ? a.w0
+                           : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                        static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+    a.out_dist = d_dist;
+    a.scratch = ctx->d_scratch;
+    a.labels = static_cast<unsigned long long*>(job->d_full_lab);
+    a.out_nh = d_nh;
+    a.words = 1;
+    a.rank_out = g->d_rank_out;
+    a.row_list = ra.queues + static_cast<size_t>(q) * n_req;
+    a.row_count = ra.counters + 2 * q;
+    e = orh::launch_spf(fp, a, ra.full_cap, job->side);
+    if (e != hipSuccess) return hip_fail(ctx, e, "what-if full-search launch");
+  }
   if (n_slots == 0) {
     // no slot fits the budget: the requests that outgrew tier 2 are searched
     // in full (spf_global_nh_kernel with the flags as its row mask)
@@ -1574,6 +1634,7 @@ int orh_whatif_destroy(orh_whatif* job) {
   }
   hipFree(job->d_base);
   hipFree(job->own_slots);
+  hipFree(job->d_full_lab);
   if (job->g->ctx->slots_owner == job) job->g->ctx->slots_owner = nullptr;
   if (job->side) hipStreamDestroy(job->side);
   if (job->ev_begin) hipEventDestroy(job->ev_begin);

@@ -232,14 +232,19 @@ def test_c4_bench_batch_vs_oracle(hip, oracle):
     big.sync()
     info = big.info()
     tier, affected = info & 7, info >> 3
-    assert int(tier.max()) <= 3, "a request took the full-search fallback although slots exist"
-    assert np.array_equal(tier == 0, affected == 0)
+    # tiers 1-3 repair (affected > 0); tier 4 searches in full the slot
+    # tier's queue (the subtrees too large for LDS) and reports no count
+    assert int(tier.max()) <= 4
+    assert np.array_equal((tier >= 1) & (tier <= 3), affected > 0)
+    assert not np.any(affected[tier == 0])
+    searched = [int(i) for i in np.nonzero(tier == 4)[0]]
     repaired = np.nonzero(affected)[0]
     assert 0 < len(repaired) < len(idx)
     rng = random.Random(44)
     top = [int(i) for i in repaired[np.argsort(-affected[repaired], kind="stable")[:24]]]
     rest = sorted(set(int(i) for i in repaired) - set(top))
-    pick = top + rng.sample(rest, 24) + rng.sample([int(i) for i in np.nonzero(affected == 0)[0]], 8)
+    pick = (top + rng.sample(rest, 24) + rng.sample(searched, min(16, len(searched))) +
+            rng.sample([int(i) for i in np.nonzero(tier == 0)[0]], 8))
     sub = ls.what_if_batch(srcs, [idx[i] for i in pick], [sets[i] for i in pick], len(pick))
     sub.run()
     sub.sync()
@@ -262,6 +267,7 @@ def test_c4_bench_batch_vs_oracle(hip, oracle):
         d, m = got[k]
         np.testing.assert_array_equal(d, dist_o[len(srcs) + k], err_msg=f"request {i} dist")
         np.testing.assert_array_equal(m, nh_o[len(srcs) + k], err_msg=f"request {i} nh")
-        changed = int(np.sum((d != dist_o[idx[i]]) | (m != nh_o[idx[i]])))
-        assert changed <= affected[i], (i, changed, affected[i])
+        if 1 <= tier[i] <= 3:
+            changed = int(np.sum((d != dist_o[idx[i]]) | (m != nh_o[idx[i]])))
+            assert changed <= affected[i], (i, changed, affected[i])
     assert affected[top[0]] > 100  # the largest sets leave the small LDS tier
