@@ -56,6 +56,8 @@ struct SpfArgs {
   // workgroup b searches row b)
   const uint32_t* row_list;
   const uint32_t* row_count;
+  // HBM kernel (kGlobalNh plan): distances only, u32 labels, out_nh unused
+  int32_t dist_only;
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of

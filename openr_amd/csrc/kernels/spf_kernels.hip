@@ -46,6 +46,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "spf_kernels.h"
@@ -1154,18 +1155,26 @@ __global__ __launch_bounds__(256) void spf_global_kernel(SpfArgs a) {
 // neighbour-label loads are in flight together (one round trip per stage for
 // the group instead of per node), then merge(u, nd, cnh, cl) runs per live
 // out-edge with u's label cl as loaded.
-template <int K, int G, typename Merge>
-__device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, unsigned long long* lab,
+// label access: {dist (hi), first-hop mask (lo)} in a u64, or the distance
+// alone in a u32 (dist-only searches: KSP2 rows feed traces, not first hops)
+__device__ inline uint32_t lab_dist(unsigned long long l) { return static_cast<uint32_t>(l >> 32); }
+__device__ inline uint32_t lab_dist(uint32_t l) { return l; }
+__device__ inline uint32_t lab_nh(unsigned long long l) { return static_cast<uint32_t>(l); }
+__device__ inline uint32_t lab_nh(uint32_t) { return 0u; }
+
+template <int K, int G, typename L, typename Merge>
+__device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* lab,
                                              const uint32_t (&vs)[G], int c, Merge& merge) {
+  constexpr bool kNh = sizeof(L) == 8;
   uint2 rec[G][K];
-  unsigned long long lv[G];
+  L lv[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (g >= c) break;
     load_recs<K>(a, vs[g], rec[g]);
     lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  unsigned long long cl[G][K];
+  L cl[G][K];
   bool ok[G][K];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -1183,9 +1192,9 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, uns
     if (g >= c) break;
     const uint32_t v = vs[g];
     if (v != s.node && (rec[g][0].x & ORH_REC_ROW_OVL)) continue;  // no transit
-    const uint32_t dv = static_cast<uint32_t>(lv[g] >> 32);
-    const uint32_t nhv = static_cast<uint32_t>(lv[g]);
-    const bool from_src = v == s.node;
+    const uint32_t dv = lab_dist(lv[g]);
+    const uint32_t nhv = lab_nh(lv[g]);
+    const bool from_src = kNh && v == s.node;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       if (!ok[g][j]) continue;
@@ -1219,8 +1228,9 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, uns
 // result is the synchronous kernel's bit for bit; what goes away is the
 // per-round barrier that held every wave to the slowest one (the C4 WAN runs
 // about a hundred near rounds per search).
-template <int K>
+template <int K, bool kNh>
 __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
+  typedef typename std::conditional<kNh, unsigned long long, uint32_t>::type L;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_work;
   __shared__ uint32_t s_min[2];
@@ -1229,14 +1239,14 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
   if (a.row_list && blockIdx.x >= *a.row_count) return;
   const uint32_t row = a.row_list ? a.row_list[blockIdx.x] : blockIdx.x;
-  constexpr unsigned long long kInfLabel = 0xFFFFFFFF00000000ull;
+  constexpr L kInfLabel = kNh ? static_cast<L>(0xFFFFFFFF00000000ull) : static_cast<L>(kInf);
   constexpr int G = K <= 4 ? 4 : 2;
   __shared__ uint32_t s_nign;
   uint32_t* near = lds;
   uint32_t* far = lds + NB;
   if (a.row_mask && !a.row_mask[row]) return;  // repaired elsewhere (whole workgroup)
   Src s(a, row);
-  unsigned long long* lab = a.labels + static_cast<size_t>(a.row_list ? blockIdx.x : row) * N;
+  L* lab = reinterpret_cast<L*>(a.labels) + static_cast<size_t>(a.row_list ? blockIdx.x : row) * N;
   // the plan's third bitmap (the synchronous kernel's second near set) holds
   // the ignore filter: FW words, a power of two <= 256, and the set's real
   // length (fixed-stride lists end in ~0u padding, e.g. KSP2's k = 2 rows)
@@ -1266,7 +1276,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
     s.fshift = fshift;
   }
   if (tid == 0) {
-    lab[s.node] = 0ull;
+    lab[s.node] = static_cast<L>(0);
     near[s.node >> 5] = 1u << (s.node & 31u);
     s_work = 1u;
   }
@@ -1277,17 +1287,23 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   uint32_t mpar = 0;
   for (;;) {
     uint32_t far_min = kInf;
-    auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, unsigned long long cl) {
-      for (;;) {
-        const uint32_t cd = static_cast<uint32_t>(cl >> 32);
-        if (nd > cd) return;
-        const unsigned long long nl = nd < cd
-            ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
-            : (cl | cnh);
-        if (nl == cl) return;
-        const unsigned long long old = atomicCAS(&lab[u], cl, nl);
-        if (old == cl) break;
-        cl = old;
+    auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, L cl) {
+      if constexpr (kNh) {
+        for (;;) {
+          const uint32_t cd = static_cast<uint32_t>(cl >> 32);
+          if (nd > cd) return;
+          const unsigned long long nl = nd < cd
+              ? ((static_cast<unsigned long long>(nd) << 32) | cnh)
+              : (cl | cnh);
+          if (nl == cl) return;
+          const unsigned long long old = atomicCAS(&lab[u], cl, nl);
+          if (old == cl) break;
+          cl = old;
+        }
+      } else {  // distance alone: a strict decrease re-queues
+        (void)cnh;
+        if (nd >= cl) return;
+        if (nd >= atomicMin(&lab[u], nd)) return;
       }
       const uint32_t bit = 1u << (u & 31u);
       if (nd < T) {
@@ -1325,7 +1341,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
         continue;
       }
       if (c > 0) {
-        expand_group<K, G>(a, s, lab, vs, c, merge);
+        expand_group<K, G, L>(a, s, lab, vs, c, merge);
         atomicSub(&s_work, static_cast<uint32_t>(c));
       }
     }
@@ -1345,8 +1361,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
       uint32_t fb = far[w2], promote = 0u;
       for (uint32_t q = fb; q; q &= q - 1) {
         const uint32_t b = __builtin_ctz(q);
-        const uint32_t d = static_cast<uint32_t>(
-            __hip_atomic_load(&lab[w2 * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
+        const uint32_t d = lab_dist(__hip_atomic_load(&lab[w2 * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (d < T) promote |= 1u << b;
         else local_min = min(local_min, d);
       }
@@ -1364,16 +1379,17 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   }
   __syncthreads();
   uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
-  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * a.words;
+  uint32_t* on = kNh ? a.out_nh + static_cast<size_t>(row) * N * a.words : nullptr;
   for (uint32_t i = tid; i < N; i += nthr) {
-    const unsigned long long l =
-        __hip_atomic_load(&lab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_nontemporal_store(static_cast<uint32_t>(l >> 32), &od[i]);
-    if (a.words == 1) {
-      __builtin_nontemporal_store(static_cast<uint32_t>(l), &on[i]);
-    } else {
-      on[static_cast<size_t>(i) * a.words] = static_cast<uint32_t>(l);
-      for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
+    const L l = __hip_atomic_load(&lab[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_nontemporal_store(lab_dist(l), &od[i]);
+    if constexpr (kNh) {
+      if (a.words == 1) {
+        __builtin_nontemporal_store(lab_nh(l), &on[i]);
+      } else {
+        on[static_cast<size_t>(i) * a.words] = lab_nh(l);
+        for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
+      }
     }
   }
 }
@@ -2161,8 +2177,10 @@ static hipError_t launch_k(const SpfPlan& plan, const SpfArgs& a, uint32_t n_row
     case SpfVariant::kGlobal:
       return launch(spf_global_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     case SpfVariant::kGlobalNh:
+      if (a.dist_only)  // distances alone (u32 labels), no first-hop rows
+        return launch(spf_global_nh_async_kernel<K, false>, a, n_rows, plan.block, plan.lds_bytes, s);
       if (nh_async())
-        return launch(spf_global_nh_async_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
+        return launch(spf_global_nh_async_kernel<K, true>, a, n_rows, plan.block, plan.lds_bytes, s);
       return launch(spf_global_nh_kernel<K>, a, n_rows, plan.block, plan.lds_bytes, s);
     default:
       return hipErrorInvalidValue;

@@ -2410,11 +2410,9 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     }
     for (uint32_t x : srcs) ro[x] = -1;
     const uint32_t S = static_cast<uint32_t>(srcs.size());
-    uint32_t words = 1;
-    rc = orh_spf_words(g, srcs.data(), S, &words);
-    if (rc) return rc;
-    // device layout (u32 words): dist1 [S][N] | nh1 [S][N][words] | dist2 [P][N] | nh2 [P][N] |
+    // device layout (u32 words): dist1 [S][N] | dist2 [P][N] | sources [S] |
     // src | dst | row1 | rowp | ign_ptr [P+1] | ign [P][cap] | need2 | out | visited | stack
+    // (the traces read distances only: both searches run dist-only)
     const size_t nd1 = static_cast<size_t>(S) * N, nd2 = static_cast<size_t>(P) * N;
     size_t off = 0;
     auto take = [&](size_t words_) {
@@ -2422,7 +2420,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
       off += (words_ + 63) & ~size_t{63};  // 256-byte aligned pieces
       return o;
     };
-    const size_t o_d1 = take(nd1), o_n1 = take(nd1 * words), o_d2 = take(nd2), o_n2 = take(nd2);
+    const size_t o_d1 = take(nd1), o_d2 = take(nd2), o_s1 = take(S);
     const size_t o_src = take(P), o_dst = take(P), o_r1 = take(P), o_rp = take(P), o_ip = take(P + 1);
     const size_t o_ign = take(size_t{P} * kKspIgnCap), o_need = take(P), o_out = take(size_t{P} * kKspOutCap);
     const size_t o_vis = take(size_t{P} * kKspHashCap);
@@ -2438,16 +2436,39 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     ORH_HIP(ctx, hipMemcpyAsync(D + o_r1, row1.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemcpyAsync(D + o_rp, rowp.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemcpyAsync(D + o_ip, ip.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ORH_HIP(ctx, hipMemcpyAsync(D + o_s1, srcs.data(), S * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
+    // both searches: the HBM frontier kernel, distances only (u32 labels)
+    orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
+    if (fp.variant == orh::SpfVariant::kUnsupported)
+      return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: no search plan for this graph");
+    fp.variant = orh::SpfVariant::kGlobalNh;
+    auto block_for = [&](uint32_t rows) { return rows <= ctx->n_cu ? 1024u : rows <= 2 * ctx->n_cu ? 512u : 256u; };
+    rc = ensure_labels(ctx, (std::max(nd1, nd2) + 1) / 2);  // u64 units, u32 labels
+    if (rc) return rc;
+    orh::SpfArgs a{};
+    a.n_nodes = N;
+    a.recs = g->d_recs;
+    a.link = g->d_link;
+    a.use_link_metric = 1;
+    a.w0 = g->max_out;
+    a.delta = uniform ? a.w0
+                      : std::max<uint32_t>(1u, static_cast<uint32_t>(
+                                                   static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+    a.scratch = ctx->d_scratch;
+    a.labels = ctx->d_labels;
+    a.words = 1;
+    a.rank_out = g->d_rank_out;
+    a.dist_only = 1;
     // k = 1 rows: the sources' plain SPFs (LinkState::getSpfResult)
-    orh_spf_request br{};
-    br.h_srcs = srcs.data();
-    br.n_src = S;
-    br.use_link_metric = 1;
+    a.n_out = S;
+    a.srcs = D + o_s1;
+    a.out_dist = D + o_d1;
+    fp.block = block_for(S);
     const orh_counters c_before = ctx->counters;
     mark(1);
-    rc = orh_spf_run(g, &br, words, D + o_d1, D + o_n1);
-    if (rc) return rc;
+    hipError_t e = orh::launch_spf(fp, a, S, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=1 search launch");
     mark(2);
     orh::KspArgs ka{};
     ka.n_nodes = N;
@@ -2470,38 +2491,18 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     ka.k = 1;
     ka.row = D + o_r1;
     ka.dist = D + o_d1;
-    hipError_t e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
+    e = orh::launch_ksp_trace(ka, g->ell_k, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=1 trace launch");
     mark(3);
     // k = 2 searches: every pair with k = 1 paths, its k = 1 links ignored
-    // (row mask = need2; one fused first-hop row per pair)
-    orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
-    if (fp.variant == orh::SpfVariant::kUnsupported)
-      return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: no search plan for this graph");
-    fp.variant = orh::SpfVariant::kGlobalNh;
-    fp.block = P <= ctx->n_cu ? 1024u : P <= 2 * ctx->n_cu ? 512u : 256u;
-    rc = ensure_labels(ctx, nd2);
-    if (rc) return rc;
-    orh::SpfArgs a{};
-    a.n_nodes = N;
+    // (row mask = need2)
     a.n_out = P;
-    a.recs = g->d_recs;
-    a.link = g->d_link;
     a.srcs = D + o_src;
     a.ignore_ptr = D + o_ip;
     a.ignore_links = D + o_ign;
-    a.use_link_metric = 1;
-    a.w0 = g->max_out;
-    a.delta = uniform ? a.w0
-                      : std::max<uint32_t>(1u, static_cast<uint32_t>(
-                                                   static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
     a.out_dist = D + o_d2;
-    a.scratch = ctx->d_scratch;
-    a.labels = ctx->d_labels;
-    a.out_nh = D + o_n2;
-    a.words = 1;
-    a.rank_out = g->d_rank_out;
     a.row_mask = D + o_need;
+    fp.block = block_for(P);
     e = orh::launch_spf(fp, a, P, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
     mark(4);
