@@ -141,6 +141,21 @@ def leg_c4(hip, cpu, reps=3, chunk=None):
     out_bytes = n_req * n_nodes * 8  # the rows alone (the output floor)
     tiers = {int(t): int((info & 7 == t).sum()) for t in range(5)}
     aff = info >> 3
+    # the same job with ORH_WHATIF_SHARE_BASE: a source-row request's row is
+    # the job's base row (referenced, not copied); only repaired rows land
+    # in the row buffer
+    del batch
+    shared = ls.what_if_batch(srcs, idx, sets, chunk, share_base=True)
+    shared.run()
+    shared.sync()
+    s_walls = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        shared.run()
+        shared.sync()
+        s_walls.append(time.perf_counter() - t0)
+    s_dt = statistics.median(s_walls)
+    del shared
     kp = c4_ksp2_pairs(names, C4_KSP2_PAIRS)
     ls.prefetch_kth_paths(c4_ksp2_pairs(names, 64, seed=C4_SEED + 99))  # warm-up pairs (not memoized for kp)
     t0 = time.perf_counter()
@@ -164,6 +179,12 @@ def leg_c4(hip, cpu, reps=3, chunk=None):
                                 "frac": round(out_bytes / (dev_ms * 1e-3) / 1e9 / 8000.0, 4),
                                 "b_spf_equivalent": {"bytes_per_spf": b_spf,
                                                      "gbs": round(n_req * b_spf / (dev_ms * 1e-3) / 1e9, 1)}},
+           "what_if_shared_base": {"what_if_spfs_per_s": round(n_req / s_dt, 1),
+                                   "batch_ms": round(s_dt * 1e3, 3),
+                                   "rows_written": n_req - tiers[0],
+                                   "note": "ORH_WHATIF_SHARE_BASE: the 50 % of requests whose source row stands "
+                                           "reference the job's base row instead of a copy (same tiers, rows "
+                                           "bit-identical: test_c4_shared_base_rows)"},
            "ksp2_pairs_per_s": round(len(kp) / kdt, 1),
            "ksp2_batch": f"{len(kp)} (src, dst) getKthPaths k=1,2 (prefetchKthPaths)"}
     if cpu:

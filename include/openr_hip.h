@@ -280,6 +280,16 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
                                          (subtrees too large for LDS, up to ORH_WHATIF_FULL per run; every
                                          such request without slots) */
 #define ORH_WHATIF_AFFECTED(x) ((x) >> 3)
+/* job flags (orh_whatif_set_flags, before a run):
+ * ORH_WHATIF_SHARE_BASE  a request whose source row stands (tier 0) is not
+ *   copied into d_dist / d_nh: its row IS the job's base row of its source
+ *   (orh_whatif_base_rows). A C4-shaped run then writes the repaired rows
+ *   only (half the 105 GB). */
+#define ORH_WHATIF_SHARE_BASE 1u
+int orh_whatif_set_flags(orh_whatif* job, uint32_t flags);
+/* the job's base rows: dist [m][N] and first-hop masks [m][N] (one word per
+ * node) of its m sources, valid until the next orh_whatif_refresh / destroy */
+int orh_whatif_base_rows(orh_whatif* job, const uint32_t** d_dist, const uint32_t** d_nh);
 /* search the job's sources again on the graph as it is now (after topology
  * deltas; allocations are kept) - the next runs derive from these rows */
 int orh_whatif_refresh(orh_whatif* job);

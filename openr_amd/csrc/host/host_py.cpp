@@ -401,8 +401,9 @@ class SpfSweep {
 class WhatIfBatch {
  public:
   WhatIfBatch(const LinkState& ls, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
-              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric)
-      : useLinkMetric_(useLinkMetric) {
+              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric,
+              bool shareBase = false)
+      : useLinkMetric_(useLinkMetric), shareBase_(shareBase) {
     if (srcIdx.size() != ignore.size()) throw std::invalid_argument("WhatIfBatch: one ignore set per request");
     if (chunk == 0) throw std::invalid_argument("WhatIfBatch: chunk must be positive");
     for (const auto& s : srcs) {
@@ -457,6 +458,8 @@ class WhatIfBatch {
       if (orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
                             &job_) != ORH_OK)
         throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
+      if (shareBase_ && orh_whatif_set_flags(job_, ORH_WHATIF_SHARE_BASE) != ORH_OK)
+        throw std::runtime_error(std::string("orh_whatif_set_flags: ") + orh_last_error(ctx_));
     } else if (orh_whatif_refresh(job_) != ORH_OK) {
       throw std::runtime_error(std::string("orh_whatif_refresh: ") + orh_last_error(ctx_));
     }
@@ -489,9 +492,21 @@ class WhatIfBatch {
     if (i < last.lo || i >= last.hi) throw std::out_of_range("WhatIfBatch.fetch: not in the last chunk");
     const size_t r = i - last.lo;
     const int b = static_cast<int>((chunks_.size() - 1) & 1);
+    const uint32_t* d = dDist_[b] + r * n_;
+    const uint32_t* m = dNh_[b] + r * n_;
+    if (shareBase_) {  // a request whose source row stands reads the job's base row
+      uint32_t inf = 0;
+      orh_memcpy_d2h(ctx_, &inf, dInfo_ + i, 4);
+      if (ORH_WHATIF_TIER(inf) == 0) {
+        const uint32_t *bd = nullptr, *bn = nullptr;
+        if (orh_whatif_base_rows(job_, &bd, &bn) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
+        d = bd + static_cast<size_t>(srcIdx_[i]) * n_;
+        m = bn + static_cast<size_t>(srcIdx_[i]) * n_;
+      }
+    }
     py::array_t<uint32_t> dist(n_), nh(n_);
-    orh_memcpy_d2h(ctx_, dist.mutable_data(), dDist_[b] + r * n_, n_ * 4ull);
-    orh_memcpy_d2h(ctx_, nh.mutable_data(), dNh_[b] + r * n_, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, dist.mutable_data(), d, n_ * 4ull);
+    orh_memcpy_d2h(ctx_, nh.mutable_data(), m, n_ * 4ull);
     return py::make_tuple(dist, nh);
   }
   size_t requests() const { return srcIdx_.size(); }
@@ -505,6 +520,7 @@ class WhatIfBatch {
     std::vector<uint32_t> ptr, links;
   };
   bool useLinkMetric_;
+  bool shareBase_;
   std::vector<uint32_t> srcs_, srcIdx_;
   std::vector<Chunk> chunks_;
   uint32_t chunk_{1};
@@ -850,11 +866,13 @@ PYBIND11_MODULE(_openr_host, m) {
            py::keep_alive<0, 1>())
       .def("what_if_batch",  // a what-if job over `srcs`: request i = (srcs[src_idx[i]], ignore[i])
            [](const LinkState& s, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
-              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric) {
-             return new WhatIfBatch(s, srcs, srcIdx, ignore, chunk, useLinkMetric);
+              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric,
+              bool shareBase) {
+             return new WhatIfBatch(s, srcs, srcIdx, ignore, chunk, useLinkMetric, shareBase);
            },
            py::arg("srcs"), py::arg("src_idx"), py::arg("ignore"), py::arg("chunk") = 4096,
-           py::arg("use_link_metric") = true, py::return_value_policy::take_ownership, py::keep_alive<0, 1>())
+           py::arg("use_link_metric") = true, py::arg("share_base") = false,
+           py::return_value_policy::take_ownership, py::keep_alive<0, 1>())
       .def("run_spf_batch",
            [](const LinkState& s, const std::vector<std::string>& srcs,
               const std::vector<std::vector<uint32_t>>& ignore, bool useLinkMetric) {

@@ -63,6 +63,9 @@ struct RepairArgs {
   // subtree repairs slower in a slot than the whole search runs; the slot
   // tier takes the rest and marks those requests kWhatifTierSearch
   uint32_t full_cap;
+  // copy only the requests the seed queued for repair (queue 0): the others'
+  // rows are their sources' base rows, which the caller reads from the job
+  uint32_t share_base;
 };
 // queue index the slot tier drains (the full search's list)
 uint32_t repair_slot_queue(const RepairArgs& a);
@@ -78,5 +81,10 @@ hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, 
 // second stream, overlapping the next batch's copy
 hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
 hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s);
+// the same with the slot tier on its own stream s3, after event `mid`
+// (recorded on s behind tiers 1 and 2): the next run's small tiers on s do
+// not wait for this run's largest repairs
+hipError_t launch_repair_back_split(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s,
+                                    hipStream_t s3, hipEvent_t mid);
 
 }  // namespace orh

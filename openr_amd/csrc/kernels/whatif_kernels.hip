@@ -102,7 +102,12 @@ constexpr uint32_t kCopyTile = 256 * 16;  // u32 elements of a row per copy work
 // base rows -> request rows; vec: every row is 16-byte aligned (N % 4 == 0
 // and aligned buffers), so a thread moves uint4s
 __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t tiles, uint32_t vec) {
-  const uint32_t r = blockIdx.x / tiles, t = blockIdx.x % tiles;
+  uint32_t r = blockIdx.x / tiles;
+  const uint32_t t = blockIdx.x % tiles;
+  if (a.share_base) {  // block i copies the i-th queued request's row
+    if (r >= a.counters[0]) return;
+    r = a.queues[r];
+  }
   const size_t N = a.n_nodes;
   const size_t b = a.base_row[r];
   const uint32_t* sd = a.base_dist + b * N;
@@ -422,6 +427,11 @@ hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_l
 }
 
 hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {
+  return launch_repair_back_split(a, ell_k, lds_limit, s, s, nullptr);
+}
+
+hipError_t launch_repair_back_split(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s,
+                                    hipStream_t s3, hipEvent_t mid) {
   if (a.n_req == 0) return hipSuccess;
   if (ell_k != 4 && ell_k != 8) return hipErrorInvalidValue;
   uint32_t sa = 0, se = 0;
@@ -447,11 +457,14 @@ hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_li
                        lds2, s, a, a.cap_a, a.cap_e, q2);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a.n_slots == 0) return e;
+  if (s3 != s) {
+    if ((e = hipEventRecord(mid, s)) != hipSuccess || (e = hipStreamWaitEvent(s3, mid, 0)) != hipSuccess) return e;
+  }
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
+    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s, a,
+    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   return hipGetLastError();
 }

@@ -1163,6 +1163,14 @@ struct orh_whatif {
   // (side stream only, so one buffer serves both run slots)
   void* d_full_lab = nullptr;
   size_t full_lab_cap = 0;
+  uint32_t flags = 0;  // ORH_WHATIF_* job flags
+  // the slot tier of run slot c on its own stream t3[c], with its own slot
+  // memory, after event mid_ev[c] (tiers 1 and 2 done on `side`): the next
+  // run's small tiers start without waiting for this run's largest repairs
+  hipStream_t t3[2] = {nullptr, nullptr};
+  hipEvent_t mid_ev[2] = {nullptr, nullptr};
+  uint8_t* t3_slots[2] = {nullptr, nullptr};
+  size_t t3_slots_cap[2] = {0, 0};
 };
 
 namespace {
@@ -1274,7 +1282,27 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   const uint32_t n_slots = static_cast<uint32_t>(std::min<size_t>(
       std::min<size_t>(kRepairSlots, n_req), kRepairSlotBudget / std::max<size_t>(slot_bytes, 1)));
   uint8_t* slot_mem = nullptr;
-  if (n_slots) {
+  static const uint32_t full_env = [] {
+    const char* e = getenv("ORH_WHATIF_FULL");
+    return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+  }();
+  static const bool t3_split = [] {  // ORH_WHATIF_T3_SPLIT=0: the slot tier stays on `side` (A/B)
+    const char* e = getenv("ORH_WHATIF_T3_SPLIT");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool split = n_slots && full_env == 0 && t3_split;
+  if (split) {
+    // run slot c's own slot memory, grown only with its stream idle
+    if (n_slots * slot_bytes > job->t3_slots_cap[c]) {
+      ORH_HIP(ctx, hipStreamSynchronize(job->t3[c]));
+      hipFree(job->t3_slots[c]);
+      job->t3_slots[c] = nullptr;
+      job->t3_slots_cap[c] = 0;
+      ORH_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&job->t3_slots[c]), n_slots * slot_bytes));
+      job->t3_slots_cap[c] = n_slots * slot_bytes;
+    }
+    slot_mem = job->t3_slots[c];
+  } else if (n_slots) {
     // the context's slots while no other job's side stream may use them,
     // else the job's own; grown only with the side stream idle
     if (!ctx->slots_owner) ctx->slots_owner = job;
@@ -1316,15 +1344,12 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ra.n_slots = n_slots;
   ra.n_recs = g->n_recs;
   ra.n_cu = ctx->n_cu;
+  ra.share_base = (job->flags & ORH_WHATIF_SHARE_BASE) ? 1u : 0u;
   // ORH_WHATIF_FULL=n (A/B, default 0): the slot tier's queue goes to full
   // searches first, up to n rows (labels within 1 GB). C4: 79 requests per
   // job searched in full 30.7-31.2 ms against 29.6 ms in slots
   // (profiles/r03/r_c4_full_search_ab.txt): the slots stay the default
   if (n_slots) {
-    static const uint32_t full_env = [] {
-      const char* e = getenv("ORH_WHATIF_FULL");
-      return e ? static_cast<uint32_t>(atoi(e)) : 0u;
-    }();
     const size_t by_mem = (size_t{1} << 30) / (static_cast<size_t>(N) * 8);
     ra.full_cap = static_cast<uint32_t>(std::min<size_t>({full_env, by_mem, n_req}));
     if (ra.full_cap) {
@@ -1345,7 +1370,8 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   // the large repairs on the side stream, after this run's front part; the
   // previous side part is ordered before them on that stream
   ORH_HIP(ctx, hipStreamWaitEvent(job->side, job->front_ev[c], 0));
-  e = orh::launch_repair_back(ra, g->ell_k, ctx->lds_limit, job->side);
+  e = split ? orh::launch_repair_back_split(ra, g->ell_k, ctx->lds_limit, job->side, job->t3[c], job->mid_ev[c])
+            : orh::launch_repair_back(ra, g->ell_k, ctx->lds_limit, job->side);
   if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch (large tiers)");
   if (n_slots && ra.full_cap) {
     // workgroup b searches request queue[b] while b < the queue's length
@@ -1413,7 +1439,9 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
     e = orh::launch_spf(fp, a, n_req, job->side);
     if (e != hipSuccess) return hip_fail(ctx, e, "what-if fallback launch");
   }
-  ORH_HIP(ctx, hipEventRecord(job->side_ev[c], job->side));
+  // the run's side part ends with its slot tier (t3[c], ordered after tiers
+  // 1 and 2 through mid_ev[c]) or on `side`
+  ORH_HIP(ctx, hipEventRecord(job->side_ev[c], split ? job->t3[c] : job->side));
   job->pending[c] = true;
   job->out_lo[c] = std::min(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh));
   job->out_hi[c] = std::max(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh)) +
@@ -1518,8 +1546,10 @@ int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t
     return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events / stream"));
   for (int c = 0; c < 2; ++c)
     if (hipEventCreateWithFlags(&job->front_ev[c], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&job->side_ev[c], hipEventDisableTiming) != hipSuccess)
-      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
+        hipEventCreateWithFlags(&job->side_ev[c], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&job->mid_ev[c], hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&job->t3[c], hipStreamNonBlocking) != hipSuccess)
+      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events / streams"));
   rc = whatif_base(job);
   if (rc) return bail(rc);
   *out = job;
@@ -1613,6 +1643,21 @@ int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out) {
   return ORH_OK;
 }
 
+int orh_whatif_set_flags(orh_whatif* job, uint32_t flags) {
+  if (!job) return ORH_E_INVALID;
+  if (flags & ~ORH_WHATIF_SHARE_BASE) return fail(job->g->ctx, ORH_E_INVALID, "orh_whatif_set_flags: unknown flag");
+  job->flags = flags;
+  return ORH_OK;
+}
+
+int orh_whatif_base_rows(orh_whatif* job, const uint32_t** d_dist, const uint32_t** d_nh) {
+  if (!job || !d_dist || !d_nh) return ORH_E_INVALID;
+  const size_t nd = job->srcs.size() * static_cast<size_t>(job->g->n_nodes);
+  *d_dist = job->d_base;
+  *d_nh = job->d_base + nd;
+  return ORH_OK;
+}
+
 int orh_whatif_destroy(orh_whatif* job) {
   if (!job) return ORH_E_INVALID;
   // queued kernels may still read the job's buffers: drain both streams
@@ -1620,8 +1665,13 @@ int orh_whatif_destroy(orh_whatif* job) {
     whatif_flush(job);
     hipStreamSynchronize(job->side);
   }
+  for (int c = 0; c < 2; ++c)
+    if (job->t3[c]) hipStreamSynchronize(job->t3[c]);
   hipStreamSynchronize(job->g->ctx->stream);
   for (int c = 0; c < 2; ++c) {
+    hipFree(job->t3_slots[c]);
+    if (job->t3[c]) hipStreamDestroy(job->t3[c]);
+    if (job->mid_ev[c]) hipEventDestroy(job->mid_ev[c]);
     hipFree(job->d_work[c]);
     if (job->front_ev[c]) hipEventDestroy(job->front_ev[c]);
     if (job->side_ev[c]) hipEventDestroy(job->side_ev[c]);

@@ -271,3 +271,34 @@ def test_c4_bench_batch_vs_oracle(hip, oracle):
             changed = int(np.sum((d != dist_o[idx[i]]) | (m != nh_o[idx[i]])))
             assert changed <= affected[i], (i, changed, affected[i])
     assert affected[top[0]] > 100  # the largest sets leave the small LDS tier
+
+
+def test_c4_shared_base_rows(hip):
+    """ORH_WHATIF_SHARE_BASE on the C4 job: the same tiers and affected
+    counts, and every sampled request's row (repaired rows from the row
+    buffer, source rows from the job's base rows) equals the dense job's."""
+    from openr_amd.workloads import C4_WHATIF_CHUNK, c4_wan, c4_what_if_job
+    adj, _ = c4_wan()
+    als_h, _ = load_topology(hip, adj, [])
+    ls = als_h[A]._impl
+    names = ls.node_names()
+    links = ls.link_ids()
+    srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
+    rows = {}
+    infos = {}
+    for share in (False, True):
+        b = ls.what_if_batch(srcs, idx, sets, C4_WHATIF_CHUNK, share_base=share)
+        b.run()
+        b.sync()
+        infos[share] = b.info()
+        last = len(idx) - C4_WHATIF_CHUNK
+        rng = random.Random(7)
+        tier = infos[share] & 7
+        pick = (rng.sample([i for i in range(last, len(idx)) if tier[i] == 0], 12) +
+                rng.sample([i for i in range(last, len(idx)) if tier[i] != 0], 12))
+        rows[share] = {i: b.fetch(i) for i in pick}
+        del b
+    assert np.array_equal(infos[False], infos[True])
+    for i, (d, m) in rows[False].items():
+        np.testing.assert_array_equal(rows[True][i][0], d, err_msg=f"request {i} dist")
+        np.testing.assert_array_equal(rows[True][i][1], m, err_msg=f"request {i} nh")
