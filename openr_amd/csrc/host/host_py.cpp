@@ -430,18 +430,14 @@ class WhatIfBatch {
     graph_ = ls.deviceGraph();
     ctx_ = ls.context();
     orh_graph_info(graph_, &n_, &edges_);
-    // two row buffers, alternating between chunks, so a chunk's large repairs
-    // overlap the next chunk's copy and small repairs
+    // up to three row buffers, cycled between chunks, so a chunk's repairs
+    // (which write into its rows) overlap the next two chunks' copies
     const size_t rows = static_cast<size_t>(chunk_) * n_;
-    nBuf_ = chunks_.size() > 1 ? 2 : 1;
+    nBuf_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(chunks_.size(), kBufs)));
     for (int b = 0; b < nBuf_; ++b)
       if (orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dDist_[b])) != ORH_OK ||
           orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dNh_[b])) != ORH_OK)
         throw std::runtime_error("WhatIfBatch: device allocation failed");
-    if (nBuf_ == 1) {
-      dDist_[1] = dDist_[0];
-      dNh_[1] = dNh_[0];
-    }
     if (orh_device_alloc(ctx_, std::max<size_t>(n, 1) * 4, reinterpret_cast<void**>(&dInfo_)) != ORH_OK)
       throw std::runtime_error("WhatIfBatch: device allocation failed");
   }
@@ -465,7 +461,7 @@ class WhatIfBatch {
     }
     for (const auto& c : chunks_) {
       const uint32_t nr = static_cast<uint32_t>(c.hi - c.lo);
-      const int b = static_cast<int>((&c - chunks_.data()) & 1);  // alternate row buffers
+      const int b = static_cast<int>((&c - chunks_.data()) % nBuf_);  // cycle the row buffers
       if (orh_whatif_run(job_, nr, srcIdx_.data() + c.lo, c.ptr.data(), c.links.data(), dDist_[b], dNh_[b],
                          dInfo_ + c.lo) != ORH_OK)
         throw std::runtime_error(std::string("orh_whatif_run: ") + orh_last_error(ctx_));
@@ -491,7 +487,7 @@ class WhatIfBatch {
     const auto& last = chunks_.back();
     if (i < last.lo || i >= last.hi) throw std::out_of_range("WhatIfBatch.fetch: not in the last chunk");
     const size_t r = i - last.lo;
-    const int b = static_cast<int>((chunks_.size() - 1) & 1);
+    const int b = static_cast<int>((chunks_.size() - 1) % nBuf_);
     const uint32_t* d = dDist_[b] + r * n_;
     const uint32_t* m = dNh_[b] + r * n_;
     if (shareBase_) {  // a request whose source row stands reads the job's base row
@@ -528,9 +524,10 @@ class WhatIfBatch {
   orh_ctx* ctx_{nullptr};
   orh_whatif* job_{nullptr};
   uint32_t n_{0}, edges_{0};
+  static constexpr size_t kBufs = 3;
   int nBuf_{1};
-  uint32_t* dDist_[2] = {nullptr, nullptr};
-  uint32_t* dNh_[2] = {nullptr, nullptr};
+  uint32_t* dDist_[kBufs] = {};
+  uint32_t* dNh_[kBufs] = {};
   uint32_t* dInfo_{nullptr};
 };
 

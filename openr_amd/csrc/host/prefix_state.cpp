@@ -134,24 +134,6 @@ orh_adv PrefixState::advRecord(const NodeAndArea& na, const PrefixEntry& e) cons
   return orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference, e.distance};
 }
 
-// pid's advertisements appended to the host pool (the numbering the device
-// reports best positions in) and as device records
-void PrefixState::buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const {
-  advLive_ -= run_[pid].second;
-  run_[pid] = {static_cast<uint32_t>(advPool_.size()), 0u};
-  *flags = 0;
-  if (!live_[pid]) return;
-  auto it = prefixes_.find(cidrOf_[pid]);
-  if (it == prefixes_.end()) return;
-  *flags = it->first.first.size() == 4 ? ORH_PFX_V4 : 0;
-  for (const auto& [na, e] : it->second) {
-    advPool_.push_back(AdvRef{&na, &e});
-    out.push_back(advRecord(na, e));
-  }
-  run_[pid].second = static_cast<uint32_t>(advPool_.size()) - run_[pid].first;
-  advLive_ += run_[pid].second;
-}
-
 orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
   if (areas_.size() > ORH_ADV_AREA_MASK + 1)
     throw std::runtime_error("PrefixState: more than 256 areas for the device mirror");
@@ -214,13 +196,51 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
     devFull_ = false;
   } else if (!dirty_.empty()) {
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<orh_adv> recs;
-    std::vector<uint32_t> ptr(1, 0);
-    std::vector<uint8_t> fl(dirty_.size(), 0);
-    for (size_t i = 0; i < dirty_.size(); ++i) {
-      buildRun(dirty_[i], recs, &fl[i]);
-      ptr.push_back(static_cast<uint32_t>(recs.size()));
+    // the dirty prefixes' runs appended to the host pool in dirty order (the
+    // numbering the device delta uses): counts, offsets, then the records,
+    // on the worker pool for large deltas
+    const size_t nd = dirty_.size();
+    std::vector<const PrefixEntries*> ents(nd, nullptr);
+    std::vector<uint32_t> ptr(nd + 1, 0);
+    std::vector<uint8_t> fl(nd, 0);
+    auto& pool = WorkerPool::instance();
+    auto each = [&](auto&& fn) {
+      if (nd >= 4096 && pool.size() > 1) {
+        pool.parallelFor(nd, [&](size_t, size_t b, size_t e) {
+          for (size_t i = b; i < e; ++i) fn(i);
+        });
+      } else {
+        for (size_t i = 0; i < nd; ++i) fn(i);
+      }
+    };
+    each([&](size_t i) {
+      const uint32_t pid = dirty_[i];
+      if (!live_[pid]) return;
+      auto it = prefixes_.find(cidrOf_[pid]);
+      if (it == prefixes_.end()) return;
+      ents[i] = &it->second;
+      ptr[i + 1] = static_cast<uint32_t>(it->second.size());
+      fl[i] = it->first.first.size() == 4 ? ORH_PFX_V4 : 0;
+    });
+    for (size_t i = 0; i < nd; ++i) {
+      advLive_ -= run_[dirty_[i]].second;
+      ptr[i + 1] += ptr[i];
     }
+    advLive_ += ptr[nd];
+    const uint32_t base = static_cast<uint32_t>(advPool_.size());
+    advPool_.resize(base + ptr[nd]);
+    std::vector<orh_adv> recs(ptr[nd]);
+    each([&](size_t i) {
+      const uint32_t pid = dirty_[i];
+      run_[pid] = {base + ptr[i], ptr[i + 1] - ptr[i]};
+      if (!ents[i]) return;
+      uint32_t k = ptr[i];
+      for (const auto& [na, e] : *ents[i]) {
+        advPool_[base + k] = AdvRef{&na, &e};
+        recs[k] = advRecord(na, e);
+        ++k;
+      }
+    });
     const auto t1 = std::chrono::steady_clock::now();
     check(ctx, orh_prefix_apply_delta(dev_, static_cast<uint32_t>(dirty_.size()), dirty_.data(),
                                       ptr.data(), recs.data(), fl.data()),

@@ -89,7 +89,6 @@ class PrefixState {
   void touch(const Cidr& prefix, bool erased);
   uint32_t internName(const std::string& n);
   uint32_t internArea(const std::string& a);
-  void buildRun(uint32_t pid, std::vector<orh_adv>& out, uint8_t* flags) const;
   orh_adv advRecord(const NodeAndArea& na, const PrefixEntry& e) const;
 
   std::unordered_map<Cidr, PrefixEntries, CidrHash> prefixes_;

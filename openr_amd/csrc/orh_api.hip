@@ -1128,6 +1128,10 @@ static bool repair_eligible(orh_graph* g, const orh_spf_request* req, uint32_t w
 
 // A what-if job (include/openr_hip.h): the plain rows of its sources, then
 // any number of request batches repaired from them
+// run slots a job cycles through: run r + kRunSlots reuses run r's queues,
+// staging and slot memory (and waits for its side part)
+constexpr int kRunSlots = 3;
+
 struct orh_whatif {
   orh_graph* g = nullptr;
   uint64_t gen = 0;  // graph structure the base rows belong to
@@ -1137,22 +1141,22 @@ struct orh_whatif {
   std::vector<uint32_t> srcs;
   uint32_t* d_base = nullptr;  // dist rows [m][N], then mask rows [m][N]
   size_t base_cap = 0;         // bytes
-  // runs alternate between two slots, each with its request staging (pinned
+  // runs cycle through kRunSlots slots, each with its request staging (pinned
   // host + device), its work queues / counters / fallback flags, and the
-  // side-stream part of its last run: the few large repairs (tiers 2, 3) of
-  // run r run on `side` while run r + 1's seed / copy / tier 1 run on the
-  // context stream
+  // side-stream part of its last run: the repair tiers of run r run on
+  // `side` (and t3[slot]) while run r + 1's seed / copy run on the context
+  // stream
   hipStream_t side = nullptr;
-  uint32_t* h_stage[2] = {nullptr, nullptr};
-  uint32_t* d_stage[2] = {nullptr, nullptr};
-  size_t stage_cap[2] = {0, 0};  // u32, both sides
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};  // upload done
-  uint32_t* d_work[2] = {nullptr, nullptr};     // queues [3][n] | counters | fallback flags [n]
-  size_t work_cap[2] = {0, 0};
-  hipEvent_t front_ev[2] = {nullptr, nullptr};  // context-stream part done
-  hipEvent_t side_ev[2] = {nullptr, nullptr};   // side-stream part done
-  bool pending[2] = {false, false};             // side part not yet joined into the context stream
-  uintptr_t out_lo[2] = {0, 0}, out_hi[2] = {0, 0};  // output span of that run (hazard checks)
+  uint32_t* h_stage[kRunSlots] = {};
+  uint32_t* d_stage[kRunSlots] = {};
+  size_t stage_cap[kRunSlots] = {};  // u32, both sides
+  hipEvent_t stage_ev[kRunSlots] = {};  // upload done
+  uint32_t* d_work[kRunSlots] = {};     // queues [3][n] | counters | fallback flags [n]
+  size_t work_cap[kRunSlots] = {};
+  hipEvent_t front_ev[kRunSlots] = {};  // context-stream part done
+  hipEvent_t side_ev[kRunSlots] = {};   // side-stream part done
+  bool pending[kRunSlots] = {};             // side part not yet joined into the context stream
+  uintptr_t out_lo[kRunSlots] = {}, out_hi[kRunSlots] = {};  // output span of that run (hazard checks)
   int cur = 0;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;  // create .. last flush
   uint64_t requests = 0;
@@ -1164,13 +1168,18 @@ struct orh_whatif {
   void* d_full_lab = nullptr;
   size_t full_lab_cap = 0;
   uint32_t flags = 0;  // ORH_WHATIF_* job flags
-  // the slot tier of run slot c on its own stream t3[c], with its own slot
-  // memory, after event mid_ev[c] (tiers 1 and 2 done on `side`): the next
-  // run's small tiers start without waiting for this run's largest repairs
-  hipStream_t t3[2] = {nullptr, nullptr};
-  hipEvent_t mid_ev[2] = {nullptr, nullptr};
-  uint8_t* t3_slots[2] = {nullptr, nullptr};
-  size_t t3_slots_cap[2] = {0, 0};
+  // the slot tier of a run on a stream of its own (t3[run % kT3]), with its
+  // slot's memory, after event mid_ev[slot] (tiers 1 and 2 done on `side`):
+  // the next run's small tiers start without waiting for its largest repairs
+  // two streams, by run parity: with the context stream and `side` that is
+  // HIP's 4 hardware queues (GPU_MAX_HW_QUEUES); a fifth stream would share
+  // a queue with `side` and hold its next tiers behind a slot tier
+  static constexpr int kT3 = 2;
+  hipStream_t t3[kT3] = {};
+  uint64_t runs = 0;
+  hipEvent_t mid_ev[kRunSlots] = {};
+  uint8_t* t3_slots[kRunSlots] = {};
+  size_t t3_slots_cap[kRunSlots] = {};
 };
 
 namespace {
@@ -1224,7 +1233,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
     const uintptr_t lo = std::min(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh));
     const uintptr_t hi = std::max(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh)) +
                          size_t{n_req} * N * 4;
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kRunSlots; ++k)
       if (job->pending[k] && (k == c || (lo < job->out_hi[k] && job->out_lo[k] < hi))) {
         ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[k], 0));
         job->pending[k] = false;
@@ -1262,7 +1271,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
     hc[i + 1] = static_cast<uint32_t>(nc);
   }
   const int c = job->cur;
-  job->cur ^= 1;
+  job->cur = (job->cur + 1) % kRunSlots;
   ORH_HIP(ctx, hipMemcpyAsync(d, h, words * 4, hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipEventRecord(job->stage_ev[c], ctx->stream));
 
@@ -1294,7 +1303,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   if (split) {
     // run slot c's own slot memory, grown only with its stream idle
     if (n_slots * slot_bytes > job->t3_slots_cap[c]) {
-      ORH_HIP(ctx, hipStreamSynchronize(job->t3[c]));
+      for (hipStream_t t : job->t3) ORH_HIP(ctx, hipStreamSynchronize(t));
       hipFree(job->t3_slots[c]);
       job->t3_slots[c] = nullptr;
       job->t3_slots_cap[c] = 0;
@@ -1370,7 +1379,9 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   // the large repairs on the side stream, after this run's front part; the
   // previous side part is ordered before them on that stream
   ORH_HIP(ctx, hipStreamWaitEvent(job->side, job->front_ev[c], 0));
-  e = split ? orh::launch_repair_back_split(ra, g->ell_k, ctx->lds_limit, job->side, job->t3[c], job->mid_ev[c])
+  hipStream_t t3s = job->t3[job->runs % orh_whatif::kT3];
+  ++job->runs;
+  e = split ? orh::launch_repair_back_split(ra, g->ell_k, ctx->lds_limit, job->side, t3s, job->mid_ev[c])
             : orh::launch_repair_back(ra, g->ell_k, ctx->lds_limit, job->side);
   if (e != hipSuccess) return hip_fail(ctx, e, "what-if repair launch (large tiers)");
   if (n_slots && ra.full_cap) {
@@ -1441,7 +1452,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   }
   // the run's side part ends with its slot tier (t3[c], ordered after tiers
   // 1 and 2 through mid_ev[c]) or on `side`
-  ORH_HIP(ctx, hipEventRecord(job->side_ev[c], split ? job->t3[c] : job->side));
+  ORH_HIP(ctx, hipEventRecord(job->side_ev[c], split ? t3s : job->side));
   job->pending[c] = true;
   job->out_lo[c] = std::min(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh));
   job->out_hi[c] = std::max(reinterpret_cast<uintptr_t>(d_dist), reinterpret_cast<uintptr_t>(d_nh)) +
@@ -1457,7 +1468,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
 // queued on it afterwards sees all of the job's rows
 int whatif_flush(orh_whatif* job) {
   orh_ctx* ctx = job->g->ctx;
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < kRunSlots; ++c)
     if (job->pending[c]) {
       ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[c], 0));
       job->pending[c] = false;
@@ -1484,7 +1495,7 @@ int whatif_base(orh_whatif* job) {
   job->bound = bound;
   rc = ensure_rev(g);
   if (rc) return rc;
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < kRunSlots; ++c)
     if (job->pending[c]) {
       ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, job->side_ev[c], 0));
       job->pending[c] = false;
@@ -1544,12 +1555,14 @@ int whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int32_t
   if (hipEventCreate(&job->ev_begin) != hipSuccess || hipEventCreate(&job->ev_end) != hipSuccess ||
       hipStreamCreateWithFlags(&job->side, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events / stream"));
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < kRunSlots; ++c)
     if (hipEventCreateWithFlags(&job->front_ev[c], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&job->side_ev[c], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&job->mid_ev[c], hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&job->t3[c], hipStreamNonBlocking) != hipSuccess)
-      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events / streams"));
+        hipEventCreateWithFlags(&job->mid_ev[c], hipEventDisableTiming) != hipSuccess)
+      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: events"));
+  for (hipStream_t& t : job->t3)
+    if (hipStreamCreateWithFlags(&t, hipStreamNonBlocking) != hipSuccess)
+      return bail(fail(ctx, ORH_E_DEVICE, "orh_whatif_create: streams"));
   rc = whatif_base(job);
   if (rc) return bail(rc);
   *out = job;
@@ -1665,12 +1678,13 @@ int orh_whatif_destroy(orh_whatif* job) {
     whatif_flush(job);
     hipStreamSynchronize(job->side);
   }
-  for (int c = 0; c < 2; ++c)
-    if (job->t3[c]) hipStreamSynchronize(job->t3[c]);
+  for (hipStream_t t : job->t3)
+    if (t) hipStreamSynchronize(t);
   hipStreamSynchronize(job->g->ctx->stream);
-  for (int c = 0; c < 2; ++c) {
+  for (hipStream_t t : job->t3)
+    if (t) hipStreamDestroy(t);
+  for (int c = 0; c < kRunSlots; ++c) {
     hipFree(job->t3_slots[c]);
-    if (job->t3[c]) hipStreamDestroy(job->t3[c]);
     if (job->mid_ev[c]) hipEventDestroy(job->mid_ev[c]);
     hipFree(job->d_work[c]);
     if (job->front_ev[c]) hipEventDestroy(job->front_ev[c]);
