@@ -88,6 +88,8 @@ struct orh_graph {
   uint32_t n_nodes = 0, n_edges = 0, n_links = 0;
   // host CSR (ABI semantics) kept for deltas, neighbour tables and bounds
   std::vector<uint32_t> row_ptr, col, w_out, w_in, meta;
+  std::vector<uint32_t> ent_row;  // entry -> row (entry_rows), valid for ent_row_gen
+  uint64_t ent_row_gen = ~0ull;
   std::vector<uint8_t> overloaded;
   std::vector<uint32_t> dn_ptr, dn;  // distinct neighbours per node, ascending id
   std::vector<uint16_t> rank_out;    // per CSR entry: col's rank among row's distinct neighbours
@@ -394,6 +396,19 @@ int upload_records(orh_graph* g, const std::vector<std::pair<uint32_t, uint32_t>
 uint32_t row_of(const orh_graph* g, uint32_t e) {
   return static_cast<uint32_t>(std::upper_bound(g->row_ptr.begin(), g->row_ptr.end(), e) -
                                g->row_ptr.begin()) - 1;
+}
+
+// row of every CSR entry, rebuilt when the structure generation moves (a
+// what-if run stages two cuts per ignored link: 131k binary searches over
+// row_ptr per 65,536-request C4 chunk otherwise)
+const std::vector<uint32_t>& entry_rows(orh_graph* g) {
+  if (g->ent_row_gen != g->gen || g->ent_row.size() != g->n_edges) {
+    g->ent_row.assign(g->n_edges, 0u);
+    for (uint32_t v = 0; v < g->n_nodes; ++v)
+      for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e) g->ent_row[e] = v;
+    g->ent_row_gen = g->gen;
+  }
+  return g->ent_row;
 }
 
 void recompute_bounds(orh_graph* g) {
@@ -1248,6 +1263,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   uint32_t* hi = h + off_ign;
   uint32_t* hc = h + off_cp;
   uint4* cuts = reinterpret_cast<uint4*>(h + off_cuts);
+  const std::vector<uint32_t>& erow = entry_rows(g);
   size_t ni = 0, nc = 0;
   hp[0] = 0;
   hc[0] = 0;
@@ -1263,7 +1279,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
       for (int e2 = 0; e2 < 2; ++e2) {
         const uint32_t e = g->link_ent[2 * static_cast<size_t>(l) + e2];
         if (e == ~0u) continue;
-        cuts[nc++] = make_uint4(row_of(g, e), g->col[e], g->pos[e], 0u);
+        cuts[nc++] = make_uint4(erow[e], g->col[e], g->pos[e], 0u);
       }
     }
     ni += len;
