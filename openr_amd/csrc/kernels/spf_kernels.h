@@ -93,9 +93,6 @@ struct HopArgs {
   // logical blocks (sources x tile phases); a grid smaller than this runs
   // persistent workgroups, each striding through its XCD's logical range
   uint32_t n_logical;
-  // 16-node rows leave as four 16-byte stores per thread: nontemporal (1) or
-  // through L2, which merges each wave's four partial 64-byte segments (0)
-  uint32_t nt_store;
 };
 
 enum class SpfVariant {

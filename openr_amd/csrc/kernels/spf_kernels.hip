@@ -1963,15 +1963,10 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
       if (kLvlPer == 16 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
-        if (a.nt_store) {
 #pragma unroll
-          for (uint32_t q = 0; q < kLvlPer / 4; ++q) {
-            const u32x4 x = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
-            __builtin_nontemporal_store(x, &o[q]);
-          }
-        } else {
-#pragma unroll
-          for (uint32_t q = 0; q < kLvlPer / 4; ++q) o[q] = u32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+        for (uint32_t q = 0; q < kLvlPer / 4; ++q) {
+          const u32x4 x = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+          __builtin_nontemporal_store(x, &o[q]);
         }
       } else {
 #pragma unroll
@@ -2268,11 +2263,6 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
     uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
     if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     a.n_logical = static_cast<uint32_t>(g2);
-    static const uint32_t nt = [] {  // ORH_HOP_NT=0: first-hop rows through L2 (A/B)
-      const char* e = getenv("ORH_HOP_NT");
-      return e ? static_cast<uint32_t>(atoi(e) != 0) : 1u;
-    }();
-    a.nt_store = nt;
     // ORH_HOP_WG_PER_CU (A/B, default 0 = one workgroup per logical block):
     // persistent workgroups, that many per CU, for even per-source work. C2
     // sweep, first hops: 0.362 ms one per block, 0.389 ms at 8 per CU, 0.439
