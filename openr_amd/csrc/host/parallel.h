@@ -32,8 +32,10 @@ class WorkerPool {
 
   // fn(worker, begin, end) over [0, n) in size() contiguous chunks; the first
   // exception (if any) is rethrown on the caller
-  void parallelFor(size_t n, const std::function<void(size_t, size_t, size_t)>& fn) {
-    const size_t parts = std::min(size(), std::max<size_t>(n, 1));
+  // chunks > 0: that many chunks (claimed dynamically by the threads; for
+  // uneven per-item cost), fn's first argument then ranges over them
+  void parallelFor(size_t n, const std::function<void(size_t, size_t, size_t)>& fn, size_t chunks = 0) {
+    const size_t parts = std::min(chunks ? chunks : size(), std::max<size_t>(n, 1));
     if (parts <= 1 || inJob_) {
       fn(0, 0, n);
       return;

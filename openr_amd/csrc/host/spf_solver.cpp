@@ -1388,7 +1388,10 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
   };
-  std::vector<Part> parts(pool.size());
+  // chunks claimed dynamically: host-path prefixes (BGP, SR-MPLS, ...) cost
+  // far more than materialised ones and cluster by prefix id
+  const size_t nChunks = std::min<size_t>(8 * pool.size(), std::max<size_t>(todo.size() + deleted.size(), 1));
+  std::vector<Part> parts(nChunks);
   // the new route of one prefix (createRouteForPrefixOrGetStaticRoute, then
   // the policy), compared with current's entry (calculateUpdate)
   auto one = [&](const Cidr& prefix, std::optional<RibUnicastEntry> r, Part& out) {
@@ -1414,10 +1417,18 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
       out.tPush += ms(t4, t5);
     }
   };
-  pool.parallelFor(todo.size(), [&](size_t w, size_t b, size_t e) {
+  // items: the prefix ids to rebuild, then the withdrawn prefixes (their
+  // routes go, or fall back to a static route, unless a live id carries them)
+  const size_t nItems = todo.size() + deleted.size();
+  pool.parallelFor(nItems, [&](size_t w, size_t b, size_t e) {
     const double c0 = prof.on ? cpuMs() : 0.0;
     parts[w].upd.reserve(parts[w].upd.size() + (e - b));  // no regrowth (and its page faults) per route
     for (size_t i = b; i < e; ++i) {
+      if (i >= todo.size()) {
+        const Cidr& c = deleted[i - todo.size()];
+        if (!ps.pidOf(c)) one(c, std::nullopt, parts[w]);
+        continue;
+      }
       const uint32_t pid = todo[i];
       const Cidr& prefix = ps.prefixOf(pid);
       const auto t0 = prof.on ? Clock::now() : Clock::time_point{};
@@ -1431,11 +1442,7 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
       one(prefix, std::move(r), parts[w]);
     }
     if (prof.on) parts[w].tCpu += cpuMs() - c0;
-  });
-  // withdrawn prefixes that no live id carries now: their routes go (or
-  // fall back to a static route)
-  for (const Cidr& c : deleted)
-    if (!ps.pidOf(c)) one(c, std::nullopt, parts[0]);
+  }, nChunks);
   if (prof.on) {
     double b = 0, pl = 0, f = 0, c = 0, pu = 0, cpu = 0;
     size_t nn = 0, busy = 0;
