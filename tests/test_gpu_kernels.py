@@ -92,6 +92,32 @@ def test_modes_grid_sweep_properties(hip, spf_mode):
         assert np.array_equal(dist[ids], np.abs(rr - rr[s]) + np.abs(cc - cc[s])), (spf_mode, s)
 
 
+def test_modes_split_grid_sweep_unreached(hip, oracle, spf_mode):
+    """40x40 grid cut in two between rows 19 and 20, all sources: half of
+    every row is unreachable, so every (node, source) level byte the search
+    never reaches must come out "unreached" (the multi-source search writes
+    those at its end; no pre-filled scratch). Compared with the oracle."""
+    n = 40
+    adj_dbs, _ = bench_grid(n)
+    for db in adj_dbs:
+        row = int(db.thisNodeName) // n
+        db.adjacencies = [a for a in db.adjacencies
+                          if (int(a.otherNodeName) // n >= 20) == (row >= 20)]
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    names = [db.thisNodeName for db in adj_dbs]
+    sweep = als_h[A]._impl.sweep(names, True)
+    sweep.run()
+    sweep.sync()
+    node_names = als_h[A]._impl.node_names()
+    for i in list(range(0, n * n, 11)) + [n * n - 1]:
+        dist, _ = sweep.fetch(i)
+        ref = als_o[A].get_spf_result(names[i])
+        assert len(ref) == n * n // 2
+        got = {node_names[v]: int(d) for v, d in enumerate(dist) if d != 0xFFFFFFFF}
+        assert got == {k: v.metric for k, v in ref.items()}, (spf_mode, names[i])
+
+
 def test_wan_50k_hbm_kernel(hip, oracle):
     """Config C4's 50k-node WAN (log-normal metrics): too large for the
     LDS-resident kernels, so AUTO selects the HBM frontier kernel. Exact
