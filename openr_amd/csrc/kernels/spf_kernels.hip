@@ -398,12 +398,10 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     s_lo[tid] = ~0u;
     s_hin[tid] = ~0u;
   }
-#ifdef ORH_MS_LVL_INIT  // A/B: every level byte starts as "unreached" (one more scratch pass)
-  {
+  {  // every level byte starts as "unreached"
     uint4* l4 = reinterpret_cast<uint4*>(lvl);
     for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
   }
-#endif
   __syncthreads();
   if (tid < S) {  // sources may repeat: OR the bits in
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
@@ -583,20 +581,6 @@ __global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
     f_cur = f_nxt;
     f_nxt = t;
   }
-#ifndef ORH_MS_LVL_INIT
-  // the scratch is not pre-filled: every (node, source) byte the search never
-  // reached is written "unreached" here, from the bits still clear in vis
-  // (none at all on a connected topology), instead of a fill pass over the
-  // whole [N][kS] block before the search
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const uint32_t v = j * B + tid;
-    if (v < N && vis[j] != full) {
-      uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
-      for (V q = full & ~vis[j]; q; q &= q - 1) lb[MsMask<M>::ctz(q)] = static_cast<uint8_t>(kLvlNone);
-    }
-  }
-#endif
 #ifdef ORH_DIAG_STAMPS
   if (tid == 0 && blockIdx.x < 4096) {  // per workgroup: entry, exit, hardware id, levels
     uint64_t* w = a.diag + 16 + 4 * static_cast<size_t>(blockIdx.x);
