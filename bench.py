@@ -93,6 +93,9 @@ def main():
     if args.rehearse_on_one_gpu:
         local = 0
     os.environ.setdefault("ORH_DEVICE", str(local))  # before the host library opens a context
+    # the deployment's allocator policy (opt-in, process-global: keep freed
+    # route-DB pages in glibc's arenas)
+    os.environ.setdefault("ORH_MALLOC_TUNE", "1")
     import torch
     import torch.distributed as dist
 

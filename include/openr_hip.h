@@ -355,6 +355,11 @@ typedef struct orh_adv {
 #define ORH_ADV_BGP (1u << 10)        /* type == BGP */
 #define ORH_ADV_MIN_NEXTHOP (1u << 11) /* minNexthop is set */
 #define ORH_ADV_PREPEND (1u << 12)    /* prependLabel is set */
+/* bits 13-31 of meta: the caller's id of the advertisement's PrefixEntry.tags
+ * set (0: no tags; ORH_ADV_TAGSET_OVF: more distinct sets than ids, which
+ * sends a policy-matched route to the host, orh_route_policy) */
+#define ORH_ADV_TAGSET_SHIFT 13u
+#define ORH_ADV_TAGSET_OVF 0x7FFFFu
 #define ORH_PFX_V4 1u                 /* prefix_flags: an IPv4 prefix */
 
 int orh_prefix_create(orh_ctx* ctx, orh_prefix_set** out);
@@ -427,6 +432,41 @@ int orh_route_diff(orh_prefix_set* ps, uint32_t n_prefix, uint32_t prev_n, const
                    const orh_select_out* prev, uint32_t* d_changed, uint32_t* d_count);
 /* device time of the last orh_route_select kernel (HIP events; waits for it) */
 int orh_last_select_ms(orh_prefix_set* ps, double* ms_out);
+
+/* ---- RibPolicy over a route selection (RibPolicy::applyPolicy) --------- */
+/* Replaces the per-route loop of RibPolicy::applyPolicy (RibPolicy.cpp
+ * :229-247) with RibPolicyStatement::match / applyAction (:73-158) for the
+ * routes a selection made (status ORH_SEL_ROUTE). A route's nexthops are the
+ * tight links behind the set bits of its first-hop mask, and a set_weight
+ * action gives every nexthop of one bit (one neighbour, one area) the same
+ * weight, so statement s is a bitmask keep[s] of the mask bits whose weight
+ * is > 0 (neighbour weight, else area weight, else default weight). Per
+ * route, the statements in order: s matches when every non-empty matcher
+ * matches (tags: the best advertisement's tag set meets s's tag set; prefixes:
+ * the route's prefix id is in s's list) and at least one is non-empty; a
+ * matching s whose keep[s] misses the route's mask drops every nexthop, so the
+ * route stays as it was and counts as invalidated (:146-152), and the next
+ * statement is tried; the first matching s that keeps a nexthop applies.
+ * out[p] = that s, ORH_POL_NONE, or ORH_POL_HOST (tag set id overflow: the
+ * host applies the policy). *d_invalidated receives the invalidated count.
+ * Asynchronous on the context stream; the tables are copied. */
+#define ORH_POL_NONE 0xFFu
+#define ORH_POL_HOST 0xFEu
+#define ORH_POL_MAX_STMTS 32u
+typedef struct orh_policy {
+  uint32_t n_stmts;                /* <= ORH_POL_MAX_STMTS */
+  uint32_t stmt_tags;              /* bit s: statement s has a non-empty tag matcher */
+  uint32_t stmt_prefixes;          /* bit s: statement s has a non-empty prefix matcher */
+  uint32_t n_tagsets;              /* tag set ids 0 .. n_tagsets - 1 */
+  const uint32_t* h_tagset_stmts;  /* [n_tagsets] bit s: the set meets statement s's tags */
+  uint32_t n_pfx;                  /* prefixes named by any prefix matcher */
+  const uint32_t* h_pfx_id;        /* [n_pfx] prefix ids, ascending */
+  const uint32_t* h_pfx_stmts;     /* [n_pfx] bit s: statement s names the prefix */
+  const uint32_t* h_keep;          /* [n_stmts][total_words] */
+  uint32_t total_words;            /* the selection's mask words */
+} orh_policy;
+int orh_route_policy(orh_prefix_set* ps, uint32_t n_prefix, const orh_select_out* sel,
+                     const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated);
 
 #ifdef __cplusplus
 }

@@ -256,16 +256,19 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
     // the reference's whole rebuild (Decision.cpp:1888-1900)
     std::optional<DecisionRouteUpdate> delta;
     const bool policyActive = policy && policy->isActive();
-    if (solver_ == &solver && ps_ == &ps && policy_ == policy && policyActive_ == policyActive &&
-        staticEpoch_ == solver.staticEpoch() && selGen_ != 0 && !std::getenv("ORH_WHOLE_REBUILD"))
+    // selGen_ is unique to one solver's snapshot, so it also names the solver
+    const uint64_t policyId = policy ? policy->generation() : 0;
+    if (selGen_ != 0 && selGen_ == solver.selGen() && psId_ == ps.id() && policyId_ == policyId &&
+        policyActive_ == policyActive && staticEpoch_ == solver.staticEpoch() &&
+        !std::getenv("ORH_WHOLE_REBUILD"))
       delta = solver.buildRouteDelta(me, als, ps, routeDb_, selGen_, psStamp_, policy);
     if (delta) {
       update = std::move(*delta);
       ++deltaRebuilds_;
       routeDb_.update(update);
     } else {
-      DecisionRouteDb db = solver.buildRouteDb(me, als, ps).value_or(DecisionRouteDb{});
-      if (policy) policy->applyPolicy(db.unicastRoutes);
+      // buildRouteDb + RibPolicy::applyPolicy (the policy decided on the device)
+      DecisionRouteDb db = solver.buildRouteDbWithPolicy(me, als, ps, policy).value_or(DecisionRouteDb{});
       update = routeDb_.calculateUpdate(db);
       // routeDb_.update(update) leaves routeDb_ equal to db: take db itself
       // (no second copy of every changed route; the old maps free in parallel)
@@ -288,12 +291,11 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
     }
     routeDb_.update(update);
   }
-  solver_ = &solver;
-  ps_ = &ps;
   selGen_ = solver.selGen();
+  psId_ = ps.id();
   psStamp_ = ps.stamp();
   staticEpoch_ = solver.staticEpoch();
-  policy_ = policy;
+  policyId_ = policy ? policy->generation() : 0;
   policyActive_ = policy && policy->isActive();
   return update;
 }

@@ -114,12 +114,12 @@ class DecisionRib {
 
  private:
   DecisionRouteDb routeDb_;
-  // what routeDb_ was last made from: the solver and its selection snapshot,
-  // the prefix state's stamp, the policy and its state, the static routes
-  const SpfSolver* solver_{nullptr};
-  const PrefixState* ps_{nullptr};
-  uint64_t selGen_{0}, psStamp_{0}, staticEpoch_{0};
-  const RibPolicy* policy_{nullptr};
+  // what routeDb_ was last made from: the solver's selection snapshot, the
+  // prefix state (instance and stamp), the policy and its state, the static
+  // routes. Every one is a process-unique generation (nextGeneration()), not
+  // an address: an object freed and another allocated in its place cannot
+  // pass for it
+  uint64_t selGen_{0}, psId_{0}, psStamp_{0}, staticEpoch_{0}, policyId_{0};
   bool policyActive_{false};
   uint64_t deltaRebuilds_{0}, wholeRebuilds_{0};
 };

@@ -534,7 +534,7 @@ class WhatIfBatch {
 // ---- canonical route-db digest --------------------------------------------
 // Per route: fields serialised in order (integers little-endian, strings and
 // lists length-prefixed, optionals with a presence byte, nexthops sorted by
-// their serialised bytes; PrefixEntry.tags is not part of it), hashed with
+// their serialised bytes; PrefixEntry.tags, sorted, only when non-empty), hashed with
 // FNV-1a 64. Routes in (prefix bytes, length) order, then labels. Lets a
 // caller compare full-size route databases (C3, C5) without materialising
 // them in Python.
@@ -624,6 +624,10 @@ void writeEntry(DigestWriter& w, const PrefixEntry& e) {
     }
   }
   w.optStr(e.data);
+  if (!e.tags.empty()) {  // (absent for tag-free entries: older digests stand)
+    w.i32(static_cast<int32_t>(e.tags.size()));
+    for (const auto& t : e.tags) w.str(t);
+  }
 }
 
 py::tuple routeDbDigest(const DecisionRouteDb& db) {
@@ -1172,18 +1176,42 @@ PYBIND11_MODULE(_openr_host, m) {
              const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
              return std::make_pair(sec, n);
            })
-      .def("time_build_route_db_with_policy",  // Decision::rebuildRoutes: build, then RibPolicy
+      .def("time_build_route_db_with_policy",  // Decision::rebuildRoutes: build + RibPolicy
            [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
               RibPolicy& policy) {
+             // (seconds, routes, updated, invalidated, routes decided on the
+             // device, device policy ms)
+             SpfSolver::PolicyStats st;
              const auto t0 = std::chrono::steady_clock::now();
-             auto db = s.buildRouteDb(me, als.m, ps);
+             auto db = s.buildRouteDbWithPolicy(me, als.m, ps, &policy, &st);
              const auto t1 = std::chrono::steady_clock::now();
+             return py::make_tuple(std::chrono::duration<double>(t1 - t0).count(),
+                                   db ? db->unicastRoutes.size() : 0, st.updated, st.invalidated,
+                                   st.onDevice, st.deviceMs);
+           })
+      .def("time_host_apply_policy",  // A/B: buildRouteDb, then applyPolicy over the map on the host
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             const auto t0 = std::chrono::steady_clock::now();
              size_t updated = 0;
              if (db) updated = policy.applyPolicy(db->unicastRoutes).updatedRoutes.size();
-             const auto t2 = std::chrono::steady_clock::now();
-             return py::make_tuple(std::chrono::duration<double>(t1 - t0).count(),
-                                   std::chrono::duration<double>(t2 - t1).count(),
-                                   db ? db->unicastRoutes.size() : 0, updated);
+             const auto t1 = std::chrono::steady_clock::now();
+             return py::make_tuple(std::chrono::duration<double>(t1 - t0).count(), updated);
+           })
+      .def("build_route_db_with_policy",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) -> py::object {
+             auto db = s.buildRouteDbWithPolicy(me, als.m, ps, &policy);
+             if (!db) return py::none();
+             return routeDbToWire(*db);
+           })
+      .def("build_route_db_with_policy_digest",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) -> py::object {
+             auto db = s.buildRouteDbWithPolicy(me, als.m, ps, &policy);
+             if (!db) return py::none();
+             return routeDbDigest(*db);
            })
       .def("create_route_for_prefix_or_get_static_route",
            [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,

@@ -10,6 +10,7 @@
 #include "parallel.h"
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <iterator>
 #include <type_traits>
@@ -30,6 +31,13 @@ namespace openr_amd {
 
 using Metric = uint64_t;  // LinkStateMetric (LinkState.h:22)
 using NodeAndArea = std::pair<std::string, std::string>;
+
+// process-unique, increasing generation numbers (never 0): instance ids and
+// change stamps that a cache may record instead of an object's address
+inline uint64_t nextGeneration() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1, std::memory_order_relaxed);
+}
 
 // Raw address bytes (IPv4: 4, IPv6: 16) held inline. A 16-byte std::string
 // is one heap allocation per copy (libstdc++ keeps 15 bytes inline), and a

@@ -120,10 +120,7 @@ bool Link::less(const Link& o) const {
 }
 
 // ---- construction -------------------------------------------------------
-uint64_t LinkState::nextStamp() {
-  static std::atomic<uint64_t> next{1};
-  return next.fetch_add(1, std::memory_order_relaxed);
-}
+uint64_t LinkState::nextStamp() { return nextGeneration(); }
 
 LinkState::LinkState(const std::string& area, orh_ctx* ctx)
     : area_(area), stamp_(nextStamp()), ctx_(ctx ? ctx : defaultContext()) {

@@ -83,10 +83,12 @@ class WorkerPool {
   // again: keep freed memory in the arenas (no trim, 256 MB top pad, mmap
   // only past 32 MB). C3 build 29.7 -> 16.6 ms, C5 first rebuild 467 -> 193
   // ms, delta 39.5 -> 24.6 ms (profiles/r03/p_malloc_ab.txt). The process
-  // keeps its peak heap; ORH_MALLOC_TUNE=0 leaves glibc's defaults.
+  // then keeps its peak heap, and the settings are process-global, so a
+  // library must not impose them: opt-in with ORH_MALLOC_TUNE=1 (the host
+  // application owns its allocator policy; bench.py opts in).
   static void tuneAllocator() {
     const char* e = std::getenv("ORH_MALLOC_TUNE");
-    if (e && std::atoi(e) == 0) return;
+    if (!e || std::atoi(e) != 1) return;
     mallopt(M_TRIM_THRESHOLD, INT_MAX);
     mallopt(M_TOP_PAD, 256 << 20);
     mallopt(M_MMAP_THRESHOLD, 32 << 20);  // glibc's largest accepted value

@@ -38,8 +38,29 @@ std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::
   ksp2Entries_ += e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
   internName(node);
   internArea(area);
+  internTagSet(e.tags);
   touch(key, false);
   return {key};
+}
+
+// distinct PrefixEntry.tags sets get ids (0: no tags) that the device mirror
+// carries per advertisement, so a RibPolicy tag matcher becomes a table
+// lookup per route (orh_route_policy); interned here, on the calling thread,
+// so the device records read the table concurrently
+uint32_t PrefixState::internTagSet(const std::set<std::string>& tags) {
+  if (tags.empty()) return 0;
+  auto [it, inserted] = tagSetIds_.emplace(tags, 0u);
+  if (inserted) {
+    tagSets_.push_back(&it->first);
+    it->second = static_cast<uint32_t>(std::min<size_t>(tagSets_.size(), ORH_ADV_TAGSET_OVF));
+  }
+  return it->second;
+}
+
+uint32_t PrefixState::tagSetId(const std::set<std::string>& tags) const {
+  if (tags.empty()) return 0;
+  auto it = tagSetIds_.find(tags);
+  return it == tagSetIds_.end() ? ORH_ADV_TAGSET_OVF : it->second;
 }
 
 std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::string& area,
@@ -84,7 +105,7 @@ std::optional<uint32_t> PrefixState::areaId(const std::string& a) const {
 // id when its last advertisement is withdrawn) and queue it for upload
 void PrefixState::touch(const Cidr& prefix, bool erased) {
   uint32_t pid;
-  ++stamp_;
+  stamp_ = nextGeneration();
   auto it = pid_.find(prefix);
   if (it != pid_.end()) {
     pid = it->second;
@@ -131,6 +152,7 @@ orh_adv PrefixState::advRecord(const NodeAndArea& na, const PrefixEntry& e) cons
   if (e.type == kPrefixTypeBgp) meta |= ORH_ADV_BGP;
   if (e.minNexthop) meta |= ORH_ADV_MIN_NEXTHOP;
   if (e.prependLabel) meta |= ORH_ADV_PREPEND;
+  meta |= tagSetId(e.tags) << ORH_ADV_TAGSET_SHIFT;
   return orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference, e.distance};
 }
 

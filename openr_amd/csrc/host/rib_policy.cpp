@@ -35,21 +35,24 @@ bool RibPolicyStatement::match(const RibUnicastEntry& route) const {  // RibPoli
   return tagMatch && prefixMatch;
 }
 
+int32_t RibPolicyStatement::weightOf(const std::optional<std::string>& area,
+                                     const std::optional<std::string>& neighbor) const {
+  // precedence: neighbour weight, then area weight, then default weight
+  int32_t w = action_.defaultWeight;
+  if (area) {
+    auto it = action_.areaToWeight.find(*area);
+    if (it != action_.areaToWeight.end()) w = it->second;
+  }
+  if (neighbor) {
+    auto it = action_.neighborToWeight.find(*neighbor);
+    if (it != action_.neighborToWeight.end()) w = it->second;
+  }
+  return w;
+}
+
 bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidated) const {
   if (!match(route)) return false;  // RibPolicy.cpp:108-161
-  // precedence: neighbour weight, then area weight, then default weight
-  auto weightOf = [&](const NextHopThrift& nh) {
-    int32_t w = action_.defaultWeight;
-    if (nh.area) {
-      auto it = action_.areaToWeight.find(*nh.area);
-      if (it != action_.areaToWeight.end()) w = it->second;
-    }
-    if (nh.neighborNodeName) {
-      auto it = action_.neighborToWeight.find(*nh.neighborNodeName);
-      if (it != action_.neighborToWeight.end()) w = it->second;
-    }
-    return w;
-  };
+  auto weightOf = [&](const NextHopThrift& nh) { return this->weightOf(nh.area, nh.neighborNodeName); };
   bool any = false;
   for (const auto& nh : route.nexthops) {
     if (weightOf(nh) > 0) {

@@ -40,6 +40,12 @@ class RibPolicyStatement {
   bool match(const RibUnicastEntry& route) const;
   bool applyAction(RibUnicastEntry& route, uint64_t* invalidated = nullptr) const;
   const std::string& name() const { return name_; }
+  // the set_weight action for one nexthop: neighbour weight, else area
+  // weight, else the default weight (RibPolicy.cpp:118-134)
+  int32_t weightOf(const std::optional<std::string>& area,
+                   const std::optional<std::string>& neighbor) const;
+  const std::set<Cidr>& prefixSet() const { return prefixSet_; }
+  const std::set<std::string>& tagSet() const { return tagSet_; }
 
  private:
   std::string name_;
@@ -66,11 +72,15 @@ class RibPolicy {
   PolicyChange applyPolicy(UnicastRouteMap& routes);
   // the same over a DecisionRouteUpdate's routes (Decision.cpp:1912-1924)
   PolicyChange applyPolicy(std::unordered_map<Cidr, RibUnicastEntry, CidrHash>& routes);
+  const std::vector<RibPolicyStatement>& statements() const { return statements_; }
   // decision.rib_policy.invalidated_routes (RibPolicy.cpp:150-153)
   uint64_t invalidatedRoutes() const { return invalidated_; }
   void addInvalidated(uint64_t n) { invalidated_ += n; }
+  // process-unique id of this policy (caches record it, not the address)
+  uint64_t generation() const { return generation_; }
 
  private:
+  uint64_t generation_{nextGeneration()};
   std::chrono::steady_clock::time_point validUntil_;
   std::vector<RibPolicyStatement> statements_;
   uint64_t invalidated_{0};

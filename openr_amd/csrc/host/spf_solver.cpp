@@ -170,6 +170,19 @@ Cmp compareMv(MetricVector l, MetricVector r) {
   return res;
 }
 
+// a selection output in one device block: status [n, padded to 4] | metric
+// [n] | best [n] | mask [n][words]
+orh_select_out selOut(uint8_t* base, uint32_t np, uint32_t words) {
+  const size_t n4 = (static_cast<size_t>(np) + 3) & ~static_cast<size_t>(3);
+  orh_select_out o{};
+  o.d_status = base;
+  o.d_metric = reinterpret_cast<uint32_t*>(base + n4);
+  o.d_best = o.d_metric + np;
+  o.d_mask = o.d_best + np;
+  o.total_words = words;
+  return o;
+}
+
 }  // namespace
 
 // ---- SpfSolver ----------------------------------------------------------------
@@ -195,6 +208,7 @@ SpfSolver::~SpfSolver() {
   if (dSel_) orh_device_free(selCtx_, dSel_);
   if (dSelPrev_) orh_device_free(selCtx_, dSelPrev_);
   if (dDiff_) orh_device_free(selCtx_, dDiff_);
+  if (dPolOut_) orh_device_free(selCtx_, dPolOut_);
 }
 
 void SpfSolver::updateStaticUnicastRoutes(
@@ -689,6 +703,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
                                const PrefixState& ps, bool diff) {
   deviceSelected_ = hostSelected_ = 0;
   lastDiffed_ = false;
+  devPol_.reset();  // policy decisions belong to the selection they were made on
   // a selection that does not complete (host path) leaves no snapshot: the
   // routes built from it do not correspond to the previous one any more
   const bool hadPrev = havePrev_;
@@ -845,16 +860,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   prof.mark(" select: areas");
   // outputs: status [n] | metric [n] | best [n] | mask [n][words]
   const uint32_t n = ps.numPrefixIds();
-  auto outOf = [&](uint8_t* base, uint32_t np) {
-    const size_t n4 = (static_cast<size_t>(np) + 3) & ~static_cast<size_t>(3);
-    orh_select_out o{};
-    o.d_status = base;
-    o.d_metric = reinterpret_cast<uint32_t*>(base + n4);
-    o.d_best = o.d_metric + np;
-    o.d_mask = o.d_best + np;
-    o.total_words = words;
-    return o;
-  };
+  auto outOf = [&](uint8_t* base, uint32_t np) { return selOut(base, np, words); };
   const size_t n4 = (static_cast<size_t>(n) + 3) & ~static_cast<size_t>(3);
   const size_t bytes = n4 + 8ull * n + 4ull * n * std::max(words, 1u);
   if (bytes > dSelCap_) {
@@ -935,7 +941,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   std::swap(dSel_, dSelPrev_);
   std::swap(dSelCap_, dSelPrevCap_);
   havePrev_ = shardWorld_ == 1;
-  ++selGen_;
+  selGen_ = nextGeneration();  // process-unique: also names this solver
   prevN_ = n;
   prevWords_ = words;
   prevLayout_ = layout;
@@ -952,15 +958,27 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
   const bool v4 = e.prefix.first.size() == 4;
   const int32_t metric = static_cast<int32_t>(selMetric_[pid]);
   const uint32_t* m = selMask_.data() + static_cast<size_t>(pid) * selWords_;
-  for (const AreaWork& w : areaWork_) {
+  // RibPolicy decided on the device: statement s sets every nexthop's weight
+  // (RibPolicy.cpp:117-141); a weight of 0 drops the nexthop, and s only
+  // applies when some nexthop keeps a weight (the kernel checked)
+  const uint32_t s = devPol_.on ? devPol_.stmt[pid] : ORH_POL_NONE;
+  const std::vector<std::vector<int32_t>>* wt = s < ORH_POL_MAX_STMTS ? &devPol_.weight[s] : nullptr;
+  for (size_t a = 0; a < areaWork_.size(); ++a) {
+    const AreaWork& w = areaWork_[a];
     const auto& tmpl = v4 ? w.tmpl4 : w.tmpl6;
     for (uint32_t k = 0; k < w.words; ++k) {
       for (uint32_t bits = m[w.wordOff + k]; bits; bits &= bits - 1) {
         const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
         if (b >= tmpl.size()) continue;
+        int32_t weight = 0;
+        if (wt) {
+          weight = (*wt)[a][b];
+          if (weight <= 0) continue;
+        }
         for (const auto& t : tmpl[b]) {
           NextHopThrift nh = t;
           nh.metric = metric;
+          nh.weight = weight;
           e.nexthops.insert(std::move(nh));
         }
       }
@@ -972,7 +990,92 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
   e.bestPrefixEntry = *best.entry;
   e.bestArea = best.key->second;
   e.doNotInstall = false;  // BGP prefixes take the host path
+  if (s == ORH_POL_HOST) {  // a tag set without a device id: matched on the host
+    uint64_t inv = 0;
+    if (devPol_.policy->applyAction(e, &inv)) ++devPol_.hostUpdated;
+    if (inv) devPol_.hostInvalidated += inv;
+  }
   return e;
+}
+
+bool SpfSolver::policyOnDevice(const PrefixState& ps, RibPolicy& policy) {
+  devPol_.reset();
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto& st = policy.statements();
+  if (st.empty() || st.size() > ORH_POL_MAX_STMTS || !selCtx_ || !dSelPrev_ || prevN_ == 0) return false;
+  const uint32_t S = static_cast<uint32_t>(st.size());
+  const uint32_t words = selWords_, n = prevN_;
+  orh_policy pol{};
+  pol.n_stmts = S;
+  pol.total_words = words;
+  // set_weight per statement, area and first-hop bit: every template of a
+  // bit is a link to one neighbour in one area, so they share the weight
+  devPol_.weight.assign(S, {});
+  std::vector<uint32_t> keep(static_cast<size_t>(S) * words, 0u);
+  for (uint32_t s = 0; s < S; ++s) {
+    devPol_.weight[s].resize(areaWork_.size());
+    for (size_t a = 0; a < areaWork_.size(); ++a) {
+      const AreaWork& w = areaWork_[a];
+      auto& wa = devPol_.weight[s][a];
+      wa.assign(w.tmpl6.size(), 0);
+      for (size_t b = 0; b < w.tmpl6.size() && b < 32ull * w.words; ++b) {
+        if (w.tmpl6[b].empty()) continue;
+        const NextHopThrift& t = w.tmpl6[b].front();
+        wa[b] = st[s].weightOf(t.area, t.neighborNodeName);
+        if (wa[b] > 0) keep[s * words + w.wordOff + b / 32] |= 1u << (b % 32);
+      }
+    }
+    if (!st[s].tagSet().empty()) pol.stmt_tags |= 1u << s;
+    if (!st[s].prefixSet().empty()) pol.stmt_prefixes |= 1u << s;
+  }
+  // tag set id -> statements whose tag matcher it meets (id 0: no tags)
+  const uint32_t nts = std::min<uint32_t>(ps.numTagSets(), ORH_ADV_TAGSET_OVF - 1) + 1;
+  std::vector<uint32_t> tagStmts(nts, 0u);
+  if (pol.stmt_tags) {
+    for (uint32_t t = 1; t < nts; ++t)
+      for (const auto& tag : ps.tagSet(t))
+        for (uint32_t s = 0; s < S; ++s)
+          if (st[s].tagSet().count(tag)) tagStmts[t] |= 1u << s;
+  }
+  // prefix ids named by the prefix matchers
+  std::map<uint32_t, uint32_t> named;
+  for (uint32_t s = 0; s < S; ++s)
+    for (const Cidr& c : st[s].prefixSet())
+      if (auto pid = ps.pidOf(c); pid && *pid < n) named[*pid] |= 1u << s;
+  std::vector<uint32_t> pfxId, pfxStmts;
+  for (const auto& [pid, mk] : named) {
+    pfxId.push_back(pid);
+    pfxStmts.push_back(mk);
+  }
+  pol.n_tagsets = nts;
+  pol.h_tagset_stmts = tagStmts.data();
+  pol.n_pfx = static_cast<uint32_t>(pfxId.size());
+  pol.h_pfx_id = pfxId.data();
+  pol.h_pfx_stmts = pfxStmts.data();
+  pol.h_keep = keep.data();
+  orh_ctx* ctx = selCtx_;
+  const size_t need = n + 64;  // out bytes | invalidated (aligned)
+  if (need > dPolOutCap_) {
+    if (dPolOut_) orh_device_free(ctx, dPolOut_);
+    dPolOut_ = nullptr;
+    dPolOutCap_ = std::max(need, 2 * dPolOutCap_);
+    if (orh_device_alloc(ctx, dPolOutCap_, reinterpret_cast<void**>(&dPolOut_)) != ORH_OK)
+      throw std::runtime_error("route policy: device allocation failed");
+  }
+  uint32_t* dInv = reinterpret_cast<uint32_t*>(dPolOut_ + ((n + 15) & ~size_t{15}));
+  const orh_select_out sel = selOut(dSelPrev_, n, words);
+  if (orh_route_policy(ps.syncDevice(ctx), n, &sel, &pol, dPolOut_, dInv) != ORH_OK)
+    throw std::runtime_error(std::string("orh_route_policy: ") + orh_last_error(ctx));
+  devPol_.stmt.resize(n);
+  uint32_t inv = 0;
+  if (orh_memcpy_d2h(ctx, devPol_.stmt.data(), dPolOut_, n) != ORH_OK ||
+      orh_memcpy_d2h(ctx, &inv, dInv, 4) != ORH_OK)
+    throw std::runtime_error(std::string("route policy copy-out: ") + orh_last_error(ctx));
+  devPol_.deviceInvalidated = inv;
+  devPol_.policy = &policy;
+  devPol_.on = true;
+  devPol_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return true;
 }
 
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
@@ -981,9 +1084,28 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& me,
   return buildRouteDbImpl(me, als, ps, false);
 }
 
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbWithPolicy(const std::string& me,
+                                                                 const AreaLinkStates& als,
+                                                                 const PrefixState& ps, RibPolicy* policy,
+                                                                 PolicyStats* stats) {
+  PolicyStats local;
+  PolicyStats& st = stats ? *stats : local;
+  st = PolicyStats{};
+  policyStats_ = &st;
+  try {
+    auto db = buildRouteDbImpl(me, als, ps, false, policy);
+    policyStats_ = nullptr;
+    return db;
+  } catch (...) {
+    policyStats_ = nullptr;
+    throw;
+  }
+}
+
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me,
                                                            const AreaLinkStates& als,
-                                                           const PrefixState& ps, bool mplsOnly) {
+                                                           const PrefixState& ps, bool mplsOnly,
+                                                           RibPolicy* policy) {
   // Decision.cpp:615-792 (mplsOnly: the MPLS routes alone, for buildRouteDelta)
   mplsKeyOk_ = false;
   bool exists = false;
@@ -1030,6 +1152,19 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   // as ORH_SEL_HOST (BGP, SR_MPLS / KSP2, minNexthop, self-advertised)
   const bool dev = !mplsOnly && selectOnDevice(me, als, ps);
   prof.mark("select (device)");
+  // RibPolicy (buildRouteDbWithPolicy): decided on the device for the
+  // device-selected routes and applied as they are materialised; host-path
+  // routes take applyAction as they are built, static routes as they are
+  // added; without a device decision, applyPolicy over the whole database
+  const bool policyActive = !mplsOnly && policy && policy->isActive();
+  const bool devPolicy = dev && policyActive && policyOnDevice(ps, *policy);
+  auto hostPolicy = [&](RibUnicastEntry& r) {
+    if (!devPolicy) return;
+    uint64_t inv = 0;
+    if (policy->applyAction(r, &inv)) ++devPol_.hostUpdated;
+    if (inv) devPol_.hostInvalidated += inv;
+  };
+  if (devPolicy) prof.mark("policy (device)");
   bool labelsDone = false;  // node-label routes built by the pipelined path
   std::vector<const Cidr*> keys;
   if (dev) {
@@ -1049,6 +1184,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         out.emplace(std::move(k), std::move(e));
       } else if (selStatus_[pid] == ORH_SEL_HOST) {
         if (auto r = createRouteForPrefix(me, als, ps, ps.prefixOf(pid))) {
+          hostPolicy(*r);
           Cidr k = r->prefix;
           out.emplace(std::move(k), std::move(*r));
         }
@@ -1116,6 +1252,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         RibUnicastEntry se;
         se.prefix = prefix;
         se.nexthops.insert(nhs.begin(), nhs.end());
+        hostPolicy(se);
         db.unicastRoutes.emplace(prefix, std::move(se));
       }
       prof.mark("unicast merge");
@@ -1191,9 +1328,38 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       RibUnicastEntry e;
       e.prefix = prefix;
       e.nexthops.insert(nhs.begin(), nhs.end());
+      hostPolicy(e);
       db.unicastRoutes.emplace(prefix, std::move(e));
     }
     prof.mark("unicast merge");
+  }
+  if (policyActive) {
+    uint64_t updated = 0, onDevice = 0;
+    if (devPolicy) {
+      const uint32_t n = ps.numPrefixIds();
+      for (uint32_t pid = 0; pid < n; ++pid)
+        if (ps.prefixLive(pid) && ownsPid(pid, n) && selStatus_[pid] == ORH_SEL_ROUTE &&
+            devPol_.stmt[pid] != ORH_POL_HOST) {
+          ++onDevice;
+          updated += devPol_.stmt[pid] < ORH_POL_MAX_STMTS;
+        }
+      updated += devPol_.hostUpdated;
+      policy->addInvalidated(devPol_.deviceInvalidated + devPol_.hostInvalidated);
+    } else {  // RibPolicy::applyPolicy over the whole database on the host
+      const uint64_t inv0 = policy->invalidatedRoutes();
+      updated = policy->applyPolicy(db.unicastRoutes).updatedRoutes.size();
+      if (policyStats_) policyStats_->invalidated = policy->invalidatedRoutes() - inv0;
+    }
+    if (policyStats_) {
+      policyStats_->updated = updated;
+      policyStats_->onDevice = onDevice;
+      if (devPolicy) {
+        policyStats_->invalidated = devPol_.deviceInvalidated + devPol_.hostInvalidated;
+        policyStats_->deviceMs = devPol_.ms;
+      }
+    }
+    devPol_.on = false;  // later materialisations (other builds) select anew
+    prof.mark("policy (host part)");
   }
   // node-label routes; duplicate labels resolve to the smaller node name.
   // The candidate entry of every adjacency database is computed on the
@@ -1366,6 +1532,10 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
   hostSelected_ = nHost;
   prof.mark("candidates");
   const bool applyPolicy = policy && policy->isActive();
+  // the policy decided on the device for the materialised routes (as in
+  // buildRouteDbWithPolicy); host-path and static routes take applyAction
+  const bool devPolicy = applyPolicy && policyOnDevice(ps, *policy);
+  if (devPolicy) prof.mark("policy (device)");
   auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
     auto it = staticUnicastRoutes_.find(p);
     if (it == staticUnicastRoutes_.end()) return std::nullopt;
@@ -1394,10 +1564,13 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
   std::vector<Part> parts(nChunks);
   // the new route of one prefix (createRouteForPrefixOrGetStaticRoute, then
   // the policy), compared with current's entry (calculateUpdate)
-  auto one = [&](const Cidr& prefix, std::optional<RibUnicastEntry> r, Part& out) {
-    if (!r) r = staticRoute(prefix);
+  auto one = [&](const Cidr& prefix, std::optional<RibUnicastEntry> r, Part& out, bool policyDone) {
+    if (!r) {
+      r = staticRoute(prefix);
+      policyDone = false;
+    }
     const auto t1 = prof.on ? Clock::now() : Clock::time_point{};
-    if (r && applyPolicy) policy->applyAction(*r, &out.invalidated);
+    if (r && applyPolicy && !policyDone) policy->applyAction(*r, &out.invalidated);
     const auto t2 = prof.on ? Clock::now() : Clock::time_point{};
     auto it = current.unicastRoutes.find(prefix);
     const auto t3 = prof.on ? Clock::now() : Clock::time_point{};
@@ -1426,20 +1599,25 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     for (size_t i = b; i < e; ++i) {
       if (i >= todo.size()) {
         const Cidr& c = deleted[i - todo.size()];
-        if (!ps.pidOf(c)) one(c, std::nullopt, parts[w]);
+        if (!ps.pidOf(c)) one(c, std::nullopt, parts[w], false);
         continue;
       }
       const uint32_t pid = todo[i];
       const Cidr& prefix = ps.prefixOf(pid);
       const auto t0 = prof.on ? Clock::now() : Clock::time_point{};
       std::optional<RibUnicastEntry> r;
-      if (selStatus_[pid] == ORH_SEL_ROUTE) r = materialize(pid, ps);
-      else if (selStatus_[pid] == ORH_SEL_HOST) r = createRouteForPrefix(me, als, ps, prefix);
+      bool policyDone = false;
+      if (selStatus_[pid] == ORH_SEL_ROUTE) {
+        r = materialize(pid, ps);
+        policyDone = devPolicy;
+      } else if (selStatus_[pid] == ORH_SEL_HOST) {
+        r = createRouteForPrefix(me, als, ps, prefix);
+      }
       if (prof.on) {
         parts[w].tBuild += ms(t0, Clock::now());
         ++parts[w].n;
       }
-      one(prefix, std::move(r), parts[w]);
+      one(prefix, std::move(r), parts[w], policyDone);
     }
     if (prof.on) parts[w].tCpu += cpuMs() - c0;
   }, nChunks);
@@ -1473,7 +1651,11 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
     for (auto& c : p.del) delta.unicastRoutesToDelete.push_back(std::move(c));
     invalidated += p.invalidated;
   }
+  // the device counted every selected route, as the reference's full rebuild
+  // counts every route it applies the policy to (RibPolicy.cpp:149-150)
+  if (devPolicy) invalidated += devPol_.deviceInvalidated + devPol_.hostInvalidated;
   if (policy) policy->addInvalidated(invalidated);
+  devPol_.on = false;
   // MPLS routes: unchanged inputs (no topology or static change since the
   // build current holds) keep them; else rebuilt and compared in full
   if (mplsKeyOk_ && mplsMe_ == me && mplsStatic_ == staticEpoch_ && mplsKey_ == mplsInputs(als)) {

@@ -10,7 +10,9 @@
 // mask OR instead of string-set unions.
 #pragma once
 
+#include <atomic>
 #include <deque>
+#include <map>
 #include <set>
 
 #include "link_state.h"
@@ -70,6 +72,8 @@ class PrefixState {
   // are logged with theirs (ids are reused)
   uint64_t stamp() const { return stamp_; }
   uint64_t pidStamp(uint32_t pid) const { return pidStamp_[pid]; }
+  // process-unique instance id (stamps are process-unique too)
+  uint64_t id() const { return id_; }
   // calls f(prefix) for each prefix withdrawn after `since`; false when the
   // log no longer reaches back that far
   template <class F>
@@ -84,11 +88,17 @@ class PrefixState {
   std::optional<uint32_t> areaId(const std::string& a) const;
   uint32_t numAreas() const { return static_cast<uint32_t>(areas_.size()); }
   const std::string& area(uint32_t id) const { return areas_[id]; }
+  // tag sets of the advertisements (ids 1 .. numTagSets(); 0 = no tags;
+  // ids saturate at ORH_ADV_TAGSET_OVF)
+  uint32_t tagSetId(const std::set<std::string>& tags) const;
+  uint32_t numTagSets() const { return static_cast<uint32_t>(tagSets_.size()); }
+  const std::set<std::string>& tagSet(uint32_t id) const { return *tagSets_[id - 1]; }
 
  private:
   void touch(const Cidr& prefix, bool erased);
   uint32_t internName(const std::string& n);
   uint32_t internArea(const std::string& a);
+  uint32_t internTagSet(const std::set<std::string>& tags);
   orh_adv advRecord(const NodeAndArea& na, const PrefixEntry& e) const;
 
   std::unordered_map<Cidr, PrefixEntries, CidrHash> prefixes_;
@@ -99,7 +109,8 @@ class PrefixState {
   std::vector<uint8_t> live_;
   std::vector<uint32_t> freePids_;
   std::vector<uint32_t> dirty_;
-  uint64_t stamp_{0};
+  uint64_t id_{nextGeneration()};
+  uint64_t stamp_{nextGeneration()};
   std::vector<uint64_t> pidStamp_;
   static constexpr size_t kDeletedLog = 1u << 20;
   std::deque<std::pair<uint64_t, Cidr>> deleted_;
@@ -107,6 +118,8 @@ class PrefixState {
   std::vector<uint8_t> isDirty_;
   std::unordered_map<std::string, uint32_t> nameIds_, areaIds_;
   std::vector<std::string> names_, areas_;
+  std::map<std::set<std::string>, uint32_t> tagSetIds_;
+  std::vector<const std::set<std::string>*> tagSets_;  // id - 1 -> set (map nodes are stable)
 
   mutable std::vector<AdvRef> advPool_;
   mutable std::vector<std::pair<uint32_t, uint32_t>> run_;  // pid -> (offset, count)
@@ -146,6 +159,21 @@ class SpfSolver {
 
   std::optional<DecisionRouteDb> buildRouteDb(const std::string& me, const AreaLinkStates& als,
                                               const PrefixState& ps);
+  // buildRouteDb, then policy->applyPolicy(db.unicastRoutes): the full
+  // rebuild of Decision::rebuildRoutes (Decision.cpp:1888-1900). The same
+  // database, with the policy decided per route on the device for the routes
+  // the device selected (orh_route_policy) and its weights set while they are
+  // materialised; host-path and static routes take RibPolicy::applyAction.
+  // Without an active policy this is buildRouteDb.
+  struct PolicyStats {
+    uint64_t updated{0};      // routes the policy transformed (PolicyChange.updatedRoutes)
+    uint64_t invalidated{0};  // statements that would have dropped every nexthop
+    uint64_t onDevice{0};     // routes whose statement the device decided
+    double deviceMs{0};       // policy tables + kernel + copy-out (host wall time)
+  };
+  std::optional<DecisionRouteDb> buildRouteDbWithPolicy(const std::string& me, const AreaLinkStates& als,
+                                                        const PrefixState& ps, RibPolicy* policy,
+                                                        PolicyStats* stats = nullptr);
   std::optional<RibUnicastEntry> createRouteForPrefixOrGetStaticRoute(
       const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
       const Cidr& prefix);
@@ -241,8 +269,39 @@ class SpfSolver {
   bool selectOnDevice(const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
                       bool diff = false);
   std::optional<DecisionRouteDb> buildRouteDbImpl(const std::string& me, const AreaLinkStates& als,
-                                                  const PrefixState& ps, bool mplsOnly);
+                                                  const PrefixState& ps, bool mplsOnly,
+                                                  RibPolicy* policy = nullptr);
+  // the route of a device-selected prefix; with the device policy on, its
+  // statement's weights applied (or RibPolicy::applyAction for ORH_POL_HOST)
   RibUnicastEntry materialize(uint32_t pid, const PrefixState& ps) const;
+  // RibPolicy decided on the device for the last selection (devPol_); false
+  // when the policy does not fit the device form (> 32 statements, no
+  // selection on the device)
+  bool policyOnDevice(const PrefixState& ps, RibPolicy& policy);
+  struct DevicePolicy {
+    bool on{false};
+    RibPolicy* policy{nullptr};
+    std::vector<uint8_t> stmt;  // per prefix id: statement, ORH_POL_NONE / _HOST
+    // weight[s][area][first-hop bit] of statement s
+    std::vector<std::vector<std::vector<int32_t>>> weight;
+    uint64_t deviceInvalidated{0};
+    mutable std::atomic<uint64_t> hostInvalidated{0}, hostUpdated{0};
+    uint64_t onDevice{0};
+    double ms{0};
+    void reset() {
+      on = false;
+      policy = nullptr;
+      stmt.clear();
+      weight.clear();
+      deviceInvalidated = onDevice = 0;
+      hostInvalidated = 0;
+      hostUpdated = 0;
+      ms = 0;
+    }
+  } devPol_;
+  uint8_t* dPolOut_{nullptr};
+  size_t dPolOutCap_{0};
+  PolicyStats* policyStats_{nullptr};  // set while buildRouteDbWithPolicy runs
 
   // device selection workspace (per solver)
   struct AreaWork {

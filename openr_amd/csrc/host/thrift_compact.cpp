@@ -69,6 +69,18 @@ void Reader::listBegin(Type* elem, uint32_t* n) {
   *n = static_cast<uint32_t>(c);
 }
 
+// one open list / set / map level of skip(), bounded together with the open
+// structs by kMaxDepth
+struct ContainerLevel {
+  explicit ContainerLevel(Reader& r) : r_(r) {
+    if (r.last_.size() + r.containers_ >= Reader::kMaxDepth)
+      throw std::invalid_argument("compact: nesting too deep");
+    ++r.containers_;
+  }
+  ~ContainerLevel() { --r_.containers_; }
+  Reader& r_;
+};
+
 void Reader::skip(Type t) {
   switch (t) {
     case kTrue: case kFalse: return;  // value in the header (field) or a byte (list element)
@@ -77,6 +89,7 @@ void Reader::skip(Type t) {
     case kDouble: need(8); p_ += 8; return;
     case kBinary: binary(); return;
     case kList: case kSet: {
+      ContainerLevel level(*this);
       Type e;
       uint32_t n;
       listBegin(&e, &n);
@@ -87,6 +100,7 @@ void Reader::skip(Type t) {
       return;
     }
     case kMap: {
+      ContainerLevel level(*this);
       Type k, v;
       uint32_t n;
       mapBegin(&k, &v, &n);

@@ -86,9 +86,11 @@ class Reader {
   Reader(const uint8_t* p, size_t n) : p_(p), e_(p + n) {}
   // nesting bound: peer-supplied bytes must not drive skip() into unbounded
   // recursion (fbthrift rejects such input as a deserialisation error)
+  // (structs, lists, sets and maps count alike: a list level costs the peer
+  // one byte, so containers are bounded as structs are)
   static constexpr size_t kMaxDepth = 64;
   void structBegin() {
-    if (last_.size() >= kMaxDepth) throw std::invalid_argument("compact: nesting too deep");
+    if (last_.size() + containers_ >= kMaxDepth) throw std::invalid_argument("compact: nesting too deep");
     last_.push_back(0);
   }
   void structEnd() { last_.pop_back(); }
@@ -135,6 +137,8 @@ class Reader {
   const uint8_t* p_;
   const uint8_t* e_;
   std::vector<int16_t> last_;
+  size_t containers_ = 0;  // list / set / map levels open inside skip()
+  friend struct ContainerLevel;
 };
 
 // ---- Decision -> Fib (Types.thrift:1003-1060, Network.thrift:48-131) -------

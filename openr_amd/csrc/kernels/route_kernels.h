@@ -57,6 +57,26 @@ struct RouteDiffArgs {
 };
 hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s);
 
+// RibPolicy over a selection (route_policy_kernel; see orh_route_policy)
+struct RoutePolicyArgs {
+  uint32_t n_prefix, words;
+  const uint2* hdr;
+  const orh_adv* adv;
+  const uint8_t* status;
+  const uint32_t* best;
+  const uint32_t* mask;
+  uint32_t n_stmts, stmt_tags, stmt_pfx;
+  uint32_t n_tagsets;
+  const uint32_t* tagset_stmts;
+  uint32_t n_pfx;
+  const uint32_t* pfx_id;
+  const uint32_t* pfx_stmts;
+  const uint32_t* keep;  // [n_stmts][words]
+  uint8_t* out;
+  uint32_t* invalidated;  // zeroed before the launch
+};
+hipError_t launch_route_policy(const RoutePolicyArgs& a, hipStream_t s);
+
 // hdr[ids[i]] = vals[i]
 hipError_t launch_scatter_hdr(uint2* hdr, const uint32_t* ids, const uint2* vals, uint32_t n,
                               hipStream_t s);

@@ -255,6 +255,63 @@ __global__ __launch_bounds__(kSelBlock) void route_diff_kernel(RouteDiffArgs a) 
   for (uint32_t k = 0; k < a.words; ++k) o[4 + k] = a.mask[static_cast<size_t>(p) * a.words + k];
 }
 
+// RibPolicy::applyPolicy (RibPolicy.cpp:229-247) over a selection, one thread
+// per prefix: the statement that applies to the route, if any (see
+// orh_route_policy for the reduction of set_weight to keep[s] masks). The
+// match reads one advertisement record (the best one's tag set id), a tag-set
+// table entry and, when a statement has a prefix matcher, a binary search over
+// the named prefix ids; the tables are a few KB and stay in L2, so the kernel
+// streams the selection records (status, best, mask: 5 + 4 W bytes per prefix)
+// plus one advertisement gather and writes one byte.
+__global__ __launch_bounds__(kSelBlock) void route_policy_kernel(RoutePolicyArgs a) {
+  const uint32_t p = blockIdx.x * kSelBlock + threadIdx.x;
+  if (p >= a.n_prefix) return;
+  uint32_t res = ORH_POL_NONE, inv = 0;
+  if (a.status[p] == ORH_SEL_ROUTE) {
+    const uint32_t meta = a.adv[a.hdr[p].x + a.best[p]].meta;
+    const uint32_t ts = meta >> ORH_ADV_TAGSET_SHIFT;
+    const uint32_t tm = ts < a.n_tagsets ? a.tagset_stmts[ts] : 0u;
+    uint32_t pm = 0;
+    if (a.n_pfx) {  // lower bound of p in the named prefix ids
+      uint32_t lo = 0, hi = a.n_pfx;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.pfx_id[mid] < p) lo = mid + 1; else hi = mid;
+      }
+      if (lo < a.n_pfx && a.pfx_id[lo] == p) pm = a.pfx_stmts[lo];
+    }
+    const uint32_t all = a.n_stmts >= 32 ? ~0u : ((1u << a.n_stmts) - 1u);
+    // RibPolicyStatement::match (:73-105): every non-empty matcher matches and
+    // at least one is non-empty
+    uint32_t match = all & (a.stmt_tags | a.stmt_pfx) & (~a.stmt_tags | tm) & (~a.stmt_pfx | pm);
+    if (ts == ORH_ADV_TAGSET_OVF && (all & a.stmt_tags)) {
+      res = ORH_POL_HOST;  // the tag set has no id: the host matches it
+      match = 0;
+    }
+    const uint32_t* m = a.mask + static_cast<size_t>(p) * a.words;
+    for (; match; match &= match - 1) {
+      const uint32_t s = static_cast<uint32_t>(__builtin_ctz(match));
+      const uint32_t* k = a.keep + static_cast<size_t>(s) * a.words;
+      uint32_t any = 0;
+      for (uint32_t w = 0; w < a.words; ++w) any |= m[w] & k[w];
+      if (any) {  // applyAction (:108-158): the weights apply
+        res = s;
+        break;
+      }
+      ++inv;  // every nexthop weighted 0: kept unchanged, counted
+    }
+  }
+  a.out[p] = static_cast<uint8_t>(res);
+  if (inv) atomicAdd(a.invalidated, inv);
+}
+
+hipError_t launch_route_policy(const RoutePolicyArgs& a, hipStream_t s) {
+  if (a.n_prefix == 0) return hipSuccess;
+  hipLaunchKernelGGL(route_policy_kernel, dim3((a.n_prefix + kSelBlock - 1) / kSelBlock), dim3(kSelBlock), 0,
+                     s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s) {
   if (a.n_prefix == 0) return hipSuccess;
   hipLaunchKernelGGL(route_diff_kernel, dim3((a.n_prefix + kSelBlock - 1) / kSelBlock), dim3(kSelBlock), 0, s, a);

@@ -1220,8 +1220,11 @@ int whatif_stage(orh_whatif* job, size_t words, uint32_t** h, uint32_t** d) {
   return ORH_OK;
 }
 
-// one batch of requests of a job: seed, copy, repair tiers (and without
-// slots the full search for what outgrew tier 2), all on the context stream
+// one batch of requests of a job: seed and copy and the small repair tiers
+// on the context stream; the large tiers, the slot tier (t3 streams) and,
+// without slots, the full search for what outgrew tier 2 on the job's side
+// streams, over job-owned memory (slots, labels), joined back into the
+// context stream through side_ev
 int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const uint32_t* ign_ptr,
                const uint32_t* ign_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info) {
   orh_graph* g = job->g;
@@ -1440,9 +1443,18 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
                                     orh::SpfMode::kGlobal);
     fp.variant = orh::SpfVariant::kGlobalNh;
     fp.block = 1024;  // only the flagged rows search; the rest exit at once
-    ORH_HIP(ctx, hipStreamSynchronize(job->side));  // labels may be grown below
-    rc = ensure_labels(ctx, static_cast<size_t>(n_req) * N);
-    if (rc) return rc;
+    // job-owned labels: this search runs on the job's side stream, which
+    // later work on the context stream (searches over ctx->d_labels) does
+    // not wait for
+    const size_t need = static_cast<size_t>(n_req) * N * 8;
+    if (need > job->full_lab_cap) {
+      ORH_HIP(ctx, hipStreamSynchronize(job->side));  // the old buffer may be in use
+      hipFree(job->d_full_lab);
+      job->d_full_lab = nullptr;
+      job->full_lab_cap = 0;
+      ORH_HIP(ctx, hipMalloc(&job->d_full_lab, need));
+      job->full_lab_cap = need;
+    }
     orh::SpfArgs a{};
     a.n_nodes = N;
     a.n_out = n_req;
@@ -1457,8 +1469,8 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
                            : std::max<uint32_t>(1u, static_cast<uint32_t>(
                                                         static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
     a.out_dist = d_dist;
-    a.scratch = ctx->d_scratch;
-    a.labels = ctx->d_labels;
+    a.scratch = ctx->d_scratch;  // unused: every row is < n_out
+    a.labels = static_cast<unsigned long long*>(job->d_full_lab);
     a.out_nh = d_nh;
     a.words = 1;
     a.rank_out = g->d_rank_out;
@@ -2636,6 +2648,9 @@ struct orh_prefix_set {
   std::vector<orh::SelArea> h_areas;
   uint32_t* d_stage = nullptr;
   size_t stage_cap = 0;  // in u32
+  uint32_t* d_pol = nullptr;  // policy tables (orh_route_policy)
+  size_t pol_cap = 0;         // in u32
+  std::vector<uint32_t> h_pol;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the last route_select launch
 };
 
@@ -2704,6 +2719,7 @@ int orh_prefix_destroy(orh_prefix_set* ps) {
   hipFree(ps->d_rank);
   hipFree(ps->d_areas);
   hipFree(ps->d_stage);
+  hipFree(ps->d_pol);
   if (ps->ev0) hipEventDestroy(ps->ev0);
   if (ps->ev1) hipEventDestroy(ps->ev1);
   delete ps;
@@ -2907,6 +2923,64 @@ int orh_route_diff(orh_prefix_set* ps, uint32_t n_prefix, uint32_t prev_n, const
   a.count = d_count;
   hipError_t e = orh::launch_route_diff(a, ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "route_diff launch");
+  return ORH_OK;
+}
+
+int orh_route_policy(orh_prefix_set* ps, uint32_t n_prefix, const orh_select_out* sel,
+                     const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated) {
+  if (!ps || !sel || !pol || !d_out || !d_invalidated) return ORH_E_INVALID;
+  orh_ctx* ctx = ps->ctx;
+  if (pol->n_stmts > ORH_POL_MAX_STMTS)
+    return fail(ctx, ORH_E_UNSUPPORTED, "orh_route_policy: more than 32 statements");
+  if (n_prefix > ps->hdr.size()) return fail(ctx, ORH_E_INVALID, "orh_route_policy: n_prefix beyond the set");
+  if (pol->total_words != sel->total_words)
+    return fail(ctx, ORH_E_INVALID, "orh_route_policy: mask widths differ");
+  if (!sel->d_status || !sel->d_best || (sel->total_words && !sel->d_mask) ||
+      (pol->n_tagsets && !pol->h_tagset_stmts) || (pol->n_pfx && (!pol->h_pfx_id || !pol->h_pfx_stmts)) ||
+      (pol->n_stmts && pol->total_words && !pol->h_keep))
+    return fail(ctx, ORH_E_INVALID, "orh_route_policy: null table");
+  for (uint32_t i = 1; i < pol->n_pfx; ++i)
+    if (pol->h_pfx_id[i] <= pol->h_pfx_id[i - 1])
+      return fail(ctx, ORH_E_INVALID, "orh_route_policy: prefix ids not ascending");
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  // a previous launch may still read the device tables, and its upload the
+  // host staging: the context stream drains before either is reused
+  ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // one upload: tag-set table | prefix ids | prefix statements | keep masks
+  const size_t nk = static_cast<size_t>(pol->n_stmts) * pol->total_words;
+  auto& h = ps->h_pol;
+  h.clear();
+  h.reserve(pol->n_tagsets + 2ull * pol->n_pfx + nk + 1);
+  h.insert(h.end(), pol->h_tagset_stmts, pol->h_tagset_stmts + pol->n_tagsets);
+  h.insert(h.end(), pol->h_pfx_id, pol->h_pfx_id + pol->n_pfx);
+  h.insert(h.end(), pol->h_pfx_stmts, pol->h_pfx_stmts + pol->n_pfx);
+  if (nk) h.insert(h.end(), pol->h_keep, pol->h_keep + nk);
+  h.push_back(0u);
+  int rc = grow(ctx, reinterpret_cast<void**>(&ps->d_pol), &ps->pol_cap, h.size(), 4, 0);
+  if (rc) return rc;
+  ORH_HIP(ctx, hipMemcpyAsync(ps->d_pol, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  ORH_HIP(ctx, hipMemsetAsync(d_invalidated, 0, sizeof(uint32_t), ctx->stream));
+  orh::RoutePolicyArgs a{};
+  a.n_prefix = n_prefix;
+  a.words = sel->total_words;
+  a.hdr = ps->d_hdr;
+  a.adv = ps->d_pool;
+  a.status = sel->d_status;
+  a.best = sel->d_best;
+  a.mask = sel->d_mask;
+  a.n_stmts = pol->n_stmts;
+  a.stmt_tags = pol->stmt_tags;
+  a.stmt_pfx = pol->stmt_prefixes;
+  a.n_tagsets = pol->n_tagsets;
+  a.tagset_stmts = ps->d_pol;
+  a.n_pfx = pol->n_pfx;
+  a.pfx_id = ps->d_pol + pol->n_tagsets;
+  a.pfx_stmts = a.pfx_id + pol->n_pfx;
+  a.keep = a.pfx_stmts + pol->n_pfx;
+  a.out = d_out;
+  a.invalidated = d_invalidated;
+  hipError_t e = orh::launch_route_policy(a, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "route_policy launch");
   return ORH_OK;
 }
 

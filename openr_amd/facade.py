@@ -161,6 +161,14 @@ class SpfSolver:
         w = self._impl.build_route_db(my_node, als._impl, ps._impl)
         return None if w is None else RouteDb.from_wire(w)
 
+    def build_route_db_with_policy(self, my_node: str, als: AreaLinkStates, ps: PrefixState,
+                                   policy) -> Optional[RouteDb]:
+        """buildRouteDb, then RibPolicy::applyPolicy over its unicast routes
+        (Decision::rebuildRoutes, Decision.cpp:1888-1900); `policy` is an
+        openr_amd.rib_policy.RibPolicy of the same backend."""
+        w = self._impl.build_route_db_with_policy(my_node, als._impl, ps._impl, policy._impl)
+        return None if w is None else RouteDb.from_wire(w)
+
     def create_route_for_prefix_or_get_static_route(self, my_node, als, ps,
                                                     prefix: IpPrefix):
         w = self._impl.create_route_for_prefix_or_get_static_route(
@@ -213,6 +221,11 @@ class Backend:
                    bgp_dry_run=False, enable_best_route_selection=False) -> SpfSolver:
         return SpfSolver(self.module, my_node, enable_v4, enable_ordered_fib,
                          bgp_dry_run, enable_best_route_selection)
+
+    def rib_policy(self, statements, ttl_secs: int):
+        """RibPolicy(thrift::RibPolicy) of this backend (RibPolicy.cpp:164-178)."""
+        from .rib_policy import RibPolicy
+        return RibPolicy(statements, ttl_secs, module=self.module)
 
     def calculate_update(self, old_db: RouteDb, new_db: RouteDb) -> RouteDbDelta:
         """DecisionRouteDb::calculateUpdate (Decision.cpp:108-143)."""

@@ -81,10 +81,12 @@ def unicast_entry(prefix: str, nexthops: Sequence[NextHopThrift] = (),
 
 
 class RibPolicyStatementCheck:
-    """A lone RibPolicyStatement (match / applyAction)."""
+    """A lone RibPolicyStatement (match / applyAction). `module`: the native
+    module that implements it (default: the product host library; the tests
+    also pass the CPU oracle's, which has the same surface)."""
 
-    def __init__(self, stmt: RibPolicyStatement):
-        self._impl = host_module().RibPolicyStatement(stmt.to_wire())
+    def __init__(self, stmt: RibPolicyStatement, module=None):
+        self._impl = (module or host_module()).RibPolicyStatement(stmt.to_wire())
 
     def match(self, route: UnicastRoute) -> bool:
         return self._impl.match(route_to_wire(route))
@@ -97,8 +99,9 @@ class RibPolicyStatementCheck:
 class RibPolicy:
     """RibPolicy(thrift::RibPolicy): statements + ttl_secs."""
 
-    def __init__(self, statements: Sequence[RibPolicyStatement], ttl_secs: int):
-        self._impl = host_module().RibPolicy([s.to_wire() for s in statements], int(ttl_secs))
+    def __init__(self, statements: Sequence[RibPolicyStatement], ttl_secs: int, module=None):
+        self._impl = (module or host_module()).RibPolicy([s.to_wire() for s in statements],
+                                                         int(ttl_secs))
 
     def is_active(self) -> bool:
         return self._impl.is_active()

@@ -264,12 +264,12 @@ class RouteDb:
 
     def canonical_full(self):
         """canonical() plus each route's bestArea and bestPrefixEntry (part of
-        RibUnicastEntry equality, RibEntry.h:65-69; tags left out)."""
+        RibUnicastEntry equality, RibEntry.h:65-69), tags included."""
         def entry(e):
             if e is None:
                 return None
             return (e.prefix, e.type, e.data, e.forwardingType, e.forwardingAlgorithm, e.mv,
-                    e.minNexthop, e.prependLabel, e.metrics)
+                    e.minNexthop, e.prependLabel, e.metrics, tuple(sorted(e.tags)))
         return (
             {str(k): (v.nexthop_set(), v.doNotInstall, v.bestArea, entry(v.bestPrefixEntry))
              for k, v in self.unicastRoutes.items()},

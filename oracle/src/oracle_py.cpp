@@ -9,6 +9,7 @@
 #include <thread>
 
 #include "oracle_decision.h"
+#include "oracle_rib_policy.h"
 
 namespace py = pybind11;
 using namespace oracle;
@@ -71,6 +72,8 @@ PrefixEntry entryFromWire(const py::tuple& t) {
     e.mv = mv;
   }
   if (!t[9].is_none()) e.data = bytesOf(t[9]);
+  if (t.size() > 10 && !t[10].is_none())
+    for (auto tag : t[10]) e.tags.insert(tag.cast<std::string>());
   return e;
 }
 
@@ -88,7 +91,8 @@ py::object entryToWire(const PrefixEntry& e) {
                         py::cast(e.prependLabel),
                         py::make_tuple(e.metrics.path_preference,
                                        e.metrics.source_preference, e.metrics.distance),
-                        mv, e.data ? py::object(py::bytes(*e.data)) : py::none());
+                        mv, e.data ? py::object(py::bytes(*e.data)) : py::none(),
+                        py::tuple(py::cast(std::vector<std::string>(e.tags.begin(), e.tags.end()))));
 }
 
 NextHopThrift nhFromWire(const py::tuple& t) {
@@ -293,6 +297,10 @@ void serEntry(Ser& s, const PrefixEntry& e) {
     }
   });
   s.opt(e.data, [&](const std::string& x) { s.str(x); });
+  if (!e.tags.empty()) {  // sorted (std::set); absent for tag-free entries
+    s.i32(static_cast<int32_t>(e.tags.size()));
+    for (const auto& t : e.tags) s.str(t);
+  }
 }
 
 // (n_unicast, n_mpls, per-route FNV digests as little-endian u64 bytes)
@@ -331,6 +339,35 @@ py::tuple routeDbDigest(const DecisionRouteDb& db) {
 // std::unordered_map would be converted to a dict by pybind11/stl.h; wrap it
 struct AreaMap {
   AreaLinkStates m;
+};
+
+// (name, prefixes | None, tags | None, (default, {area: w}, {nbr: w}) | None),
+// the wire form openr_amd/rib_policy.py gives both backends
+RibPolicyStatementSpec statementFromWire(const py::tuple& t) {
+  RibPolicyStatementSpec s;
+  s.name = t[0].cast<std::string>();
+  if (!t[1].is_none()) {
+    s.prefixes.emplace();
+    for (auto p : t[1]) {
+      auto pt = p.cast<py::tuple>();
+      s.prefixes->emplace_back(bytesOf(pt[0]), pt[1].cast<int32_t>());
+    }
+  }
+  if (!t[2].is_none()) s.tags = t[2].cast<std::vector<std::string>>();
+  if (!t[3].is_none()) {
+    auto w = t[3].cast<py::tuple>();
+    RibRouteActionWeight a;
+    a.default_weight = w[0].cast<int32_t>();
+    a.area_to_weight = w[1].cast<std::map<std::string, int32_t>>();
+    a.neighbor_to_weight = w[2].cast<std::map<std::string, int32_t>>();
+    s.set_weight = std::move(a);
+  }
+  return s;
+}
+
+struct StatementProbe {  // a lone RibPolicyStatement (RibPolicyTest.cpp statement tests)
+  RibPolicyStatement st;
+  uint64_t invalidated{0};
 };
 
 }  // namespace
@@ -655,5 +692,80 @@ PYBIND11_MODULE(openr_oracle, m) {
              }
              s.updateStaticMplsRoutes(u, del);
            })
+      // Decision::rebuildRoutes' full rebuild (Decision.cpp:1888-1900):
+      // buildRouteDb, then RibPolicy::applyPolicy on its unicast routes
+      .def("build_route_db_with_policy",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) -> py::object {
+             auto db = s.buildRouteDb(me, als.m, ps);
+             if (!db) return py::none();
+             policy.applyPolicy(db->unicastRoutes);
+             return routeDbToWire(*db);
+           })
+      .def("build_route_db_with_policy_digest",
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,
+              RibPolicy& policy) -> py::object {
+             std::optional<DecisionRouteDb> db;
+             {
+               py::gil_scoped_release rel;
+               db = s.buildRouteDb(me, als.m, ps);
+               if (db) policy.applyPolicy(db->unicastRoutes);
+             }
+             if (!db) return py::none();
+             return routeDbDigest(*db);
+           })
       .def_property_readonly("route_build_runs", [](const SpfSolver& s) { return s.routeBuildRuns; });
+
+  // RibPolicy (RibPolicy.cpp:19-247), the same Python surface as the
+  // product's openr_amd._openr_host.RibPolicy
+  py::class_<RibPolicy>(m, "RibPolicy")
+      .def(py::init([](py::list statements, int64_t ttlSecs) {
+             std::vector<RibPolicyStatementSpec> specs;
+             for (auto st : statements) specs.push_back(statementFromWire(st.cast<py::tuple>()));
+             try {
+               return new RibPolicy(specs, ttlSecs);
+             } catch (const std::invalid_argument& e) {
+               throw py::value_error(e.what());
+             }
+           }),
+           py::arg("statements"), py::arg("ttl_secs"))
+      .def("is_active", &RibPolicy::isActive)
+      .def("ttl_ms", [](const RibPolicy& p) { return p.getTtlDuration().count(); })
+      .def("match", [](const RibPolicy& p, py::tuple r) { return p.match(unicastFromWire(r)); })
+      .def("apply_action",
+           [](RibPolicy& p, py::tuple r) {
+             RibUnicastEntry e = unicastFromWire(r);
+             const bool changed = p.applyAction(e);
+             return py::make_tuple(changed, unicastToWire(e));
+           })
+      .def("apply_policy",  // (updated prefixes, deleted prefixes, transformed unicast routes)
+           [](RibPolicy& p, py::list routes) {
+             std::unordered_map<Cidr, RibUnicastEntry, CidrHash> m;
+             for (auto r : routes) {
+               RibUnicastEntry e = unicastFromWire(r.cast<py::tuple>());
+               Cidr k = e.prefix;
+               m.emplace(std::move(k), std::move(e));
+             }
+             auto ch = p.applyPolicy(m);
+             py::list up, del, out;
+             for (const auto& c : ch.updatedRoutes) up.append(py::make_tuple(py::bytes(c.first), c.second));
+             for (const auto& c : ch.deletedRoutes) del.append(py::make_tuple(py::bytes(c.first), c.second));
+             for (const auto& [_, e] : m) out.append(unicastToWire(e));
+             return py::make_tuple(up, del, out);
+           })
+      .def_property_readonly("invalidated_routes", &RibPolicy::invalidatedRoutes);
+  py::class_<StatementProbe>(m, "RibPolicyStatement")
+      .def(py::init([](py::tuple st) {
+        try {
+          return new StatementProbe{RibPolicyStatement(statementFromWire(st))};
+        } catch (const std::invalid_argument& e) {
+          throw py::value_error(e.what());
+        }
+      }))
+      .def("match", [](const StatementProbe& s, py::tuple r) { return s.st.match(unicastFromWire(r)); })
+      .def("apply_action", [](StatementProbe& s, py::tuple r) {
+        RibUnicastEntry e = unicastFromWire(r);
+        const bool changed = s.st.applyAction(e, s.invalidated);
+        return py::make_tuple(changed, unicastToWire(e));
+      });
 }

@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <functional>
 #include <optional>
+#include <set>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -121,12 +122,13 @@ struct PrefixEntry {
   PrefixMetrics metrics;
   std::optional<MetricVector> mv;
   std::optional<std::string> data;
+  std::set<std::string> tags;  // Types.thrift PrefixEntry field 11 (set<string>)
   bool operator==(const PrefixEntry& o) const {
     return prefixAddr == o.prefixAddr && prefixLen == o.prefixLen &&
         type == o.type && forwardingType == o.forwardingType &&
         forwardingAlgorithm == o.forwardingAlgorithm &&
         minNexthop == o.minNexthop && prependLabel == o.prependLabel &&
-        metrics == o.metrics && mv == o.mv && data == o.data;
+        metrics == o.metrics && mv == o.mv && data == o.data && tags == o.tags;
   }
 };
 

@@ -245,6 +245,24 @@ def test_nesting_depth_limited(mod):
     assert mod.adj_db_from_compact(_insert_before_stop(data, shallow)) == db.to_wire()
 
 
+@pytest.mark.parametrize("kind", ["list", "map"])
+def test_container_nesting_depth_limited(mod, kind):
+    """Unknown fields of nested lists (one byte per level) or maps (three
+    bytes per level) are bounded like nested structs: a peer cannot drive
+    skip() into unbounded recursion."""
+    db = bench_grid(2, 0)[0][0]
+    data = mod.adj_db_to_compact(db.to_wire())
+
+    def nested(levels):
+        if kind == "list":  # field 20 list<list<...<list<>>>>: one element per level
+            return b"\xe9" + b"\x19" * levels + b"\x09"
+        return b"\xeb" + b"\x01\x5b\x02" * levels + b"\x00"  # map<i32, map<...>>: {1: ...}
+
+    with pytest.raises(ValueError, match="nesting"):
+        mod.adj_db_from_compact(_insert_before_stop(data, nested(1_000_000)))
+    assert mod.adj_db_from_compact(_insert_before_stop(data, nested(8))) == db.to_wire()
+
+
 def test_skip_map_of_bools(mod):
     """An unknown map<i32, bool> field: each bool is a one-byte value, so the
     fields after it must still decode."""
