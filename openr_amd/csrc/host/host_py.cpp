@@ -1104,6 +1104,20 @@ PYBIND11_MODULE(_openr_host, m) {
            },
            py::arg("solver"), py::arg("me"), py::arg("als"), py::arg("ps"), py::arg("full"),
            py::arg("prefixes"), py::arg("policy") = nullptr, py::arg("wire") = true)
+      .def("rebuild_routes_thrift",  // the same; the update as thrift::RouteDatabaseDelta bytes
+           [](DecisionRib& r, SpfSolver& solver, const std::string& me, const AreaMap& als,
+              const PrefixState& ps, bool full, std::vector<py::tuple> prefixes, RibPolicy* policy) {
+             std::vector<Cidr> pfx;
+             pfx.reserve(prefixes.size());
+             for (auto& t : prefixes) pfx.emplace_back(AddrBytes(str(t[0])), t[1].cast<int32_t>());
+             return py::bytes(compact::routeDatabaseDelta(r.rebuildRoutes(solver, me, als.m, ps, full, pfx, policy)));
+           },
+           py::arg("solver"), py::arg("me"), py::arg("als"), py::arg("ps"), py::arg("full"),
+           py::arg("prefixes"), py::arg("policy") = nullptr)
+      .def("route_db_thrift",  // routeDb_ as thrift::RouteDatabase bytes
+           [](const DecisionRib& r, const std::string& me) {
+             return py::bytes(compact::routeDatabase(r.routeDb(), me));
+           })
       .def_property_readonly("delta_rebuilds", &DecisionRib::deltaRebuilds)
       .def_property_readonly("whole_rebuilds", &DecisionRib::wholeRebuilds)
       .def("rebuild_routes_pending",  // from a DecisionIngest's pending updates (then reset)

@@ -337,11 +337,37 @@ class ShardedMap {
     auto [it, ok] = s_[i].emplace(std::move(k), std::forward<VV>(value));
     return {iterator(this, i, it), ok};
   }
+  // emplace(std::make_pair(k, v)) (NetlinkSocket.cpp:386 style)
+  std::pair<iterator, bool> emplace(value_type&& kv) {
+    const size_t i = shardOf(kv.first);
+    auto [it, ok] = s_[i].emplace(std::move(kv));
+    return {iterator(this, i, it), ok};
+  }
+  std::pair<iterator, bool> insert(const value_type& kv) {
+    const size_t i = shardOf(kv.first);
+    auto [it, ok] = s_[i].insert(kv);
+    return {iterator(this, i, it), ok};
+  }
+  template <class... Args>
+  std::pair<iterator, bool> try_emplace(const K& k, Args&&... args) {
+    const size_t i = shardOf(k);
+    auto [it, ok] = s_[i].try_emplace(k, std::forward<Args>(args)...);
+    return {iterator(this, i, it), ok};
+  }
   template <class VV>
   void insert_or_assign(const K& k, VV&& value) {
     s_[shardOf(k)].insert_or_assign(k, std::forward<VV>(value));
   }
+  V& at(const K& k) { return s_[shardOf(k)].at(k); }  // std::out_of_range when absent
+  const V& at(const K& k) const { return s_[shardOf(k)].at(k); }
+  V& operator[](const K& k) { return s_[shardOf(k)][k]; }
   size_t erase(const K& k) { return s_[shardOf(k)].erase(k); }
+  // erase by iterator, returning the next element (Fib.cpp:360 loop form)
+  iterator erase(const_iterator pos) {
+    const size_t i = pos.s_;
+    return iterator(this, i, s_[i].erase(pos.it_));
+  }
+  iterator erase(iterator pos) { return erase(const_iterator(pos)); }
   Shard& shard(size_t i) { return s_[i]; }
   const Shard& shard(size_t i) const { return s_[i]; }
 

@@ -2076,6 +2076,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   info.mask_bits = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.mask_bytes * 8 : 0;
   info.batch_sources = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.ms_width : 0;
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
+#ifdef ORH_EXP_MSBFS_ONLY  // timing experiment only (tools/diag_build.sh): no phase 2
+    ctx->last_info = info;
+    ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    return ORH_OK;
+#endif
     e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
     e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);

@@ -540,6 +540,48 @@ PYBIND11_MODULE(openr_oracle, m) {
            },
            py::arg("srcs"), py::arg("order"), py::arg("nbrs"), py::arg("threads") = 8,
            py::arg("ignores") = std::vector<std::vector<std::tuple<std::string, std::string, std::string>>>{})
+      .def("kth_paths_threaded",
+           [](const LinkState& s, std::vector<std::pair<std::string, std::string>> pairs, int threads,
+              std::vector<std::string> replay) {
+             // getKthPaths(src, dst, 1) and (src, dst, 2) per pair on per-thread
+             // LinkState copies (the memo is not thread-safe), pairs of one
+             // source on one thread (its SpfResult memoised there). The copies
+             // replay the adjacency databases in `replay` order - the order the
+             // caller loaded them - so every LinkSet has the original's
+             // insertion sequence and iteration order (parallel-link ties).
+             std::vector<std::vector<Path>> k1(pairs.size()), k2(pairs.size());
+             {
+               py::gil_scoped_release rel;
+               threads = std::max(1, std::min<int>(threads, static_cast<int>(pairs.size())));
+               const auto& dbs = s.getAdjacencyDatabases();
+               for (const auto& n : replay)
+                 if (!dbs.count(n)) throw std::invalid_argument("kth_paths_threaded: no database of " + n);
+               std::map<std::string, int> owner;
+               for (const auto& p : pairs) owner.emplace(p.first, static_cast<int>(owner.size()) % threads);
+               std::vector<std::thread> ws;
+               for (int t = 0; t < threads; ++t) {
+                 ws.emplace_back([&, t] {
+                   LinkState copy(s.getArea());  // built on its thread
+                   for (const auto& n : replay) copy.updateAdjacencyDatabase(dbs.at(n));
+                   for (size_t i = 0; i < pairs.size(); ++i) {
+                     if (owner.at(pairs[i].first) != t) continue;
+                     k1[i] = copy.getKthPaths(pairs[i].first, pairs[i].second, 1);
+                     k2[i] = copy.getKthPaths(pairs[i].first, pairs[i].second, 2);
+                   }
+                 });
+               }
+               for (auto& w : ws) w.join();
+             }
+             py::list out;
+             for (size_t i = 0; i < pairs.size(); ++i) {
+               py::list a, b;
+               for (const auto& p : k1[i]) a.append(pathToWire(p));
+               for (const auto& p : k2[i]) b.append(pathToWire(p));
+               out.append(py::make_tuple(a, b));
+             }
+             return out;
+           },
+           py::arg("pairs"), py::arg("threads"), py::arg("replay"))
       .def("time_spf_sources",
            [](const LinkState& s, std::vector<std::string> srcs, int threads) {
              // Timed all-sources SPF: one LinkState copy per thread (the memo is

@@ -55,3 +55,18 @@ def test_host_module_imports():
     mod = host_module()
     for name in ("LinkState", "AreaLinkStates", "PrefixState", "SpfSolver", "SpfSweep"):
         assert hasattr(mod, name)
+
+
+def test_route_map_unordered_map_api(tmp_path):
+    """DecisionRouteDb::unicastRoutes / DecisionRouteUpdate::
+    unicastRoutesToUpdate are 64-shard maps, not std::unordered_map: the
+    reference's own call patterns on them (Decision.h:110, RouteUpdate.h:34-41,
+    Decision.cpp:148, Fib.cpp:304 / :357-361, NetlinkSocket.cpp:386) compile
+    and behave as on std::unordered_map (tests/cxx/route_map_api.cpp)."""
+    import subprocess
+    exe = tmp_path / "route_map_api"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-pthread", "-I" + os.path.join(ROOT, "openr_amd", "csrc", "host"),
+                    "-I" + os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "cxx", "route_map_api.cpp"),
+                    "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), (out.returncode, out.stdout)

@@ -93,6 +93,40 @@ def test_c2_sweep_first_hops_exact(hip, oracle, variant):
     assert info["hop_nodes"] == 16, info  # first_hop_lvl_kernel<16>, as benched
 
 
+@pytest.mark.parametrize("variant", [0, 7])
+def test_c2_sweep_all_sources_exact(hip, oracle, variant):
+    """Every one of the 10,000 rows of a benched C2 sweep (the grid, and the
+    what-if variant 7 with its seeded drained link) against the oracle's
+    runSpf tables on 16 threads, dist rows and first-hop masks in full, in
+    chunks of 1,000 sources (~11 s of oracle time per variant)."""
+    from bench import drain_what_if_link
+    n = 100
+    adj_dbs, _ = bench_grid(n)
+    if variant:
+        assert drain_what_if_link(adj_dbs, n, variant)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    names = [str(i) for i in range(n * n)]
+    ls_h, ls_o = als_h[A], als_o[A]
+    sweep = ls_h._impl.sweep(names, True)
+    sweep.run()
+    sweep.sync()
+    info = sweep.info()
+    assert info["variant"] == MSBFS and info["hop_nodes"] == 16, info
+    order = ls_h._impl.node_names()
+    W = sweep.words
+    for lo in range(0, n * n, 1000):
+        srcs = names[lo:lo + 1000]
+        dist_o, nh_o = ls_o._impl.spf_tables(srcs, order, [ls_h._impl.neighbors(s) for s in srcs], 16)
+        for k, s in enumerate(srcs):
+            dist, nh = sweep.fetch(lo + k)
+            assert np.array_equal(dist, dist_o[k]), ("dist", s)
+            assert not np.any(nh_o[k][:, W:]), s
+            assert np.array_equal(nh.reshape(len(order), W), nh_o[k][:, :W]), ("first hops", s)
+        del dist_o, nh_o
+        gc.collect()
+
+
 @pytest.mark.parametrize("env", [{"ORH_MS_WIDE": "1"}, {"ORH_MS_SKIP": "1"}])
 def test_c2_sweep_opt_in_variants(hip, oracle, monkeypatch, env):
     """The opt-in MS-BFS variants on the same sweep, 64 sources compared in

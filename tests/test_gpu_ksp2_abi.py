@@ -130,6 +130,33 @@ def test_ksp2_device_batch_c4(hip, oracle, monkeypatch):
             assert got[(s, d, k)] == als_o[A].get_kth_paths(s, d, k), (s, d, k)
 
 
+def test_ksp2_device_batch_c4_vs_oracle(hip, oracle):
+    """The benched C4 KSP2 batch (c4_wan(), 1,024 seeded pairs, one device
+    batch) against the oracle's own getKthPaths (LinkState.cpp:762-791) on 40
+    of its pairs: the 20 with the most k = 1 + k = 2 paths and 20 seeded
+    others, k = 1 and k = 2, link by link. The oracle runs them on 16
+    threads, each with a LinkState copy loaded in the same order as the
+    product's (same LinkSet iteration order)."""
+    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan
+    adj, _ = c4_wan()
+    als_h, _ = load_topology(hip, adj, [])
+    ls = als_h[A]._impl
+    pairs = c4_ksp2_pairs(ls.node_names(), C4_KSP2_PAIRS)
+    ls.prefetch_kth_paths(pairs)
+    assert ls.ksp_stats() == (len(set(pairs)), 0)
+    got = {(s, d): (als_h[A].get_kth_paths(s, d, 1), als_h[A].get_kth_paths(s, d, 2)) for s, d in pairs}
+    ranked = sorted(set(pairs), key=lambda p: (-(len(got[p][0]) + len(got[p][1])), p))
+    pick = ranked[:20]
+    rest = [p for p in sorted(set(pairs)) if p not in set(pick)]
+    pick += random.Random(41).sample(rest, 20)
+    assert sum(len(got[p][0]) + len(got[p][1]) for p in pick) > 60
+    als_o, _ = load_topology(oracle, adj, [])
+    want = als_o[A]._impl.kth_paths_threaded(pick, 16, [db.thisNodeName for db in adj])
+    for p, (k1, k2) in zip(pick, want):
+        assert got[p][0] == [[LinkDesc(*l) for l in path] for path in k1], (p, 1)
+        assert got[p][1] == [[LinkDesc(*l) for l in path] for path in k2], (p, 2)
+
+
 def test_kth_paths_link_handles(hip, oracle):
     """getKthPaths in the reference's type: paths of LinkRef handles walked as
     selectBestPathsKsp2 walks them (Decision.cpp:1035-1076:

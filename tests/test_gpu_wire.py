@@ -1,0 +1,126 @@
+"""The wire output of device-built route databases (SURVEY.md §8f f3;
+Types.thrift:1003-1060 RouteDatabase / RouteDatabaseDelta, Decision.h:92-104
+DecisionRouteDb::toThrift).
+
+The product builds the route database on the device path and serialises it in
+C++ (SpfSolver build_route_db_thrift, DecisionRib rebuild_routes_thrift);
+those bytes must equal the same Compact serialiser run over the oracle's
+databases (and deltas: calculateUpdate of the oracle's builds), and decode
+with the independent schema-less decoder (tests/compact_decode.py). The
+serialiser writes routes in prefix / label order and nexthops in
+NextHopThrift order (the reference lists unordered_* iteration order, see
+DESIGN.md §9), so equal databases give equal bytes.
+
+  C1 grid (node / adjacency labels)               RouteDatabase
+  C3 Clos at 3,000 prefixes, both selection modes RouteDatabase
+  random topologies with SR_MPLS / KSP2 prefixes   RouteDatabase
+  C5 at 3,000 prefixes with the UCMP policy        RouteDatabase + two
+                                                   RouteDatabaseDeltas (whole
+                                                   and delta rebuilds)
+"""
+import random
+
+import pytest
+
+from compact_decode import decode
+from openr_amd import host_module
+from openr_amd.facade import load_topology
+from openr_amd.topology import bench_grid
+from openr_amd.types import (IpPrefix, K_TESTING_AREA, PrefixEntry, PrefixForwardingAlgorithm,
+                             PrefixForwardingType, PrefixMetrics, create_prefix_entry)
+from openr_amd.workloads import C5_AREAS, c3_fabric, c5_multi_area
+
+from test_gpu_parity import random_topology
+from test_gpu_policy import _ucmp
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_bytes(hip, oracle, adj, pfx, me, best_route=False):
+    mod = host_module()
+    als_h, ps_h = load_topology(hip, adj, pfx)
+    als_o, ps_o = load_topology(oracle, adj, pfx)
+    sh = hip.spf_solver(me, True, enable_best_route_selection=best_route)
+    got = sh._impl.build_route_db_thrift(me, als_h._impl, ps_h._impl)
+    wire = oracle.spf_solver(me, True, enable_best_route_selection=best_route)._impl.build_route_db(
+        me, als_o._impl, ps_o._impl)
+    want = mod.route_db_thrift(wire, me)
+    assert got == want
+    d = decode(got)
+    assert d[1] == me.encode()
+    assert len(d[4]) == len(wire[0]) and len(d.get(5, [])) == len(wire[1])
+    return d, sh
+
+
+def test_route_db_bytes_c1(hip, oracle):
+    adj, pfx = bench_grid(10, 1)
+    d, sh = _same_bytes(hip, oracle, adj, pfx, "1")
+    assert len(d[4]) == 99 and len(d[5]) == 99 + 3
+
+
+@pytest.mark.parametrize("best_route", [False, True])
+def test_route_db_bytes_c3(hip, oracle, best_route):
+    adj, pfx = c3_fabric(num_prefixes=3000)
+    d, sh = _same_bytes(hip, oracle, adj, pfx, "2-0-0", best_route)
+    assert len(d[4]) > 2900
+    assert sh.device_selected > 2900  # the device selection built them
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_route_db_bytes_ksp2_random(hip, oracle, seed):
+    """SR_MPLS / KSP2 prefixes (PUSH / SWAP / PHP label stacks, KSP2 second
+    paths traced on the device) on random graphs with parallel links."""
+    dbs = random_topology(6100 + seed, n=20, extra=30, parallel=0.3)
+    rng = random.Random(seed)
+    pfx = []
+    for i in range(60):
+        for db in rng.sample(dbs, rng.randint(1, 3)):
+            e = create_prefix_entry(IpPrefix.of(f"fc00:{seed}::{i:x}/128"))
+            if rng.random() < 0.5:
+                e.forwardingType = PrefixForwardingType.SR_MPLS
+                if rng.random() < 0.6:
+                    e.forwardingAlgorithm = PrefixForwardingAlgorithm.KSP2_ED_ECMP
+            pfx.append((db.thisNodeName, K_TESTING_AREA, e))
+    me = sorted(db.thisNodeName for db in dbs)[seed]
+    d, _ = _same_bytes(hip, oracle, dbs, pfx, me)
+    assert any(3 in nh for r in d[4] for nh in r[4])  # MPLS actions on the wire
+
+
+def test_route_delta_bytes_c5_policy(hip, oracle):
+    """Decision::rebuildRoutes with the C5 UCMP policy on the product
+    (DecisionRib: a whole rebuild, then full rebuilds after prefix and metric
+    changes, which run as deltas) against the oracle's buildRouteDb +
+    applyPolicy and calculateUpdate, as RouteDatabase / RouteDatabaseDelta
+    bytes."""
+    mod = host_module()
+    areas, pfx = c5_multi_area(num_prefixes=3000)
+    adj = [db for a in C5_AREAS for db in areas[a]]
+    als_h, ps_h = load_topology(hip, adj, pfx)
+    als_o, ps_o = load_topology(oracle, adj, pfx)
+    sh = hip.spf_solver("me", True, enable_best_route_selection=True)
+    so = oracle.spf_solver("me", True, enable_best_route_selection=True)
+    ph = hip.rib_policy(_ucmp(), 3600)
+    rib = hip.module.DecisionRib()
+    prev_wire = ([], [])
+    rng = random.Random(12)
+    for rnd in range(3):
+        delta = rib.rebuild_routes_thrift(sh._impl, "me", als_h._impl, ps_h._impl, True, [], ph._impl)
+        cur = so._impl.build_route_db_with_policy("me", als_o._impl, ps_o._impl,
+                                                  oracle.rib_policy(_ucmp(), 3600)._impl)
+        assert delta == mod.route_delta_thrift(prev_wire, cur), rnd
+        assert rib.route_db_thrift("me") == mod.route_db_thrift(cur, "me"), rnd
+        dd = decode(delta)
+        assert rnd > 0 or len(dd[2]) == len(cur[0])
+        prev_wire = cur
+        for _ in range(150):
+            node, area, e = pfx[rng.randrange(len(pfx))]
+            e2 = PrefixEntry(e.prefix, metrics=PrefixMetrics(1, rng.randint(0, 3), rng.randint(0, 3),
+                                                             rng.randint(0, 3)), tags=e.tags)
+            ps_h.update_prefix(node, area, e2)
+            ps_o.update_prefix(node, area, e2)
+        a = C5_AREAS[rnd % 4]
+        db = areas[a][rng.randrange(len(areas[a]) - 1)]
+        db.adjacencies[0].metric = rng.randint(1, 4)
+        als_h[a].update_adjacency_database(db)
+        als_o[a].update_adjacency_database(db)
+    assert rib.delta_rebuilds >= 1

@@ -39,3 +39,22 @@ def test_route_db_digest_sensitivity(oracle):
     x = np.frombuffer(a[2], np.uint64)
     y = np.frombuffer(b[2], np.uint64)
     assert 0 < np.count_nonzero(x != y) < len(x)
+
+
+def test_kth_paths_threaded_matches_get_kth_paths(oracle):
+    """kth_paths_threaded (per-thread LinkState copies replayed in load
+    order) equals get_kth_paths on the loaded LinkState, parallel-link ties
+    included (random graphs with parallel links)."""
+    from test_gpu_parity import random_topology
+    dbs = random_topology(2300, n=18, extra=30, max_metric=3, parallel=0.4, overload=0.1,
+                          link_overload=0.05)
+    als, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    pairs = [(s, d) for s in names[:6] for d in names]
+    got = als[A]._impl.kth_paths_threaded(pairs, 4, [db.thisNodeName for db in dbs])
+    n = 0
+    for (s, d), (k1, k2) in zip(pairs, got):
+        assert [list(map(tuple, p)) for p in k1] == [list(map(tuple, p)) for p in als[A].get_kth_paths(s, d, 1)]
+        assert [list(map(tuple, p)) for p in k2] == [list(map(tuple, p)) for p in als[A].get_kth_paths(s, d, 2)]
+        n += len(k1) + len(k2)
+    assert n > 100

@@ -4,4 +4,6 @@
 set -e
 cd "$(dirname "$0")/.."
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-value -Wno-unused-result "$@" \
-  -o openr_amd/lib/libopenr_hip.so openr_amd/csrc/orh_api.hip openr_amd/csrc/kernels/spf_kernels.hip
+  -o openr_amd/lib/libopenr_hip.so openr_amd/csrc/orh_api.hip openr_amd/csrc/kernels/spf_kernels.hip \
+  openr_amd/csrc/kernels/route_kernels.hip openr_amd/csrc/kernels/whatif_kernels.hip \
+  openr_amd/csrc/kernels/ksp_kernels.hip
