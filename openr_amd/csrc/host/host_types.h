@@ -181,15 +181,23 @@ struct NextHopThrift {
   }
 };
 
+// std::hash<thrift::NextHopThrift> (openr/common/NetworkUtil.cpp:24-66): the
+// sum of the member hashes (libstdc++ std::hash of the address bytes and the
+// ifName, identity hashes of weight, metric and the MPLS action's fields).
+// With the reference's insertion sequence (getNextHopsThrift's area / LinkSet
+// loop, RibPolicy's rebuild) a NextHopSet then iterates - and toThrift lists -
+// its nexthops in the reference's order
 struct NextHopHash {
   size_t operator()(const NextHopThrift& nh) const {
-    size_t h = strHash(nh.address.addr) * 31 + std::hash<int32_t>()(nh.metric);
-    if (nh.address.ifName) h = h * 31 + strHash(*nh.address.ifName);
+    size_t h = strHash(nh.address.addr);
+    if (nh.address.ifName) h += std::hash<std::string>()(*nh.address.ifName);
+    h += std::hash<int32_t>()(nh.weight);
+    h += std::hash<int32_t>()(nh.metric);
     if (nh.mplsAction) {
-      h = h * 31 + static_cast<size_t>(nh.mplsAction->action);
-      if (nh.mplsAction->swapLabel) h = h * 31 + static_cast<size_t>(*nh.mplsAction->swapLabel);
+      h += std::hash<int8_t>()(static_cast<int8_t>(nh.mplsAction->action));
+      if (nh.mplsAction->swapLabel) h += std::hash<int32_t>()(*nh.mplsAction->swapLabel);
       if (nh.mplsAction->pushLabels)
-        for (auto l : *nh.mplsAction->pushLabels) h = h * 31 + static_cast<size_t>(l);
+        for (auto l : *nh.mplsAction->pushLabels) h += std::hash<int32_t>()(l);
     }
     return h;
   }

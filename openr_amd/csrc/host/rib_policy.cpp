@@ -64,32 +64,12 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidat
     if (invalidated) ++*invalidated;
     return false;
   }
-  // NextHopHash leaves the weight out, so with one weight across the set (no
-  // two nexthops differ only by weight, e.g. every route fresh from
-  // buildRouteDb) the weights are set in place and dropped nexthops erased:
-  // bucket positions stay valid and no two elements can become equal
-  bool sameWeight = true;
-  for (const auto& nh : route.nexthops)
-    if (nh.weight != route.nexthops.begin()->weight) {
-      sameWeight = false;
-      break;
-    }
-  if (sameWeight) {
-    for (auto it = route.nexthops.begin(); it != route.nexthops.end();) {
-      const int32_t w = weightOf(*it);
-      if (w <= 0) {
-        it = route.nexthops.erase(it);
-      } else {
-        const_cast<NextHopThrift&>(*it).weight = w;  // not part of the hash
-        ++it;
-      }
-    }
-    return true;
-  }
-  // otherwise the kept nexthops move into a new set as nodes: no copies of
-  // their strings, no allocations
-  NextHopSet out;
-  out.reserve(route.nexthops.size());
+  // the kept nexthops move into a new set as nodes (no copies of their
+  // strings, no allocations), in the old set's iteration order - the
+  // reference's insertion sequence into newNexthops (RibPolicy.cpp:116-141),
+  // so the new set iterates as the reference's does (the weight is part of
+  // the hash, NetworkUtil.cpp:57-66)
+  NextHopSet out;  // grown as the reference's is (no reserve: the bucket count shapes the order)
   while (!route.nexthops.empty()) {
     auto node = route.nexthops.extract(route.nexthops.begin());
     const int32_t w = weightOf(node.value());

@@ -183,6 +183,9 @@ orh_select_out selOut(uint8_t* base, uint32_t np, uint32_t words) {
   return o;
 }
 
+// no MPLS action on a template nexthop (unicast SP_ECMP routes)
+const auto noAction = [](const NextHopThrift&) -> std::optional<MplsAction> { return std::nullopt; };
+
 }  // namespace
 
 // ---- SpfSolver ----------------------------------------------------------------
@@ -756,6 +759,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     sel[a] = orh_select_area{};
     w.words = 0;
     w.tmpl4.clear();
+    w.linkOrder.clear();
     w.tmpl6.clear();
     const LinkState* ls = order[a];
     if (!ls) continue;
@@ -817,18 +821,24 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     // minMetric, Decision.cpp:1271-1276, for a neighbour on a shortest path)
     w.tmpl4.assign(row.nbrs.size(), {});
     w.tmpl6.assign(row.nbrs.size(), {});
+    w.linkOrder.clear();
     const uint32_t myId = row.src;
-    for (uint32_t lid : ls->linksFromNode(me)) {
+    for (uint32_t lid : ls->linksFromNode(me)) {  // LinkSet iteration order
       const Link& l = ls->link(lid);
       const uint32_t nbr = l.other(myId);
       if (!l.isUp() || !row.reachable(nbr) || l.metricFrom(myId) != row.metric(nbr)) continue;
       auto k = std::lower_bound(row.nbrs.begin(), row.nbrs.end(), nbr) - row.nbrs.begin();
       if (k >= static_cast<ptrdiff_t>(row.nbrs.size()) || row.nbrs[k] != nbr) continue;
       const std::string& nbrName = ls->nodeName(nbr);
+      w.linkOrder.emplace_back(static_cast<uint32_t>(k), static_cast<uint32_t>(w.tmpl6[k].size()));
       w.tmpl6[k].push_back(nextHop(l.nhV6From(myId), l.ifFrom(myId), 0, std::nullopt, l.area, nbrName));
       w.tmpl4[k].push_back(nextHop(l.nhV4From(myId), l.ifFrom(myId), 0, std::nullopt, l.area, nbrName));
     }
   }
+  areaIter_.clear();
+  for (const auto& [area, ls] : als)  // the reference's area loop order
+    for (size_t a = 0; a < order.size(); ++a)
+      if (order[a] == &ls) areaIter_.push_back(static_cast<uint32_t>(a));
   // digest of everything a materialised route depends on besides its
   // selection record: the area layout and every nexthop template
   uint64_t layout = 1469598103934665603ull;
@@ -948,6 +958,29 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   return true;
 }
 
+template <class Act>
+void SpfSolver::insertTemplates(const uint32_t* m, bool v4, int32_t metric,
+                                const std::vector<std::vector<int32_t>>* wt,
+                                std::vector<std::pair<const NextHopThrift*, int32_t>>* wts, NextHopSet& out,
+                                Act&& act) const {
+  // getNextHopsThrift's loops (Decision.cpp:1245-1246): areas in
+  // AreaLinkStates order, then my links in LinkSet order; a link is a
+  // nexthop when its neighbour's first-hop bit is set and it is tight
+  for (uint32_t a : areaIter_) {
+    const AreaWork& w = areaWork_[a];
+    if (!w.words) continue;
+    const auto& tmpl = v4 ? w.tmpl4 : w.tmpl6;
+    for (const auto& [b, j] : w.linkOrder) {
+      if (!((m[w.wordOff + b / 32] >> (b % 32)) & 1u)) continue;
+      NextHopThrift nh = tmpl[b][j];
+      nh.metric = metric;
+      nh.mplsAction = act(nh);
+      auto it = out.insert(std::move(nh)).first;
+      if (wts) wts->emplace_back(&*it, (*wt)[a][b]);
+    }
+  }
+}
+
 RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) const {
   // selectBestPathsSpf -> getNextHopsThrift -> addBestPaths (Decision.cpp
   // :904-963, :1230-1334, :1089-1150) for a device-selected IP / SP_ECMP
@@ -962,27 +995,26 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
   // (RibPolicy.cpp:117-141); a weight of 0 drops the nexthop, and s only
   // applies when some nexthop keeps a weight (the kernel checked)
   const uint32_t s = devPol_.on ? devPol_.stmt[pid] : ORH_POL_NONE;
-  const std::vector<std::vector<int32_t>>* wt = s < ORH_POL_MAX_STMTS ? &devPol_.weight[s] : nullptr;
-  for (size_t a = 0; a < areaWork_.size(); ++a) {
-    const AreaWork& w = areaWork_[a];
-    const auto& tmpl = v4 ? w.tmpl4 : w.tmpl6;
-    for (uint32_t k = 0; k < w.words; ++k) {
-      for (uint32_t bits = m[w.wordOff + k]; bits; bits &= bits - 1) {
-        const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
-        if (b >= tmpl.size()) continue;
-        int32_t weight = 0;
-        if (wt) {
-          weight = (*wt)[a][b];
-          if (weight <= 0) continue;
-        }
-        for (const auto& t : tmpl[b]) {
-          NextHopThrift nh = t;
-          nh.metric = metric;
-          nh.weight = weight;
-          e.nexthops.insert(std::move(nh));
-        }
-      }
+  if (s < ORH_POL_MAX_STMTS) {
+    // the reference builds the route (weights 0), then the policy moves the
+    // kept nexthops into a new set in the first set's iteration order
+    // (RibPolicy.cpp:116-141): the same two sets here, so the result
+    // iterates in the reference's order; weights from the device decision
+    thread_local std::vector<std::pair<const NextHopThrift*, int32_t>> wts;
+    wts.clear();
+    NextHopSet built;
+    insertTemplates(m, v4, metric, &devPol_.weight[s], &wts, built, noAction);
+    while (!built.empty()) {
+      auto node = built.extract(built.begin());  // node addresses are stable
+      int32_t w = 0;
+      for (const auto& [p, pw] : wts)
+        if (p == &node.value()) w = pw;
+      if (w <= 0) continue;
+      node.value().weight = w;
+      e.nexthops.insert(std::move(node));
     }
+  } else {
+    insertTemplates(m, v4, metric, nullptr, nullptr, e.nexthops, noAction);
   }
   uint32_t cnt = 0;
   const AdvRef* advs = ps.advs(pid, &cnt);
@@ -1219,22 +1251,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           auto v = ls.nodeId(adjDb.thisNodeName);
           if (!v || !myRow.reachable(*v)) return;
           const int32_t metric = static_cast<int32_t>(myRow.metric(*v));
+          const uint32_t* vm = myRow.nh.data() + static_cast<size_t>(*v) * tw->words;
           bool any = false;
-          for (uint32_t k = 0; k < tw->words; ++k) {
-            for (uint32_t bits = myRow.nh[static_cast<size_t>(*v) * tw->words + k]; bits;
-                 bits &= bits - 1) {
-              any = true;
-              const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
-              for (const auto& t : tw->tmpl6[b]) {
-                NextHopThrift nh = t;
-                nh.metric = metric;
-                nh.mplsAction = *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
-                                                                           : mpls(kSwap, lbl);
-                entry.nexthops.insert(std::move(nh));
-              }
-            }
-          }
+          for (uint32_t k = 0; k < tw->words; ++k) any |= vm[k] != 0;
           if (!any) return;
+          // the row's words are the only area's: wordOff 0
+          insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops,
+                          [&](const NextHopThrift& nh) -> std::optional<MplsAction> {
+                            return *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp) : mpls(kSwap, lbl);
+                          });
         }
         cand[i] = std::move(entry);
       };
@@ -1394,21 +1419,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         auto v = ls.nodeId(adjDb.thisNodeName);
         if (!v || !myRow->reachable(*v)) return;
         const int32_t metric = static_cast<int32_t>(myRow->metric(*v));
+        const uint32_t* vm = myRow->nh.data() + static_cast<size_t>(*v) * tw->words;
         bool any = false;
-        for (uint32_t k = 0; k < tw->words; ++k) {
-          for (uint32_t bits = myRow->nh[static_cast<size_t>(*v) * tw->words + k]; bits;
-               bits &= bits - 1) {
-            any = true;
-            const uint32_t b = k * 32 + static_cast<uint32_t>(__builtin_ctz(bits));
-            for (const auto& t : tw->tmpl6[b]) {
-              NextHopThrift nh = t;
-              nh.metric = metric;
-              nh.mplsAction = *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
-                                                                         : mpls(kSwap, label);
-              entry.nexthops.insert(std::move(nh));
-            }
-          }
-        }
+        for (uint32_t k = 0; k < tw->words; ++k) any |= vm[k] != 0;
+        if (any)  // one area: its words start at 0
+          insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops,
+                          [&](const NextHopThrift& nh) -> std::optional<MplsAction> {
+                            return *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
+                                                                              : mpls(kSwap, label);
+                          });
         if (!any) return;
       } else {
         const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};

@@ -316,8 +316,23 @@ class SpfSolver {
     // per first-hop bit: tight up links of me to that neighbour as nexthop
     // templates (metric set per route), v6 and v4 addresses
     std::vector<std::vector<NextHopThrift>> tmpl6, tmpl4;
+    // the templates in my LinkSet iteration order as (bit, index in
+    // tmpl[bit]): getNextHopsThrift's insertion order (Decision.cpp:1245-1246)
+    std::vector<std::pair<uint32_t, uint32_t>> linkOrder;
   };
   std::vector<AreaWork> areaWork_;
+  // areaWork_ indices in AreaLinkStates iteration order (the reference's
+  // outer loop over areaLinkStates, Decision.cpp:1245)
+  std::vector<uint32_t> areaIter_;
+  // inserts the nexthops of first-hop mask m (indexed by each area's
+  // wordOff) in the reference's order with the given metric and weight 0,
+  // the MPLS action act(template); with wt, each inserted element's weight
+  // under wt[area][bit] is recorded in *wts (by element address)
+  template <class Act>
+  void insertTemplates(const uint32_t* m, bool v4, int32_t metric,
+                       const std::vector<std::vector<int32_t>>* wt,
+                       std::vector<std::pair<const NextHopThrift*, int32_t>>* wts, NextHopSet& out,
+                       Act&& act) const;
   orh_ctx* selCtx_{nullptr};
   uint8_t* dSel_{nullptr};  // status | metric | best | mask
   size_t dSelCap_{0};

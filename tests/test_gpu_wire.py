@@ -124,3 +124,66 @@ def test_route_delta_bytes_c5_policy(hip, oracle):
         als_h[a].update_adjacency_database(db)
         als_o[a].update_adjacency_database(db)
     assert rib.delta_rebuilds >= 1
+
+
+def _lists(wire):
+    """prefix / label -> the nexthop list in the backend's unordered_set
+    iteration order (what DecisionRouteDb::toThrift would list)."""
+    uc = {(r[0], r[1]): [tuple(n) for n in r[2]] for r in wire[0]}
+    mp = {m[0]: [tuple(n) for n in m[1]] for m in wire[1]}
+    return uc, mp
+
+
+def _ksp2_random(seed):
+    dbs = random_topology(6200 + seed, n=20, extra=30, parallel=0.4)
+    rng = random.Random(seed)
+    pfx = []
+    for i in range(60):
+        for db in rng.sample(dbs, rng.randint(1, 3)):
+            e = create_prefix_entry(IpPrefix.of(f"fc00:{seed}::{i:x}/128"))
+            if rng.random() < 0.5:
+                e.forwardingType = PrefixForwardingType.SR_MPLS
+                if rng.random() < 0.6:
+                    e.forwardingAlgorithm = PrefixForwardingAlgorithm.KSP2_ED_ECMP
+            pfx.append((db.thisNodeName, K_TESTING_AREA, e))
+    return dbs, pfx, sorted(db.thisNodeName for db in dbs)[seed]
+
+
+@pytest.mark.parametrize("case", ["c1", "c3", "ksp2_0", "ksp2_1", "c5_policy"])
+def test_nexthop_list_order(hip, oracle, case):
+    """every route's nexthops iterate - and toThrift would
+    list them - in the oracle's order, i.e. std::unordered_set<NextHopThrift>
+    with std::hash<NextHopThrift> (NetworkUtil.cpp:24-66) filled in the
+    reference's insertion sequence: getNextHopsThrift's area / LinkSet loops
+    (Decision.cpp:1245-1246, parallel links included), KSP2 paths, node-label
+    SWAP / PHP routes, and RibPolicy's rebuild of a transformed route
+    (RibPolicy.cpp:116-141). Routes built on the device (selection + template
+    materialisation) and on the host path alike."""
+    me, policy = "1", None
+    if case == "c1":
+        adj, pfx = bench_grid(10, 1)
+    elif case == "c3":
+        adj, pfx = c3_fabric(num_prefixes=3000)
+        me = "2-0-0"
+    elif case.startswith("ksp2"):
+        adj, pfx, me = _ksp2_random(int(case[-1]))
+    else:
+        areas, pfx = c5_multi_area(num_prefixes=3000)
+        adj = [db for a in C5_AREAS for db in areas[a]]
+        me, policy = "me", _ucmp()
+    als_h, ps_h = load_topology(hip, adj, pfx)
+    als_o, ps_o = load_topology(oracle, adj, pfx)
+    best = case == "c5_policy"
+    sh = hip.spf_solver(me, True, enable_best_route_selection=best)._impl
+    so = oracle.spf_solver(me, True, enable_best_route_selection=best)._impl
+    if policy:
+        wh = sh.build_route_db_with_policy(me, als_h._impl, ps_h._impl, hip.rib_policy(policy, 3600)._impl)
+        wo = so.build_route_db_with_policy(me, als_o._impl, ps_o._impl, oracle.rib_policy(policy, 3600)._impl)
+    else:
+        wh = sh.build_route_db(me, als_h._impl, ps_h._impl)
+        wo = so.build_route_db(me, als_o._impl, ps_o._impl)
+    (uh, mh), (uo, mo) = _lists(wh), _lists(wo)
+    assert uh.keys() == uo.keys() and mh.keys() == mo.keys()
+    bad = [k for k in uo if uh[k] != uo[k]] + [k for k in mo if mh[k] != mo[k]]
+    assert not bad, f"{len(bad)} of {len(uo) + len(mo)} routes list their nexthops in another order, e.g. {bad[0]}"
+    assert sum(len(v) > 1 for v in list(uo.values()) + list(mo.values())) > 10  # orders that can differ
