@@ -1917,10 +1917,28 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
     for (uint32_t word = 0; word < W; ++word) {
       uint32_t acc[kLvlPer] = {};
       uint32_t pk[kWords] = {};  // byte k of word q: mask bits 0..7 of node 4q + k (packed path)
-      for (uint32_t e = 0; e < ne; ++e) {
-        const uint4 en = ent[e];
+      // the neighbour rows of kGroup entries are loaded back to back before
+      // any is used: one memory round trip per group, not per entry (the
+      // loads of a dynamic-length loop are otherwise issued one at a time)
+      constexpr uint32_t kGroup = 4;
+      for (uint32_t e0 = 0; e0 < ne; e0 += kGroup) {
+      uint4 ens[kGroup];
+      Vec nxs[kGroup];
+      uint32_t use = 0;  // bit g: entry e0 + g belongs to this word
+#pragma unroll
+      for (uint32_t g = 0; g < kGroup; ++g) {
+        if (e0 + g >= ne) break;
+        ens[g] = ent[e0 + g];
+        if (((ens[g].w & 0x7FFFFFFFu) >> 5) != word) continue;
+        use |= 1u << g;
+        if (!(ens[g].w & 0x80000000u))
+          nxs[g] = *reinterpret_cast<const Vec*>(a.lvl_rows + static_cast<size_t>(ens[g].z) * P + v0);
+      }
+#pragma unroll
+      for (uint32_t g = 0; g < kGroup; ++g) {
+        if (!((use >> g) & 1u)) continue;
+        const uint4 en = ens[g];
         const uint32_t r = en.w & 0x7FFFFFFFu;
-        if ((r >> 5) != word) continue;
         const uint32_t bit = 1u << (r & 31u);
         if (en.x >= v0 && en.x < v0 + kLvlPer) {
 #pragma unroll
@@ -1928,7 +1946,7 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
             if (v0 + k == en.x && dv[k] != kInf) acc[k] |= bit;
         }
         if (en.w & 0x80000000u) continue;  // overloaded neighbour: no transit
-        const Vec nx = *reinterpret_cast<const Vec*>(a.lvl_rows + static_cast<size_t>(en.z) * P + v0);
+        const Vec nx = nxs[g];
         uint32_t nw[kWords];
         words_of(nx, nw);
         bool direct = own_direct || en.y != w0;
@@ -1958,6 +1976,7 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
           }
         }
       }
+      }  // entry group
 #pragma unroll
       for (uint32_t k = 0; k < kLvlPer; ++k) acc[k] |= (pk[k / 4] >> ((k & 3u) * 8u)) & 0xFFu;
       if (kLvlPer == 16 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
