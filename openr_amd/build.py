@@ -30,7 +30,7 @@ HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "sp
             os.path.join(CSRC, "kernels", "ksp_kernels.hip")]
 HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "prefix_state.cpp", "spf_solver.cpp",
                                                    "rib_policy.cpp", "thrift_compact.cpp",
-                                                   "decision_ingest.cpp", "host_py.cpp")]
+                                                   "decision_ingest.cpp", "multi_device.cpp", "host_py.cpp")]
 
 
 def _hipcc() -> str:

@@ -13,6 +13,7 @@
 #include "rib_policy.h"
 #include "spf_solver.h"
 #include "decision_ingest.h"
+#include "multi_device.h"
 #include "thrift_compact.h"
 
 namespace py = pybind11;
@@ -933,6 +934,48 @@ PYBIND11_MODULE(_openr_host, m) {
       .def_property_readonly("nodes", &SpfSweep::nodes)
       .def_property_readonly("edges", &SpfSweep::edges)
       .def_property_readonly("sources", &SpfSweep::sources);
+
+  // one topology on several devices, the all-sources SPF split over them
+  // (multi_device.h; SURVEY.md §8e inside the library, no torch)
+  py::class_<ReplicatedLinkState>(m, "ReplicatedLinkState")
+      .def(py::init<const std::string&, const std::vector<int>&>(), py::arg("area"), py::arg("devices"))
+      .def("update_adjacency_database",
+           [](ReplicatedLinkState& s, py::tuple db, uint64_t up, uint64_t down) {
+             return changeToWire(s.updateAdjacencyDatabase(adjDbFromWire(db), up, down));
+           },
+           py::arg("db"), py::arg("hold_up_ttl") = 0, py::arg("hold_down_ttl") = 0)
+      .def("delete_adjacency_database",
+           [](ReplicatedLinkState& s, const std::string& n) { return changeToWire(s.deleteAdjacencyDatabase(n)); })
+      .def("decrement_holds", [](ReplicatedLinkState& s) { return changeToWire(s.decrementHolds()); })
+      .def_property_readonly("replicas", &ReplicatedLinkState::replicas)
+      .def("replica", &ReplicatedLinkState::replica, py::return_value_policy::reference_internal)
+      .def("sweep",
+           [](const ReplicatedLinkState& s, const std::vector<std::string>& srcs, bool useLinkMetric) {
+             return new MultiDeviceSweep(s, srcs, useLinkMetric);
+           },
+           py::arg("srcs"), py::arg("use_link_metric") = true, py::return_value_policy::take_ownership,
+           py::keep_alive<0, 1>());
+  py::class_<MultiDeviceSweep>(m, "MultiDeviceSweep")
+      .def("run", &MultiDeviceSweep::run)
+      .def("sync", &MultiDeviceSweep::sync)
+      .def("last_ms", &MultiDeviceSweep::lastMs, py::arg("block"))
+      .def("block", &MultiDeviceSweep::block)
+      .def_property_readonly("blocks", &MultiDeviceSweep::blocks)
+      .def_property_readonly("sources", &MultiDeviceSweep::sources)
+      .def_property_readonly("nodes", &MultiDeviceSweep::nodes)
+      .def_property_readonly("words", &MultiDeviceSweep::words)
+      .def("fetch",
+           [](const MultiDeviceSweep& s, size_t i) {
+             py::array_t<uint32_t> dist(s.nodes()), nh(static_cast<size_t>(s.nodes()) * s.words());
+             s.fetch(i, dist.mutable_data(), nh.mutable_data());
+             return py::make_tuple(dist, nh);
+           })
+      .def("gather", [](const MultiDeviceSweep& s) {
+        py::array_t<uint32_t> dist({s.sources(), static_cast<size_t>(s.nodes())});
+        py::array_t<uint32_t> nh({s.sources(), static_cast<size_t>(s.nodes()) * s.words()});
+        s.gather(dist.mutable_data(), nh.mutable_data());
+        return py::make_tuple(dist, nh);
+      });
 
   py::class_<WhatIfBatch>(m, "WhatIfBatch")
       .def("run", &WhatIfBatch::run)

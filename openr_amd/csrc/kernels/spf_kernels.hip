@@ -1920,7 +1920,10 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
       // the neighbour rows of kGroup entries are loaded back to back before
       // any is used: one memory round trip per group, not per entry (the
       // loads of a dynamic-length loop are otherwise issued one at a time)
-      constexpr uint32_t kGroup = 4;
+#ifndef ORH_HOP_GROUP
+#define ORH_HOP_GROUP 4  // (1: one entry per round trip, the round-3 loop; A/B builds)
+#endif
+      constexpr uint32_t kGroup = ORH_HOP_GROUP;
       for (uint32_t e0 = 0; e0 < ne; e0 += kGroup) {
       uint4 ens[kGroup];
       Vec nxs[kGroup];

@@ -149,7 +149,7 @@ def _ksp2_random(seed):
     return dbs, pfx, sorted(db.thisNodeName for db in dbs)[seed]
 
 
-@pytest.mark.parametrize("case", ["c1", "c3", "ksp2_0", "ksp2_1", "c5_policy"])
+@pytest.mark.parametrize("case", ["c1", "c3", "ksp2_0", "ksp2_1", "c5_policy", "c3_policy"])
 def test_nexthop_list_order(hip, oracle, case):
     """every route's nexthops iterate - and toThrift would
     list them - in the oracle's order, i.e. std::unordered_set<NextHopThrift>
@@ -167,13 +167,22 @@ def test_nexthop_list_order(hip, oracle, case):
         me = "2-0-0"
     elif case.startswith("ksp2"):
         adj, pfx, me = _ksp2_random(int(case[-1]))
-    else:
+    elif case == "c5_policy":
         areas, pfx = c5_multi_area(num_prefixes=3000)
         adj = [db for a in C5_AREAS for db in areas[a]]
         me, policy = "me", _ucmp()
+    else:  # ~36-way ECMP routes rebuilt by a policy: some neighbours dropped, others reweighted
+        from openr_amd.rib_policy import RibPolicyStatement, RibRouteActionWeight
+        adj, pfx = c3_fabric(num_prefixes=3000)
+        me = "2-0-0"
+        nbrs = sorted({a.otherNodeName for db in adj if db.thisNodeName == me for a in db.adjacencies})
+        rng = random.Random(77)
+        weights = {n: rng.choice([0, 1, 3, 5]) for n in rng.sample(nbrs, len(nbrs) // 2)}
+        some = rng.sample(sorted({e.prefix for _, _, e in pfx}, key=str), 1500)
+        policy = [RibPolicyStatement("nbr", some, None, RibRouteActionWeight(2, {}, weights))]
     als_h, ps_h = load_topology(hip, adj, pfx)
     als_o, ps_o = load_topology(oracle, adj, pfx)
-    best = case == "c5_policy"
+    best = case.endswith("policy")
     sh = hip.spf_solver(me, True, enable_best_route_selection=best)._impl
     so = oracle.spf_solver(me, True, enable_best_route_selection=best)._impl
     if policy:
@@ -186,4 +195,5 @@ def test_nexthop_list_order(hip, oracle, case):
     assert uh.keys() == uo.keys() and mh.keys() == mo.keys()
     bad = [k for k in uo if uh[k] != uo[k]] + [k for k in mo if mh[k] != mo[k]]
     assert not bad, f"{len(bad)} of {len(uo) + len(mo)} routes list their nexthops in another order, e.g. {bad[0]}"
-    assert sum(len(v) > 1 for v in list(uo.values()) + list(mo.values())) > 10  # orders that can differ
+    if case != "c5_policy":  # (C5's `me` has one link per area: single-nexthop routes)
+        assert sum(len(v) > 1 for v in list(uo.values()) + list(mo.values())) >= 5  # orders that can differ
