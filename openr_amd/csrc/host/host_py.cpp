@@ -957,6 +957,7 @@ PYBIND11_MODULE(_openr_host, m) {
            py::keep_alive<0, 1>());
   py::class_<MultiDeviceSweep>(m, "MultiDeviceSweep")
       .def("run", &MultiDeviceSweep::run)
+      .def("run_block", &MultiDeviceSweep::runBlock, py::arg("block"))
       .def("sync", &MultiDeviceSweep::sync)
       .def("last_ms", &MultiDeviceSweep::lastMs, py::arg("block"))
       .def("block", &MultiDeviceSweep::block)

@@ -134,15 +134,18 @@ MultiDeviceSweep::~MultiDeviceSweep() {
   }
 }
 
+void MultiDeviceSweep::runBlock(size_t r) {
+  Block& b = blocks_.at(r);
+  if (b.srcs.empty()) return;
+  orh_spf_request req{};
+  req.h_srcs = b.srcs.data();
+  req.n_src = static_cast<uint32_t>(b.srcs.size());
+  req.use_link_metric = useLinkMetric_ ? 1 : 0;
+  check(b.ctx, orh_spf_run(b.g, &req, words_, b.dDist, b.dNh), "orh_spf_run");
+}
+
 void MultiDeviceSweep::run() {
-  for (auto& b : blocks_) {
-    if (b.srcs.empty()) continue;
-    orh_spf_request req{};
-    req.h_srcs = b.srcs.data();
-    req.n_src = static_cast<uint32_t>(b.srcs.size());
-    req.use_link_metric = useLinkMetric_ ? 1 : 0;
-    check(b.ctx, orh_spf_run(b.g, &req, words_, b.dDist, b.dNh), "orh_spf_run");
-  }
+  for (size_t r = 0; r < blocks_.size(); ++r) runBlock(r);
 }
 
 void MultiDeviceSweep::sync() {

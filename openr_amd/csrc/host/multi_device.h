@@ -56,6 +56,7 @@ class MultiDeviceSweep {
   MultiDeviceSweep& operator=(const MultiDeviceSweep&) = delete;
 
   void run();   // every block, asynchronously on its device's stream
+  void runBlock(size_t r);  // block r alone (per-device timing, rehearsals on one GPU)
   void sync();  // waits for every device
   size_t sources() const { return total_; }
   uint32_t nodes() const { return n_; }

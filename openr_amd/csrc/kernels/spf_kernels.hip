@@ -372,7 +372,7 @@ __device__ inline uint32_t wave_or(uint32_t v) {
 }
 
 template <int K, class M, int J, bool kSkip>
-__global__ __launch_bounds__(768) void spf_msbfs_kernel(SpfArgs a) {
+__global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t kS = MsMask<M>::kS;
   typedef typename MsMask<M>::V V;
@@ -2161,6 +2161,20 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
   // batches: the batches that share a CU are not the slow ones
   // (per-workgroup stamps, profiles/r02/msbfs_ab.md), and u64 masks cost more
   // per level than they save
+  // latency plan: when every batch has a CU to itself (a sweep over a shard
+  // of the sources, N GPUs sharing one topology), the per-level time of one
+  // workgroup is the sweep time, so the batch gets 1024 threads (fewer nodes
+  // per thread: J = 12 instead of 20 on the 10k grid). ORH_MS_LATENCY=0: off
+  {
+    const char* lat = getenv("ORH_MS_LATENCY");
+    const uint32_t batches = (n_rows + plan.mask_bytes * 8 - 1) / (plan.mask_bytes * 8);
+    const uint32_t j = (n_nodes + 1023) / 1024;
+    if (!(lat && atoi(lat) == 0) && !getenv("ORH_MS_BLOCK") && n_cu && batches <= n_cu &&
+        plan.block < 1024 && j <= 32) {
+      plan.block = 1024;
+      plan.ms_j = (j + 3) & ~3u;
+    }
+  }
   const size_t bytes64 = 2 * 8 * static_cast<size_t>(plan.ms_pitch);
   const char* e = getenv("ORH_MS_WIDE");
   const bool allow = e && atoi(e) == 1;
