@@ -58,6 +58,9 @@ struct SpfArgs {
   const uint32_t* row_count;
   // HBM kernel (kGlobalNh plan): distances only, u32 labels, out_nh unused
   int32_t dist_only;
+  // u16 LDS search (launch_spf_lds16): [0] count, then the rows it left to
+  // the HBM kernel (a distance that needs 17 bits)
+  uint32_t* ovf_rows;
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -161,6 +164,12 @@ struct SpfPlan {
 SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t ell_k,
                  size_t lds_limit, bool multi_source, SpfMode mode);
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s);
+// distances only, one search per CU with u16 distances in LDS
+// (spf_lds16_kernel), rows it cannot finish re-run by `fallback` (a kGlobalNh
+// plan) over the list a.ovf_rows (n_rows + 1 words); needs a.dist_only
+size_t lds16_bytes(uint32_t n_nodes);
+hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows, uint32_t ell_k,
+                            hipStream_t s);
 // multi-source plans, once the row count is known: sources per batch, and
 // u64 masks when u32 ones would put more than one batch on a CU
 void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit);

@@ -744,6 +744,13 @@ __global__ __launch_bounds__(kMaxBlock) void spf_bfs_nh_kernel(SpfArgs a) {
     int prog = 0;
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
+    // the packed columns are opaque per level: otherwise the compiler hoists
+    // their unpacked halves and the neighbour addresses out of the level loop
+    // (4 x the registers of col per owned node, spilling at J >= 8)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int h = 0; h < KH; ++h) asm volatile("" : "+v"(col[j][h]));
     // every owned unsettled node's level in one batch of independent reads
     uint32_t lv[J];
 #pragma unroll
@@ -1390,6 +1397,219 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
         on[static_cast<size_t>(i) * a.words] = lab_nh(l);
         for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// phase 1c'': the asynchronous delta-stepping search with u16 distances in LDS
+// ---------------------------------------------------------------------------
+// Distances only (KSP2 searches): the async kernel above with its labels moved
+// from HBM into LDS as u16 pairs (two nodes per word, lowered by
+// compare-and-swap), so the 50k-node WAN of C4 (100 KB of distances + 12.5 KB
+// of near / far bitmaps) keeps a whole search on one CU. Relaxation chains
+// then pay LDS latency instead of a global atomic per hop; only the edge
+// records (read-only, shared by every search, L2-resident) come from memory.
+// A candidate of 0xFFFF or more is not representable: it is dropped and the
+// row flagged. The result is still exact unless a node ends unreached (a
+// dropped candidate was larger than any finite distance the node ends with,
+// and a node whose true distance needs 17 bits leaves itself unreached), so a
+// flagged row with an unreached node is queued in ovf_rows for the HBM kernel
+// (launch_spf_lds16 runs it over that list).
+template <int K>
+__global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf, s_inf;
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  const uint32_t row = blockIdx.x;
+  if (a.row_mask && !a.row_mask[row]) return;
+  constexpr int G = K <= 4 ? 4 : 2;
+  const uint32_t DWp = ((N + 1) / 2 + 3) & ~3u;
+  uint32_t* dist = lds;  // node u: bits 16 (u & 1) .. of word u / 2; 0xFFFF unreached
+  uint32_t* near = lds + DWp;
+  uint32_t* far = near + NB;
+  uint32_t* filt = far + NB;
+  uint32_t FW = 1;
+  while (2 * FW <= min(NB, 256u)) FW *= 2;
+  const uint32_t fshift = 32u - (5u + static_cast<uint32_t>(__builtin_ctz(FW)));
+  Src s(a, row);
+  for (uint32_t i = tid; i < DWp; i += nthr) dist[i] = 0xFFFFFFFFu;
+  for (uint32_t i = tid; i < 2 * NB; i += nthr) near[i] = 0u;
+  if (s.n_ign)
+    for (uint32_t i = tid; i < FW; i += nthr) filt[i] = 0u;
+  if (tid < 2) s_min[tid] = kInf;
+  if (tid == 0) {
+    s_nign = 0u;
+    s_ovf = 0u;
+    s_inf = 0u;
+  }
+  __syncthreads();
+  if (s.n_ign) {
+    for (uint32_t i = tid; i < s.n_ign; i += nthr) {
+      const uint32_t l = s.ign[i];
+      if (l == 0xFFFFFFFFu) continue;
+      atomicAdd(&s_nign, 1u);
+      const uint32_t h = ign_hash(l, fshift);
+      atomicOr(&filt[h >> 5], 1u << (h & 31u));
+    }
+    __syncthreads();
+    s.n_ign = s_nign;  // sorted: the real entries come first
+    s.filt = filt;
+    s.fshift = fshift;
+  }
+  if (tid == 0) {
+    dist[s.node >> 1] &= ~(0xFFFFu << ((s.node & 1u) * 16u));
+    near[s.node >> 5] = 1u << (s.node & 31u);
+    s_work = 1u;
+  }
+  __syncthreads();
+  auto get = [&](uint32_t u) { return (dist[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu; };
+
+  const uint32_t delta = a.delta;
+  uint32_t T = delta;
+  uint32_t mpar = 0;
+  bool ovf = false;
+  for (;;) {
+    uint32_t far_min = kInf;
+    // lower u to nd, starting from the word w as read; queue it if lowered
+    auto merge = [&](uint32_t u, uint32_t nd, uint32_t w) {
+      const uint32_t sh = (u & 1u) * 16u;
+      if (nd >= ((w >> sh) & 0xFFFFu)) return;
+      if (nd >= 0xFFFFu) {
+        ovf = true;
+        return;
+      }
+      for (;;) {
+        const uint32_t nw = (w & ~(0xFFFFu << sh)) | (nd << sh);
+        const uint32_t prev = atomicCAS(&dist[u >> 1], w, nw);
+        if (prev == w) break;
+        w = prev;
+        if (nd >= ((w >> sh) & 0xFFFFu)) return;  // lowered further meanwhile
+      }
+      const uint32_t bit = 1u << (u & 31u);
+      if (nd < T) {
+        atomicAdd(&s_work, 1u);  // counted before the bit is visible
+        const uint32_t old = atomicOr(&near[u >> 5], bit);
+        atomicAnd(&far[u >> 5], ~bit);
+        if (old & bit) atomicSub(&s_work, 1u);  // already queued
+      } else {
+        atomicOr(&far[u >> 5], bit);
+        far_min = min(far_min, nd);
+      }
+    };
+    uint32_t wi = tid, bits = 0, wbase = 0;
+    for (;;) {
+      uint32_t vs[G];
+      int c = 0;
+      while (c < G) {
+        while (!bits && wi < NB) {
+          bits = __hip_atomic_load(&near[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (bits) bits = atomicExch(&near[wi], 0u);  // at least the bits seen: only we clear
+          wbase = wi * 32;
+          wi += nthr;
+        }
+        if (!bits) break;
+        vs[c++] = wbase + __builtin_ctz(bits);
+        bits &= bits - 1;
+      }
+      if (!bits && wi >= NB) wi = tid;  // words exhausted: rescan them next time
+      if (__builtin_amdgcn_ballot_w64(c > 0) == 0ull) {
+        const uint32_t pending = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&s_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (pending == 0u) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (c > 0) {
+        // the group's records in flight together, then the neighbours' words
+        uint2 rec[G][K];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (g < c) load_recs<K>(a, vs[g], rec[g]);
+        uint32_t dv[G], nw[G][K];
+        bool ok[G][K];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          dv[g] = g < c ? get(vs[g]) : 0u;
+          const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
+            nw[g][j] = ok[g][j] ? dist[(rec[g][j].x & ORH_REC_COL_MASK) >> 1] : 0u;
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (g >= c) break;
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (ok[g][j])
+              merge(rec[g][j].x & ORH_REC_COL_MASK, dv[g] + (a.use_link_metric ? rec[g][j].y : 1u), nw[g][j]);
+          const uint2 last = rec[g][K - 1];
+          const bool transit = vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL);
+          if (transit && (last.x & ORH_REC_CONT)) {
+            const uint32_t start = last.x & ORH_REC_COL_MASK;
+            for (uint32_t q = 0; q < last.y; ++q) {
+              const uint2 r = a.recs[start + q];
+              if (!live(a, s, r, start + q)) continue;
+              const uint32_t u = r.x & ORH_REC_COL_MASK;
+              merge(u, dv[g] + (a.use_link_metric ? r.y : 1u), dist[u >> 1]);
+            }
+          }
+        }
+        atomicSub(&s_work, static_cast<uint32_t>(c));
+      }
+    }
+    {
+      const uint32_t fm = wave_min(far_min);
+      if ((tid & 63u) == 0 && fm != kInf) atomicMin(&s_min[mpar], fm);
+    }
+    __syncthreads();  // bucket drained everywhere; far bound folded
+    const uint32_t m = s_min[mpar];
+    if (m == kInf) break;  // far set empty: done
+    T = m + delta;
+    const uint32_t npar = mpar ^ 1u;
+    if (tid == 0) s_min[npar] = kInf;
+    __syncthreads();
+    uint32_t local_min = kInf, promoted = 0;
+    for (uint32_t w2 = tid; w2 < NB; w2 += nthr) {
+      const uint32_t fb = far[w2];
+      uint32_t promote = 0u;
+      for (uint32_t q = fb; q; q &= q - 1) {
+        const uint32_t b = __builtin_ctz(q);
+        const uint32_t d = get(w2 * 32 + b);
+        if (d < T) promote |= 1u << b;
+        else local_min = min(local_min, d);
+      }
+      if (promote) {
+        far[w2] = fb & ~promote;
+        near[w2] = promote;  // the near set is empty between buckets
+        promoted += __builtin_popcount(promote);
+      }
+    }
+    if (promoted) atomicAdd(&s_work, promoted);
+    const uint32_t wm = wave_min(local_min);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
+    mpar = npar;
+    __syncthreads();
+  }
+  if (ovf) s_ovf = 1u;
+  __syncthreads();
+  uint32_t* od = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+  bool inf = false;
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const uint32_t d = get(i);
+    inf |= d == 0xFFFFu;
+    __builtin_nontemporal_store(d == 0xFFFFu ? kInf : d, &od[i]);
+  }
+  if (s_ovf) {  // exact unless a node ended unreached: then the HBM kernel redoes the row
+    if (inf) s_inf = 1u;
+    __syncthreads();
+    if (tid == 0 && s_inf) {
+      const uint32_t k = atomicAdd(&a.ovf_rows[0], 1u);
+      a.ovf_rows[1 + k] = row;
     }
   }
 }
@@ -2250,6 +2470,38 @@ static hipError_t launch_bfs_nh(const SpfArgs& a, uint32_t n_rows, uint32_t bloc
     case 32: return launch(spf_bfs_nh_kernel<K, 32>, a, n_rows, block, lds, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+size_t lds16_bytes(uint32_t n_nodes) {
+  const size_t nb = (n_nodes + 31) / 32;
+  size_t fw = 1;
+  while (2 * fw <= std::min<size_t>(nb, 256)) fw *= 2;
+  return 4 * ((((n_nodes + 1) / 2 + 3) & ~size_t{3}) + 2 * nb + fw);
+}
+
+hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows, uint32_t ell_k,
+                            hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  if (!a.ovf_rows || !a.dist_only || fallback.variant != SpfVariant::kGlobalNh) return hipErrorInvalidValue;
+  a.n_rows = n_rows;
+  const size_t lds = lds16_bytes(a.n_nodes);
+  hipError_t e = hipMemsetAsync(a.ovf_rows, 0, 4, s);
+  if (e != hipSuccess) return e;
+  // ORH_LDS16_BLOCK (A/B): threads per search (one search per CU either way)
+  static const uint32_t block = [] {
+    const char* v = getenv("ORH_LDS16_BLOCK");
+    const int b = v ? atoi(v) : 1024;
+    return (b >= 64 && b <= 1024 && b % 64 == 0) ? static_cast<uint32_t>(b) : 1024u;
+  }();
+  e = ell_k == 8 ? launch(spf_lds16_kernel<8>, a, n_rows, block, lds, s)
+                 : launch(spf_lds16_kernel<4>, a, n_rows, block, lds, s);
+  if (e != hipSuccess) return e;
+  // rows the u16 search could not finish: the HBM kernel over that list
+  // (workgroups past the list's length exit at once)
+  SpfArgs b = a;
+  b.row_list = a.ovf_rows + 1;
+  b.row_count = a.ovf_rows;
+  return launch_spf(fallback, b, n_rows, s);
 }
 
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {

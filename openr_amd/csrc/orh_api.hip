@@ -2522,6 +2522,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     const size_t o_ign = take(size_t{P} * kKspIgnCap), o_need = take(P), o_out = take(size_t{P} * kKspOutCap);
     const size_t o_vis = take(size_t{P} * kKspHashCap);
     const size_t o_st = take(size_t{P} * kKspStackCap * (sizeof(orh::KspFrame) / 4));
+    const size_t o_ovf = take(size_t{std::max(S, P)} + 1);
     rc = ensure_bytes(ctx, &ctx->d_ksp, &ctx->d_ksp_cap, off * 4);
     if (rc) return rc;
     uint32_t* D = reinterpret_cast<uint32_t*>(ctx->d_ksp);
@@ -2541,6 +2542,16 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
       return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: no search plan for this graph");
     fp.variant = orh::SpfVariant::kGlobalNh;
     auto block_for = [&](uint32_t rows) { return rows <= ctx->n_cu ? 1024u : rows <= 2 * ctx->n_cu ? 512u : 256u; };
+    // one search per CU with u16 distances in LDS when they fit (the HBM
+    // kernel finishes any row that needs wider distances); ORH_KSP_LDS=0: the
+    // HBM kernel for every row (A/B)
+    const char* lds_e = getenv("ORH_KSP_LDS");
+    const bool lds_env = !(lds_e && lds_e[0] == '0');
+    const bool use_lds16 = lds_env && orh::lds16_bytes(N) <= ctx->lds_limit;
+    auto search = [&](const orh::SpfArgs& sa, uint32_t rows) {
+      return use_lds16 ? orh::launch_spf_lds16(fp, sa, rows, g->ell_k, ctx->stream)
+                       : orh::launch_spf(fp, sa, rows, ctx->stream);
+    };
     rc = ensure_labels(ctx, (std::max(nd1, nd2) + 1) / 2);  // u64 units, u32 labels
     if (rc) return rc;
     orh::SpfArgs a{};
@@ -2557,6 +2568,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.words = 1;
     a.rank_out = g->d_rank_out;
     a.dist_only = 1;
+    a.ovf_rows = D + o_ovf;
     // k = 1 rows: the sources' plain SPFs (LinkState::getSpfResult)
     a.n_out = S;
     a.srcs = D + o_s1;
@@ -2564,7 +2576,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     fp.block = block_for(S);
     const orh_counters c_before = ctx->counters;
     mark(1);
-    hipError_t e = orh::launch_spf(fp, a, S, ctx->stream);
+    hipError_t e = search(a, S);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=1 search launch");
     mark(2);
     orh::KspArgs ka{};
@@ -2600,7 +2612,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.out_dist = D + o_d2;
     a.row_mask = D + o_need;
     fp.block = block_for(P);
-    e = orh::launch_spf(fp, a, P, ctx->stream);
+    e = search(a, P);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
     mark(4);
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
@@ -2624,6 +2636,11 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
       }
       std::fprintf(stderr, "ksp-batch after copy-out sync host %8.3f ms\n",
                    std::chrono::duration<double, std::milli>(h_now() - t_host).count());
+      if (use_lds16) {
+        uint32_t n_ovf = 0;
+        ORH_HIP(ctx, hipMemcpy(&n_ovf, D + o_ovf, 4, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "ksp-batch lds16: %u of %u k=2 rows re-run by the HBM kernel\n", n_ovf, P);
+      }
       for (double& h : host_ms) h = 0;
     }
   }

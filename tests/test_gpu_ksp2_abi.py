@@ -187,3 +187,46 @@ def test_kth_paths_link_handles(hip, oracle):
                     assert cur == dst
                     assert nh6 == adj[(src, if0)].nextHopV6.addr
     assert walked > 50
+
+
+@pytest.mark.parametrize("lds", ["1", "0"])
+@pytest.mark.parametrize("seed,lo,hi", [(2300, 1, 5), (2301, 20000, 40000)])
+def test_ksp2_device_batch_lds16(hip, oracle, monkeypatch, lds, seed, lo, hi):
+    """The batch's k = 1 / k = 2 searches with u16 distances in LDS
+    (spf_lds16_kernel, the default when a graph fits) and with the HBM kernel
+    alone (ORH_KSP_LDS=0). At metrics 20,000-40,000 a path of two or three
+    links needs 17 bits: those rows leave nodes unreached in the u16 search
+    and are re-run by the HBM kernel from the fallback list. Every pair
+    equals the oracle's getKthPaths."""
+    monkeypatch.setenv("ORH_KSP_LDS", lds)
+    dbs = random_topology(seed, n=22, extra=36, min_metric=lo, max_metric=hi, parallel=0.4,
+                          overload=0.1, link_overload=0.06)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    names = sorted(db.thisNodeName for db in dbs)
+    pairs = [(s, d) for s in names for d in names]
+    ls = als_h[A]._impl
+    ls.prefetch_kth_paths(pairs)
+    assert ls.ksp_stats() == (len(pairs), 0)
+    for s, d in pairs:
+        for k in (1, 2):
+            assert als_h[A].get_kth_paths(s, d, k) == als_o[A].get_kth_paths(s, d, k), (s, d, k)
+
+
+def test_ksp2_c4_lds16_vs_hbm(hip, monkeypatch):
+    """The benched C4 batch (1,024 pairs on the 50k-node WAN) through the u16
+    LDS searches and through the HBM kernel alone: the same paths for every
+    pair, k = 1 and k = 2 (the HBM path is pinned to the oracle above)."""
+    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan
+    adj, _ = c4_wan()
+    got = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("ORH_KSP_LDS", lds)
+        als_h, _ = load_topology(hip, adj, [])
+        ls = als_h[A]._impl
+        pairs = c4_ksp2_pairs(ls.node_names(), C4_KSP2_PAIRS)
+        ls.prefetch_kth_paths(pairs)
+        assert ls.ksp_stats() == (len(set(pairs)), 0)
+        got.append({(s, d, k): als_h[A].get_kth_paths(s, d, k) for s, d in pairs for k in (1, 2)})
+    assert got[0] == got[1]
+    assert sum(len(v) for v in got[0].values()) > C4_KSP2_PAIRS
