@@ -1476,11 +1476,11 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     // lower u to nd, starting from the word w as read; queue it if lowered
     auto merge = [&](uint32_t u, uint32_t nd, uint32_t w) {
       const uint32_t sh = (u & 1u) * 16u;
-      if (nd >= ((w >> sh) & 0xFFFFu)) return;
-      if (nd >= 0xFFFFu) {
+      if (nd >= 0xFFFFu) {  // before the compare: an unreached node holds 0xFFFF too
         ovf = true;
         return;
       }
+      if (nd >= ((w >> sh) & 0xFFFFu)) return;
       for (;;) {
         const uint32_t nw = (w & ~(0xFFFFu << sh)) | (nd << sh);
         const uint32_t prev = atomicCAS(&dist[u >> 1], w, nw);
@@ -2113,17 +2113,11 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
     bool own_direct = false;
 #pragma unroll
     for (uint32_t q = 0; q < kWords; ++q) own_direct |= has_byte_fe(ow[q]);
-    uint32_t dv[kLvlPer], ls[kLvlPer];
-#pragma unroll
-    for (uint32_t k = 0; k < kLvlPer; ++k) {
-      if (v0 + k == src || v0 + k >= N) {  // the source has no next hops
-        dv[k] = kInf;
-        ls[k] = kLvlNone;
-      } else {
-        dv[k] = dist_at(i, own, k);
-        ls[k] = LvlVec<kLvlPer>::byte(own, k);
-      }
-    }
+    // d_s(v0 + k) where needed (the direct path; kInf: the source, which has
+    // no next hops, and the padding past N) - not held for all k (VGPRs)
+    auto own_dist = [&](uint32_t k) -> uint32_t {
+      return (v0 + k == src || v0 + k >= N) ? kInf : dist_at(i, own, k);
+    };
     // own level bytes with the source's byte forced to "unreached" (no next
     // hops; bytes past N are the row padding, unreached already)
     uint32_t ot[kWords];
@@ -2166,7 +2160,7 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
         if (en.x >= v0 && en.x < v0 + kLvlPer) {
 #pragma unroll
           for (uint32_t k = 0; k < kLvlPer; ++k)
-            if (v0 + k == en.x && dv[k] != kInf) acc[k] |= bit;
+            if (v0 + k == en.x && ((ot[k / 4] >> ((k & 3u) * 8u)) & 0xFFu) != kLvlNone) acc[k] |= bit;
         }
         if (en.w & 0x80000000u) continue;  // overloaded neighbour: no transit
         const Vec nx = nxs[g];
@@ -2189,13 +2183,15 @@ __global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
         } else if (!direct) {  // plain levels, a rank past 7
 #pragma unroll
           for (uint32_t k = 0; k < kLvlPer; ++k)
-            if (((nw[k / 4] >> ((k & 3u) * 8u)) & 0xFFu) + 1u == ls[k]) acc[k] |= bit;
+            if (((nw[k / 4] >> ((k & 3u) * 8u)) & 0xFFu) + 1u == ((ot[k / 4] >> ((k & 3u) * 8u)) & 0xFFu))
+              acc[k] |= bit;
         } else {
 #pragma unroll
           for (uint32_t k = 0; k < kLvlPer; ++k) {
-            if (dv[k] == kInf) continue;
+            const uint32_t dk = own_dist(k);
+            if (dk == kInf) continue;
             const uint32_t x = dist_at(en.z, nx, k);
-            if (x != kInf && static_cast<uint64_t>(en.y) + x == dv[k]) acc[k] |= bit;
+            if (x != kInf && static_cast<uint64_t>(en.y) + x == dk) acc[k] |= bit;
           }
         }
       }
