@@ -1407,15 +1407,22 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
 // Distances only (KSP2 searches): the async kernel above with its labels moved
 // from HBM into LDS as u16 pairs (two nodes per word, lowered by
 // compare-and-swap), so the 50k-node WAN of C4 (100 KB of distances + 12.5 KB
-// of near / far bitmaps) keeps a whole search on one CU. Relaxation chains
-// then pay LDS latency instead of a global atomic per hop; only the edge
-// records (read-only, shared by every search, L2-resident) come from memory.
-// A candidate of 0xFFFF or more is not representable: it is dropped and the
-// row flagged. The result is still exact unless a node ends unreached (a
-// dropped candidate was larger than any finite distance the node ends with,
-// and a node whose true distance needs 17 bits leaves itself unreached), so a
-// flagged row with an unreached node is queued in ovf_rows for the HBM kernel
-// (launch_spf_lds16 runs it over that list).
+// of near / far bitmaps + a 16 KB spill table) keeps a whole search on one
+// CU. Relaxation chains then pay LDS latency instead of a global atomic per
+// hop; only the edge records (read-only, shared by every search,
+// L2-resident) come from memory.
+// A u16 entry holds distances 0..0xFFFD inline; 0xFFFF is unreached and
+// 0xFFFE "spilled": the node's distance (>= 0xFFFE, the heavy-tailed metrics
+// of C4 leave a few such nodes per row) sits in an LDS hash table keyed by
+// node id. A spilled node that later gets an inline distance simply drops its
+// table entry from use (inline < any spilled value). Only when the table is
+// full is a candidate dropped; the row is then exact unless a node ends
+// unreached (a dropped candidate exceeds every finite distance its node ends
+// with, and a node whose distance needed the table stays unreached), so such
+// a row is queued in ovf_rows for the HBM kernel (launch_spf_lds16).
+constexpr uint32_t kSpillSlots = 2048, kSpillProbe = 64;
+constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
+
 template <int K>
 __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1427,16 +1434,19 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   if (a.row_mask && !a.row_mask[row]) return;
   constexpr int G = K <= 4 ? 4 : 2;
   const uint32_t DWp = ((N + 1) / 2 + 3) & ~3u;
-  uint32_t* dist = lds;  // node u: bits 16 (u & 1) .. of word u / 2; 0xFFFF unreached
+  uint32_t* dist = lds;  // node u: bits 16 (u & 1) .. of word u / 2
   uint32_t* near = lds + DWp;
   uint32_t* far = near + NB;
   uint32_t* filt = far + NB;
   uint32_t FW = 1;
   while (2 * FW <= min(NB, 256u)) FW *= 2;
+  uint32_t* sp_key = filt + FW;  // spill table: node id (~0u empty) | distance
+  uint32_t* sp_val = sp_key + kSpillSlots;
   const uint32_t fshift = 32u - (5u + static_cast<uint32_t>(__builtin_ctz(FW)));
   Src s(a, row);
   for (uint32_t i = tid; i < DWp; i += nthr) dist[i] = 0xFFFFFFFFu;
   for (uint32_t i = tid; i < 2 * NB; i += nthr) near[i] = 0u;
+  for (uint32_t i = tid; i < 2 * kSpillSlots; i += nthr) sp_key[i] = ~0u;
   if (s.n_ign)
     for (uint32_t i = tid; i < FW; i += nthr) filt[i] = 0u;
   if (tid < 2) s_min[tid] = kInf;
@@ -1465,7 +1475,27 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     s_work = 1u;
   }
   __syncthreads();
-  auto get = [&](uint32_t u) { return (dist[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu; };
+  // spill slot of u (inserted when `insert`), or -1: absent / table full
+  auto sp_slot = [&](uint32_t u, bool insert) -> int {
+    uint32_t h = (u * 0x9E3779B1u) >> (32u - 11u);  // 2048 slots
+    for (uint32_t p = 0; p < kSpillProbe; ++p, h = (h + 1u) & (kSpillSlots - 1u)) {
+      const uint32_t k = sp_key[h];
+      if (k == u) return static_cast<int>(h);
+      if (k != ~0u) continue;
+      if (!insert) return -1;
+      const uint32_t prev = atomicCAS(&sp_key[h], ~0u, u);
+      if (prev == ~0u || prev == u) return static_cast<int>(h);
+    }
+    return -1;
+  };
+  // distance of u from its u16 entry e (kInf: unreached)
+  auto eff = [&](uint32_t u, uint32_t e) -> uint32_t {
+    if (e < kD16Spill) return e;
+    if (e == kD16None) return kInf;
+    const int sl = sp_slot(u, false);
+    return sl < 0 ? kInf : sp_val[sl];
+  };
+  auto get = [&](uint32_t u) { return eff(u, (dist[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu); };
 
   const uint32_t delta = a.delta;
   uint32_t T = delta;
@@ -1476,17 +1506,32 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     // lower u to nd, starting from the word w as read; queue it if lowered
     auto merge = [&](uint32_t u, uint32_t nd, uint32_t w) {
       const uint32_t sh = (u & 1u) * 16u;
-      if (nd >= 0xFFFFu) {  // before the compare: an unreached node holds 0xFFFF too
-        ovf = true;
-        return;
-      }
-      if (nd >= ((w >> sh) & 0xFFFFu)) return;
-      for (;;) {
-        const uint32_t nw = (w & ~(0xFFFFu << sh)) | (nd << sh);
-        const uint32_t prev = atomicCAS(&dist[u >> 1], w, nw);
-        if (prev == w) break;
-        w = prev;
-        if (nd >= ((w >> sh) & 0xFFFFu)) return;  // lowered further meanwhile
+      uint32_t e = (w >> sh) & 0xFFFFu;
+      if (nd < kD16Spill) {  // inline: below any spilled distance
+        for (;;) {
+          if (e < kD16Spill && nd >= e) return;
+          const uint32_t nw = (w & ~(0xFFFFu << sh)) | (nd << sh);
+          const uint32_t prev = atomicCAS(&dist[u >> 1], w, nw);
+          if (prev == w) break;
+          w = prev;
+          e = (w >> sh) & 0xFFFFu;
+        }
+      } else {
+        if (e < kD16Spill) return;  // an inline distance is smaller
+        const int sl = sp_slot(u, true);
+        if (sl < 0) {  // table full: dropped
+          ovf = true;
+          return;
+        }
+        if (nd >= atomicMin(&sp_val[sl], nd)) return;
+        while (e == kD16None) {  // mark the entry spilled (unless it went inline meanwhile)
+          const uint32_t nw = w & ~(0x1u << sh);  // 0xFFFF -> 0xFFFE
+          const uint32_t prev = atomicCAS(&dist[u >> 1], w, nw);
+          if (prev == w) break;
+          w = prev;
+          e = (w >> sh) & 0xFFFFu;
+        }
+        if (e < kD16Spill) return;
       }
       const uint32_t bit = 1u << (u & 31u);
       if (nd < T) {
@@ -1601,8 +1646,8 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   bool inf = false;
   for (uint32_t i = tid; i < N; i += nthr) {
     const uint32_t d = get(i);
-    inf |= d == 0xFFFFu;
-    __builtin_nontemporal_store(d == 0xFFFFu ? kInf : d, &od[i]);
+    inf |= d == kInf;
+    __builtin_nontemporal_store(d, &od[i]);
   }
   if (s_ovf) {  // exact unless a node ended unreached: then the HBM kernel redoes the row
     if (inf) s_inf = 1u;
@@ -2472,7 +2517,7 @@ size_t lds16_bytes(uint32_t n_nodes) {
   const size_t nb = (n_nodes + 31) / 32;
   size_t fw = 1;
   while (2 * fw <= std::min<size_t>(nb, 256)) fw *= 2;
-  return 4 * ((((n_nodes + 1) / 2 + 3) & ~size_t{3}) + 2 * nb + fw);
+  return 4 * ((((n_nodes + 1) / 2 + 3) & ~size_t{3}) + 2 * nb + fw + 2 * kSpillSlots);
 }
 
 hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows, uint32_t ell_k,

@@ -230,3 +230,26 @@ def test_ksp2_c4_lds16_vs_hbm(hip, monkeypatch):
         got.append({(s, d, k): als_h[A].get_kth_paths(s, d, k) for s, d in pairs for k in (1, 2)})
     assert got[0] == got[1]
     assert sum(len(v) for v in got[0].values()) > C4_KSP2_PAIRS
+
+
+def test_ksp2_lds16_spill_table_full(hip, oracle):
+    """2,600 nodes at metrics 20,000-40,000: almost every distance needs the
+    spill table, which holds 2,048 nodes, so rows also overflow it and go to
+    the HBM kernel - sampled pairs equal the oracle's getKthPaths."""
+    dbs = random_topology(2400, n=2600, extra=2600, min_metric=20000, max_metric=40000, parallel=0.1,
+                          overload=0.02, link_overload=0.02)
+    als_h, _ = load_topology(hip, dbs, [])
+    als_o, _ = load_topology(oracle, dbs, [])
+    rng = random.Random(2400)
+    names = sorted(db.thisNodeName for db in dbs)
+    pairs = [(s, d) for s in rng.sample(names, 3) for d in rng.sample(names, 6)]
+    ls = als_h[A]._impl
+    ls.prefetch_kth_paths(pairs)
+    assert ls.ksp_stats() == (len(set(pairs)), 0)
+    found = 0
+    for s, d in pairs:
+        for k in (1, 2):
+            got = als_h[A].get_kth_paths(s, d, k)
+            assert got == als_o[A].get_kth_paths(s, d, k), (s, d, k)
+            found += len(got)
+    assert found > len(pairs)
