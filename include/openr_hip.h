@@ -166,6 +166,8 @@ typedef struct orh_spf_info {
                           (16 or 4), 1 for the u32-row kernel, 0 when fused */
   uint32_t hop_split;  /* first-hop phase: workgroups per source */
   uint32_t batch_sources; /* MS-BFS: sources per workgroup (<= mask_bits), else 0 */
+  uint32_t ms_threads;    /* MS-BFS: threads per workgroup (1024: the latency plan), else 0 */
+  uint32_t ms_skip;       /* MS-BFS: interval skip on (latency plan or ORH_MS_SKIP=1) */
 } orh_spf_info;
 int orh_last_spf_info(const orh_ctx* ctx, orh_spf_info* out);
 /* device time (HIP events on the context stream) of the last orh_spf_run;

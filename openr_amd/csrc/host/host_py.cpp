@@ -359,6 +359,8 @@ class SpfSweep {
     d["batch_sources"] = i.batch_sources;
     d["hop_nodes"] = i.hop_nodes;
     d["hop_split"] = i.hop_split;
+    d["ms_threads"] = i.ms_threads;
+    d["ms_skip"] = i.ms_skip;
     return d;
   }
   py::tuple fetch(size_t i) {

@@ -388,17 +388,46 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
   uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
+  // arrival log (u16 / u32 masks): per 64-node slice (one wave's nodes of one
+  // j) an append-only list of {new bits, lane, level} events, 64 * kS
+  // entries (a node gains >= 1 bit per event); turned into the node-major
+  // level blocks once the search ends
+  const bool use_log = sizeof(M) <= 4 && a.ms_log != nullptr;
+  uint64_t* log = use_log ? a.ms_log + static_cast<size_t>(blockIdx.x) * J * B * kS : nullptr;
+  const uint32_t lane = tid & 63u, wave = tid >> 6, waves = B >> 6;
+  // events per (j, wave) slice so far: LDS past the frontier arrays and the
+  // block-assembly area (registers would cost J SGPRs / VGPRs and spill)
+  uint32_t* s_lpos = lds + a.ms_lpos_off / 4u;
+  // append this wave's arrivals of slice j at level lv (nx: the lane's new
+  // bits); wo is the wave index, opaque per level so that the J slice
+  // offsets are not hoisted out of the level loop into SGPRs
+  auto log_events = [&](int j, V nx, uint32_t lv, uint32_t wo) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nx != 0u);
+    if (!m) return;
+    uint32_t sl = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j) * waves + wo);
+    asm volatile("" : "+s"(sl));  // the slice's offsets computed here, not hoisted
+    const uint32_t base = s_lpos[sl];
+    if (nx) {
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+      log[static_cast<size_t>(sl) * 64u * kS + pos] =
+          (static_cast<uint64_t>(nx) << 32) | (lane << 8) | min(lv, kLvlDirect);
+    }
+    if (lane == 0) s_lpos[sl] = base + static_cast<uint32_t>(__builtin_popcountll(m));
+  };
 #ifdef ORH_DIAG_STAMPS
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
 
   for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
+  if (use_log)
+    for (uint32_t i = tid; i < J * waves; i += B) s_lpos[i] = 0u;
   if (tid < 3) {
     s_prog[tid] = 0u;
     s_lo[tid] = ~0u;
     s_hin[tid] = ~0u;
   }
-  {  // every level byte starts as "unreached"
+  if (!use_log) {  // every level byte starts as "unreached"
     uint4* l4 = reinterpret_cast<uint4*>(lvl);
     for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
   }
@@ -407,7 +436,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
     const uintptr_t byte = reinterpret_cast<uintptr_t>(f_cur + src) + tid / 8u;
     atomicOr(reinterpret_cast<uint32_t*>(byte & ~uintptr_t(3)), 1u << ((byte & 3u) * 8u + (tid & 7u)));
-    lvl[static_cast<size_t>(src) * kS + tid] = 0;
+    if (!use_log) lvl[static_cast<size_t>(src) * kS + tid] = 0;
   }
   if (kSkip && tid < S) {  // level 0's frontier: the sources
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
@@ -441,6 +470,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   for (int j = 0; j < J; ++j) {
     const uint32_t v = j * B + tid;
     if (v < N) vis[j] = f_cur[v];  // level 0: the sources
+    if (use_log) log_events(j, v < N ? vis[j] : V(0), 0u, wave);
   }
 
   const uint32_t w0 = a.w0;
@@ -458,6 +488,8 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
+    uint32_t wo = __builtin_amdgcn_readfirstlane(wave);  // (log_events)
+    asm volatile("" : "+s"(wo));
     // ids that can gain a bit at this level: within bw of the previous
     // level's new frontier (scalar; empty when the frontier was)
     uint32_t reach_lo = 0u, reach_hi = ~0u, jm = 0u;  // jm: this wave's slices with a new frontier bit
@@ -526,18 +558,22 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
 #ifdef ORH_DIAG_STAMPS
         const uint64_t t_s0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef ORH_EXP_NO_LVL_STORE  // timing experiment only: drops the level bytes
+        if (use_log) log_events(j, nx, level, wo);
+#endif
         if (nx) {
           prog = 1;
-#ifndef ORH_EXP_NO_LVL_STORE  // timing experiment only: drops the level bytes
+#ifndef ORH_EXP_NO_LVL_STORE
           {
           uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
           if (level < kLvlDirect) {
-            for (V q = nx; q; q &= q - 1) lb[MsMask<M>::ctz(q)] = static_cast<uint8_t>(level);
-          } else {
+            if (!use_log)
+              for (V q = nx; q; q &= q - 1) lb[MsMask<M>::ctz(q)] = static_cast<uint8_t>(level);
+          } else {  // deep levels: the distance row directly (the level byte says so)
             const uint32_t vh = a.host_of[v];
             for (V q = nx; q; q &= q - 1) {
               const uint32_t b = MsMask<M>::ctz(q);
-              lb[b] = kLvlDirect;
+              if (!use_log) lb[b] = kLvlDirect;
               dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
             }
           }
@@ -580,6 +616,36 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     M* t = f_cur;
     f_cur = f_nxt;
     f_nxt = t;
+  }
+  if (use_log) {
+    // the log -> node-major level blocks: per slice, this wave's 64 nodes x
+    // kS bytes assembled in LDS (the frontier arrays are free: every wave
+    // has left the level loop), then written out whole, 16 bytes a lane
+    __syncthreads();
+    uint8_t* blk = reinterpret_cast<uint8_t*>(lds) + static_cast<size_t>(wave) * 64u * kS;
+    uint4* mine = reinterpret_cast<uint4*>(blk + lane * kS);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint32_t v = j * B + tid;
+#pragma unroll
+      for (uint32_t q = 0; q < kS / 16; ++q) mine[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      __syncthreads();
+      const uint32_t sl = static_cast<uint32_t>(j) * waves + wave;
+      const uint64_t* ev = log + static_cast<size_t>(sl) * 64u * kS;
+      const uint32_t n_ev = s_lpos[sl];
+      for (uint32_t e = lane; e < n_ev; e += 64u) {
+        const uint64_t x = ev[e];
+        uint8_t* nb = blk + ((x >> 8) & 63u) * kS;
+        const uint8_t lv = static_cast<uint8_t>(x & 0xFFu);
+        for (V q = static_cast<V>(x >> 32); q; q &= q - 1) nb[MsMask<M>::ctz(q)] = lv;
+      }
+      __syncthreads();
+      if (v < N) {
+        uint4* out = reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS);
+#pragma unroll
+        for (uint32_t q = 0; q < kS / 16; ++q) out[q] = mine[q];
+      }
+    }
   }
 #ifdef ORH_DIAG_STAMPS
   if (tid == 0 && blockIdx.x < 4096) {  // per workgroup: entry, exit, hardware id, levels
@@ -2376,9 +2442,17 @@ template <int K, class M, int J>
 static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   if (a.ms_width == 0 || a.ms_width > MsMask<M>::kS) return hipErrorInvalidValue;
   const uint32_t batches = (n_rows + a.ms_width - 1) / a.ms_width;
+  // the arrival log's block assembly reuses the frontier arrays' LDS: 64 x kS
+  // bytes per wave
+  size_t lds = plan.lds_bytes;
+  SpfArgs b = a;
+  if (a.ms_log) {  // + the per-slice event counts, past the assembly area
+    b.ms_lpos_off = static_cast<uint32_t>(std::max<size_t>(plan.lds_bytes, size_t{plan.block} * MsMask<M>::kS));
+    lds = b.ms_lpos_off + size_t{4} * J * (plan.block / 64);
+  }
   if (a.ms_bw)
-    return launch(spf_msbfs_kernel<K, M, J, true>, a, batches, plan.block, plan.lds_bytes, s);
-  return launch(spf_msbfs_kernel<K, M, J, false>, a, batches, plan.block, plan.lds_bytes, s);
+    return launch(spf_msbfs_kernel<K, M, J, true>, b, batches, plan.block, lds, s);
+  return launch(spf_msbfs_kernel<K, M, J, false>, b, batches, plan.block, lds, s);
 }
 
 template <int K, class M>
@@ -2406,6 +2480,12 @@ static hipError_t launch_ms(const SpfPlan& plan, const SpfArgs& a, uint32_t n_ro
   }
 }
 
+size_t ms_log_bytes(const SpfPlan& plan, uint32_t n_rows) {
+  if (plan.variant != SpfVariant::kMsBfs || plan.ms_width == 0 || plan.mask_bytes > 4) return 0;
+  const size_t batches = (n_rows + plan.ms_width - 1) / plan.ms_width;
+  return batches * plan.ms_j * plan.block * (plan.mask_bytes * 8) * sizeof(uint64_t);
+}
+
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows) {
   if (plan.variant != SpfVariant::kMsBfs || plan.ms_width == 0) return 0;
   const uint32_t w = plan.ms_width;
@@ -2425,7 +2505,12 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
   // latency plan: when every batch has a CU to itself (a sweep over a shard
   // of the sources, N GPUs sharing one topology), the per-level time of one
   // workgroup is the sweep time, so the batch gets 1024 threads (fewer nodes
-  // per thread: J = 12 instead of 20 on the 10k grid). ORH_MS_LATENCY=0: off
+  // per thread: J = 12 instead of 20 on the 10k grid). ORH_MS_LATENCY=0: off;
+  // ORH_MS_LATENCY=2: with the interval skip as well (it cuts a lone C2
+  // corner batch 0.48 -> 0.32 ms, profiles/r02/msbfs_ab.md, but a C2 shard of
+  // 1,254 sources measured 0.785 vs 0.748 ms with it, profiles/r04/
+  // f_strong_rehearsal_skip.txt vs e_strong_rehearsal.txt)
+  plan.ms_skip = 0;
   {
     const char* lat = getenv("ORH_MS_LATENCY");
     const uint32_t batches = (n_rows + plan.mask_bytes * 8 - 1) / (plan.mask_bytes * 8);
@@ -2434,6 +2519,7 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
         plan.block < 1024 && j <= 32) {
       plan.block = 1024;
       plan.ms_j = (j + 3) & ~3u;
+      plan.ms_skip = lat && atoi(lat) == 2;
     }
   }
   const size_t bytes64 = 2 * 8 * static_cast<size_t>(plan.ms_pitch);

@@ -116,6 +116,7 @@ struct orh_graph {
   std::vector<uint32_t> ms_dev_of, ms_host_of;  // host -> CM id, CM id -> host
   bool ms_dirty = true;
   uint32_t ms_bw = 0;  // CM bandwidth over live records when the interval skip is on, else 0
+  uint32_t ms_bw_layout = 1;  // the same bandwidth whatever the opt-in (latency-plan skip)
   uint2* d_ms_recs = nullptr;
   uint32_t* d_ms_dev_of = nullptr;
   uint32_t* d_ms_host_of = nullptr;
@@ -332,6 +333,7 @@ void build_ms_layout(orh_graph* g, std::vector<uint2>& recs) {
   const char* e = getenv("ORH_MS_SKIP");
   const bool on = e && atoi(e) == 1;
   g->ms_bw = on ? std::max(bw, 1u) : 0u;
+  g->ms_bw_layout = std::max(bw, 1u);
 }
 
 int sync_ms_layout(orh_graph* g) {
@@ -1959,10 +1961,17 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
     int rc = sync_ms_layout(g);
     if (rc) return rc;
-    a.ms_bw = g->ms_bw;
+    // the interval skip: opt-in for every sweep (ORH_MS_SKIP=1) or for the
+    // latency plan alone (ORH_MS_LATENCY=2)
+    a.ms_bw = g->ms_bw ? g->ms_bw : run_plan.ms_skip ? g->ms_bw_layout : 0u;
     a.ms_width = run_plan.ms_width;
-    rc = ensure_ms_lvl(ctx, orh::ms_scratch_bytes(run_plan, N, n_rows));
+    // ORH_MS_LOG=0 (A/B): level bytes stored as they arrive, no arrival log
+    const char* lg = getenv("ORH_MS_LOG");
+    const size_t scratch = (orh::ms_scratch_bytes(run_plan, N, n_rows) + 255) & ~size_t{255};
+    const size_t log_bytes = (lg && atoi(lg) == 0) ? 0 : orh::ms_log_bytes(run_plan, n_rows);
+    rc = ensure_ms_lvl(ctx, scratch + log_bytes);
     if (rc) return rc;
+    a.ms_log = log_bytes ? reinterpret_cast<uint64_t*>(ctx->d_ms_lvl + scratch) : nullptr;
     a.recs = g->d_ms_recs;
     a.dev_of = g->d_ms_dev_of;
     a.host_of = g->d_ms_host_of;
@@ -2075,6 +2084,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   info.rows = n_rows;
   info.mask_bits = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.mask_bytes * 8 : 0;
   info.batch_sources = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.ms_width : 0;
+  info.ms_threads = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.block : 0;
+  info.ms_skip = run_plan.variant == orh::SpfVariant::kMsBfs && a.ms_bw ? 1u : 0u;
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
 #ifdef ORH_EXP_MSBFS_ONLY  // timing experiment only (tools/diag_build.sh): no phase 2
     ctx->last_info = info;

@@ -348,3 +348,25 @@ def test_prefix_mirror_incremental(hip, oracle):
         so = oracle.spf_solver(me, True, enable_best_route_selection=best)
         assert_digests_equal(sh, so, me, als_h, ps_h, als_o, ps_o)
         assert sh.device_selected > 0
+
+
+@pytest.mark.parametrize("lat", ["1", "2", "0"])
+@pytest.mark.parametrize("variant", [0, 7])
+def test_c2_latency_plan(hip, oracle, monkeypatch, lat, variant):
+    """A sweep over a shard of the grid's sources (20 batches, each with a CU
+    to itself): the latency plan's 1,024-thread workgroups with the interval
+    skip (ORH_MS_LATENCY=2), without it (default) and the 512-thread plan
+    (ORH_MS_LATENCY=0); 64 rows in full against the oracle each time."""
+    from bench import drain_what_if_link
+    monkeypatch.setenv("ORH_MS_LATENCY", lat)
+    n = 100
+    adj_dbs, _ = bench_grid(n)
+    if variant:
+        assert drain_what_if_link(adj_dbs, n, variant)
+    als_h, _ = load_topology(hip, adj_dbs, [])
+    als_o, _ = load_topology(oracle, adj_dbs, [])
+    names = [str(i) for i in random.Random(640 + variant).sample(range(n * n), 640)]
+    info = _sweep_tables(als_h[A], als_o[A], names, list(range(0, 640, 10)))
+    assert info["variant"] == MSBFS and info["batch_sources"] == 32, info
+    assert info["ms_threads"] == (512 if lat == "0" else 1024), info
+    assert info["ms_skip"] == (1 if lat == "2" else 0), info

@@ -233,16 +233,17 @@ def test_ksp2_c4_lds16_vs_hbm(hip, monkeypatch):
 
 
 def test_ksp2_lds16_spill_table_full(hip, oracle):
-    """2,600 nodes at metrics 20,000-40,000: almost every distance needs the
-    spill table, which holds 2,048 nodes, so rows also overflow it and go to
-    the HBM kernel - sampled pairs equal the oracle's getKthPaths."""
-    dbs = random_topology(2400, n=2600, extra=2600, min_metric=20000, max_metric=40000, parallel=0.1,
-                          overload=0.02, link_overload=0.02)
+    """A 2,400-node ladder at metric 30,000: every node more than two links
+    away needs the spill table, which holds 2,048 nodes, so every search
+    overflows it and its row is re-run by the HBM kernel - sampled pairs
+    equal the oracle's getKthPaths."""
+    from openr_amd.topology import ladder
+    L = 1200
+    dbs, _ = ladder(L, 30000)
     als_h, _ = load_topology(hip, dbs, [])
     als_o, _ = load_topology(oracle, dbs, [])
-    rng = random.Random(2400)
-    names = sorted(db.thisNodeName for db in dbs)
-    pairs = [(s, d) for s in rng.sample(names, 3) for d in rng.sample(names, 6)]
+    pairs = [("a0", f"a{L - 1}"), ("a0", f"b{L - 1}"), ("b0", f"a{L // 2}"),
+             (f"a{L // 2}", "b0"), (f"b{L // 2}", f"a{L - 1}"), (f"a{L // 2 + 3}", f"b{L // 2 - 40}")]
     ls = als_h[A]._impl
     ls.prefetch_kth_paths(pairs)
     assert ls.ksp_stats() == (len(set(pairs)), 0)

@@ -14,6 +14,8 @@ step() {  # step LOG CMD...
   return 0
 }
 step "$OUT/ksp_tests.log" timeout -k 10 600 python -u -m pytest tests/test_gpu_ksp2_abi.py -v -k "lds16" --timeout 300 --timeout-method thread
+step "$OUT/latency_tests.log" timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -v -k "latency_plan" --timeout 300 --timeout-method thread --timeout 300 --timeout-method thread
+step "$OUT/strong.log" timeout -k 10 300 python -u tools/strong_rehearsal.py 100 1 2 4 8
 step "$OUT/ksp_stage.log" timeout -k 10 300 python -u tools/ksp2_stage_ab.py 1
 step "$OUT/prof_one.log" timeout -k 10 900 bash tools/profile.sh ${TAG}_one --topologies 1 --lanes 1 --steps 10 --warmup 2 --no-cpu-baseline --no-route-db --legs=
 step "$OUT/prof_step.log" timeout -k 10 900 bash tools/profile.sh ${TAG}_step --steps 5 --warmup 2 --no-cpu-baseline --no-route-db --legs=
