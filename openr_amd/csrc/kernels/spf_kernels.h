@@ -24,8 +24,7 @@ struct SpfArgs {
   const uint32_t* host_of;    // multi-source BFS: [N] Cuthill-McKee id -> host id
   const uint32_t* order;      // [n_rows] multi-source batch order of the rows
   uint8_t* ms_lvl;            // multi-source BFS: node-major level bytes [batches][N][S]
-  uint64_t* ms_log;           // multi-source BFS: arrival log [batches][J * block / 64][64 * S] (nullable)
-  uint32_t ms_lpos_off;       // multi-source BFS with the log: LDS byte offset of the per-slice counts
+  uint64_t* ms_log;           // multi-source BFS (u16 / u32 masks): arrival logs [batches][waves][J * 64 * S]
   uint32_t ms_pitch;          // multi-source BFS: frontier-array entries (> N)
   uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
   uint32_t ms_bw;             // multi-source BFS: layout bandwidth for the interval skip (0: no skip)
@@ -178,7 +177,7 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
 void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit);
 // bytes of node-major level scratch a multi-source plan needs for n_rows rows
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
-// bytes of the multi-source arrival log (u16 / u32 masks; 0 otherwise), after
+// bytes of the multi-source arrival logs (u16 / u32 masks; 0 otherwise), after
 // ms_set_width: per batch J * block * mask bits events of 8 bytes
 size_t ms_log_bytes(const SpfPlan& plan, uint32_t n_rows);
 

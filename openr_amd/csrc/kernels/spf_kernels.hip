@@ -388,46 +388,39 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
   uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
-  // arrival log (u16 / u32 masks): per 64-node slice (one wave's nodes of one
-  // j) an append-only list of {new bits, lane, level} events, 64 * kS
-  // entries (a node gains >= 1 bit per event); turned into the node-major
-  // level blocks once the search ends
-  const bool use_log = sizeof(M) <= 4 && a.ms_log != nullptr;
-  uint64_t* log = use_log ? a.ms_log + static_cast<size_t>(blockIdx.x) * J * B * kS : nullptr;
+  // arrival log (u16 / u32 masks, kLog): each wave appends its nodes' level
+  // events {new bits (hi), slice j << 14 | lane << 8 | level (lo)} to a log
+  // of its own - one scalar count, one coalesced store per (j, level) with
+  // arrivals - and the node-major level blocks are assembled from the logs
+  // once the search ends. Capacity: a node gains >= 1 bit per event, so
+  // J * 64 * kS events per wave
+  constexpr bool kLog = sizeof(M) <= 4;
   const uint32_t lane = tid & 63u, wave = tid >> 6, waves = B >> 6;
-  // events per (j, wave) slice so far: LDS past the frontier arrays and the
-  // block-assembly area (registers would cost J SGPRs / VGPRs and spill)
-  uint32_t* s_lpos = lds + a.ms_lpos_off / 4u;
-  // append this wave's arrivals of slice j at level lv (nx: the lane's new
-  // bits); wo is the wave index, opaque per level so that the J slice
-  // offsets are not hoisted out of the level loop into SGPRs
-  auto log_events = [&](int j, V nx, uint32_t lv, uint32_t wo) {
+  uint64_t* wlog = kLog ? a.ms_log + (static_cast<size_t>(blockIdx.x) * waves + wave) * J * 64u * kS : nullptr;
+  uint32_t wcnt = 0;  // events in this wave's log (wave-uniform)
+  __shared__ uint32_t s_wcnt[16];
+  auto log_events = [&](int j, V nx, uint32_t lv) {
     const uint64_t m = __builtin_amdgcn_ballot_w64(nx != 0u);
     if (!m) return;
-    uint32_t sl = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(j) * waves + wo);
-    asm volatile("" : "+s"(sl));  // the slice's offsets computed here, not hoisted
-    const uint32_t base = s_lpos[sl];
     if (nx) {
-      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+      const uint32_t pos = wcnt + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-      log[static_cast<size_t>(sl) * 64u * kS + pos] =
-          (static_cast<uint64_t>(nx) << 32) | (lane << 8) | min(lv, kLvlDirect);
+      wlog[pos] = (static_cast<uint64_t>(nx) << 32) | (static_cast<uint32_t>(j) << 14) | (lane << 8) |
+                  min(lv, kLvlDirect);
     }
-    if (lane == 0) s_lpos[sl] = base + static_cast<uint32_t>(__builtin_popcountll(m));
+    wcnt += static_cast<uint32_t>(__builtin_popcountll(m));
   };
 #ifdef ORH_DIAG_STAMPS
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
 
   for (uint32_t i = tid; i < 2 * a.ms_pitch; i += B) f_cur[i] = 0;
-  if (use_log)
-    for (uint32_t i = tid; i < J * waves; i += B) s_lpos[i] = 0u;
   if (tid < 3) {
     s_prog[tid] = 0u;
     s_lo[tid] = ~0u;
     s_hin[tid] = ~0u;
   }
-  if (!use_log) {  // every level byte starts as "unreached"
+  if (!kLog) {  // every level byte starts as "unreached"
     uint4* l4 = reinterpret_cast<uint4*>(lvl);
     for (uint32_t i = tid; i < N * kS / 16; i += B) l4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
   }
@@ -436,7 +429,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
     const uintptr_t byte = reinterpret_cast<uintptr_t>(f_cur + src) + tid / 8u;
     atomicOr(reinterpret_cast<uint32_t*>(byte & ~uintptr_t(3)), 1u << ((byte & 3u) * 8u + (tid & 7u)));
-    if (!use_log) lvl[static_cast<size_t>(src) * kS + tid] = 0;
+    if (!kLog) lvl[static_cast<size_t>(src) * kS + tid] = 0;
   }
   if (kSkip && tid < S) {  // level 0's frontier: the sources
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
@@ -470,7 +463,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   for (int j = 0; j < J; ++j) {
     const uint32_t v = j * B + tid;
     if (v < N) vis[j] = f_cur[v];  // level 0: the sources
-    if (use_log) log_events(j, v < N ? vis[j] : V(0), 0u, wave);
+    if (kLog) log_events(j, v < N ? vis[j] : V(0), 0u);
   }
 
   const uint32_t w0 = a.w0;
@@ -488,8 +481,6 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     // a 768-thread workgroup per CU at J = 16 uses ~74)
     uint32_t me = tid;
     asm volatile("" : "+v"(me));
-    uint32_t wo = __builtin_amdgcn_readfirstlane(wave);  // (log_events)
-    asm volatile("" : "+s"(wo));
     // ids that can gain a bit at this level: within bw of the previous
     // level's new frontier (scalar; empty when the frontier was)
     uint32_t reach_lo = 0u, reach_hi = ~0u, jm = 0u;  // jm: this wave's slices with a new frontier bit
@@ -559,7 +550,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
         const uint64_t t_s0 = __builtin_amdgcn_s_memtime();
 #endif
 #ifndef ORH_EXP_NO_LVL_STORE  // timing experiment only: drops the level bytes
-        if (use_log) log_events(j, nx, level, wo);
+        if (kLog) log_events(j, nx, level);
 #endif
         if (nx) {
           prog = 1;
@@ -567,13 +558,13 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
           {
           uint8_t* lb = lvl + static_cast<size_t>(v) * kS;
           if (level < kLvlDirect) {
-            if (!use_log)
+            if (!kLog)
               for (V q = nx; q; q &= q - 1) lb[MsMask<M>::ctz(q)] = static_cast<uint8_t>(level);
           } else {  // deep levels: the distance row directly (the level byte says so)
             const uint32_t vh = a.host_of[v];
             for (V q = nx; q; q &= q - 1) {
               const uint32_t b = MsMask<M>::ctz(q);
-              if (!use_log) lb[b] = kLvlDirect;
+              if (!kLog) lb[b] = kLvlDirect;
               dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
             }
           }
@@ -617,34 +608,45 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     f_cur = f_nxt;
     f_nxt = t;
   }
-  if (use_log) {
-    // the log -> node-major level blocks: per slice, this wave's 64 nodes x
-    // kS bytes assembled in LDS (the frontier arrays are free: every wave
-    // has left the level loop), then written out whole, 16 bytes a lane
+  if constexpr (kLog) {
+    // the logs -> node-major level blocks, one wave's nodes at a time: the
+    // workgroup zeroes their J * 64 blocks in LDS (the frontier arrays are
+    // free once every wave has left the level loop), scatters the wave's
+    // events into them (loads in flight eight at a time) and writes the
+    // blocks out whole, 16 bytes a thread
+    if (lane == 0) s_wcnt[wave] = wcnt;
     __syncthreads();
-    uint8_t* blk = reinterpret_cast<uint8_t*>(lds) + static_cast<size_t>(wave) * 64u * kS;
-    uint4* mine = reinterpret_cast<uint4*>(blk + lane * kS);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const uint32_t v = j * B + tid;
-#pragma unroll
-      for (uint32_t q = 0; q < kS / 16; ++q) mine[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    // node blocks padded to kS + 4 bytes: consecutive blocks start 9 (kS =
+    // 32) or 5 (kS = 16) banks apart, so the scattered byte writes of a wave
+    // spread over the banks instead of 8 blocks sharing one
+    constexpr uint32_t kP = kS + 4, kQ = kS / 16;
+    uint8_t* blk = reinterpret_cast<uint8_t*>(lds);
+    const uint32_t nw32 = J * 64u * kP / 4u;
+    for (uint32_t w = 0; w < waves; ++w) {
+      for (uint32_t i = tid; i < nw32; i += B) lds[i] = ~0u;
       __syncthreads();
-      const uint32_t sl = static_cast<uint32_t>(j) * waves + wave;
-      const uint64_t* ev = log + static_cast<size_t>(sl) * 64u * kS;
-      const uint32_t n_ev = s_lpos[sl];
-      for (uint32_t e = lane; e < n_ev; e += 64u) {
-        const uint64_t x = ev[e];
-        uint8_t* nb = blk + ((x >> 8) & 63u) * kS;
-        const uint8_t lv = static_cast<uint8_t>(x & 0xFFu);
-        for (V q = static_cast<V>(x >> 32); q; q &= q - 1) nb[MsMask<M>::ctz(q)] = lv;
+      const uint32_t n_ev = s_wcnt[w];
+      const uint64_t* wl = a.ms_log + (static_cast<size_t>(blockIdx.x) * waves + w) * J * 64u * kS;
+      for (uint32_t e0 = tid; e0 < n_ev; e0 += 8u * B) {
+        uint64_t x[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) x[u] = e0 + u * B < n_ev ? wl[e0 + u * B] : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+          uint8_t* nb = blk + ((static_cast<uint32_t>(x[u]) >> 8) & 0x7FFu) * kP;  // (j * 64 + lane) * kP
+          const uint8_t lv = static_cast<uint8_t>(x[u] & 0xFFu);
+          for (V q = static_cast<V>(x[u] >> 32); q; q &= q - 1) nb[MsMask<M>::ctz(q)] = lv;
+        }
       }
       __syncthreads();
-      if (v < N) {
-        uint4* out = reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS);
-#pragma unroll
-        for (uint32_t q = 0; q < kS / 16; ++q) out[q] = mine[q];
+      for (uint32_t i = tid; i < J * 64u * kQ; i += B) {
+        const uint32_t node = i / kQ, q = i % kQ;  // node = j * 64 + lane
+        const uint32_t v = (node >> 6) * B + w * 64u + (node & 63u);
+        const uint32_t* src = lds + node * (kP / 4u) + q * 4u;
+        if (v < N)
+          reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS)[q] = make_uint4(src[0], src[1], src[2], src[3]);
       }
+      __syncthreads();
     }
   }
 #ifdef ORH_DIAG_STAMPS
@@ -2166,8 +2168,15 @@ __device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t group) {
 
 // One workgroup per (source, tile phase): the source's tight first links are
 // gathered once, then the workgroup walks tiles phase, phase + split, ...
+// ORH_HOP_WAVES (A/B builds): waves per SIMD the register allocation must
+// allow (4: <= 128 VGPRs, room beside the MS-BFS workgroups of other streams)
+#ifdef ORH_HOP_WAVES
+#define ORH_HOP_ATTR __attribute__((amdgpu_waves_per_eu(ORH_HOP_WAVES)))
+#else
+#define ORH_HOP_ATTR
+#endif
 template <uint32_t kLvlPer>
-__global__ __launch_bounds__(kBlock) void first_hop_lvl_kernel(HopArgs a) {
+__global__ __launch_bounds__(kBlock) ORH_HOP_ATTR void first_hop_lvl_kernel(HopArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_cnt;
   typedef typename LvlVec<kLvlPer>::T Vec;
@@ -2444,12 +2453,14 @@ static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_
   const uint32_t batches = (n_rows + a.ms_width - 1) / a.ms_width;
   // the arrival log's block assembly reuses the frontier arrays' LDS: 64 x kS
   // bytes per wave
+  // the log's block assembly reuses the frontier arrays' LDS: one wave's
+  // J * 64 node blocks at a time
   size_t lds = plan.lds_bytes;
-  SpfArgs b = a;
-  if (a.ms_log) {  // + the per-slice event counts, past the assembly area
-    b.ms_lpos_off = static_cast<uint32_t>(std::max<size_t>(plan.lds_bytes, size_t{plan.block} * MsMask<M>::kS));
-    lds = b.ms_lpos_off + size_t{4} * J * (plan.block / 64);
+  if (sizeof(M) <= 4) {
+    if (!a.ms_log) return hipErrorInvalidValue;
+    lds = std::max<size_t>(lds, size_t{J} * 64 * (MsMask<M>::kS + 4));
   }
+  const SpfArgs& b = a;
   if (a.ms_bw)
     return launch(spf_msbfs_kernel<K, M, J, true>, b, batches, plan.block, lds, s);
   return launch(spf_msbfs_kernel<K, M, J, false>, b, batches, plan.block, lds, s);
@@ -2671,7 +2682,14 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
     // a workgroup per source walks the tiles (one gather of the source's
     // first links), split over phases while that leaves < 8192 workgroups
     const uint32_t t16 = (a.n_nodes + kBlock * 16 - 1) / (kBlock * 16);
-    const bool wide = static_cast<uint64_t>(t16) * a.n_out >= 8192;
+    // ORH_HOP_NARROW=1 (A/B): 4 nodes per thread even for large batches
+    // (65 instead of 158 VGPRs: waves that fit beside the MS-BFS workgroups
+    // of other streams)
+    static const bool narrow = [] {
+      const char* e = getenv("ORH_HOP_NARROW");
+      return e && atoi(e) == 1;
+    }();
+    const bool wide = !narrow && static_cast<uint64_t>(t16) * a.n_out >= 8192;
     a.tiles = wide ? t16 : (a.n_nodes + kBlock * 4 - 1) / (kBlock * 4);
     a.tile_split = 1;
     while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;

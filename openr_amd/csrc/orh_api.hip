@@ -1965,10 +1965,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     // latency plan alone (ORH_MS_LATENCY=2)
     a.ms_bw = g->ms_bw ? g->ms_bw : run_plan.ms_skip ? g->ms_bw_layout : 0u;
     a.ms_width = run_plan.ms_width;
-    // ORH_MS_LOG=0 (A/B): level bytes stored as they arrive, no arrival log
-    const char* lg = getenv("ORH_MS_LOG");
     const size_t scratch = (orh::ms_scratch_bytes(run_plan, N, n_rows) + 255) & ~size_t{255};
-    const size_t log_bytes = (lg && atoi(lg) == 0) ? 0 : orh::ms_log_bytes(run_plan, n_rows);
+    const size_t log_bytes = orh::ms_log_bytes(run_plan, n_rows);
     rc = ensure_ms_lvl(ctx, scratch + log_bytes);
     if (rc) return rc;
     a.ms_log = log_bytes ? reinterpret_cast<uint64_t*>(ctx->d_ms_lvl + scratch) : nullptr;
