@@ -25,6 +25,11 @@ struct SpfArgs {
   const uint32_t* order;      // [n_rows] multi-source batch order of the rows
   uint8_t* ms_lvl;            // multi-source BFS: node-major level bytes [batches][N][S]
   uint64_t* ms_log;           // multi-source BFS (u16 / u32 masks): arrival logs [batches][waves][J * 64 * S]
+  // u16 LDS search (nullable): row r may stop once the nodes stop_nodes
+  // [stop_ptr[r], stop_ptr[r + 1]) are final - rows that feed path traces to
+  // those targets (KSP2) need no node beyond them
+  const uint32_t* stop_ptr;
+  const uint32_t* stop_nodes;
   uint32_t ms_pitch;          // multi-source BFS: frontier-array entries (> N)
   uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
   uint32_t ms_bw;             // multi-source BFS: layout bandwidth for the interval skip (0: no skip)

@@ -1494,7 +1494,7 @@ constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
 template <int K>
 __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf, s_inf;
+  __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf, s_inf, s_stop;
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
@@ -1502,6 +1502,11 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   if (a.row_mask && !a.row_mask[row]) return;
   constexpr int G = K <= 4 ? 4 : 2;
   const uint32_t DWp = ((N + 1) / 2 + 3) & ~3u;
+  uint32_t stop_lo = 0, stop_hi = 0;  // this row's target nodes (early stop)
+  if (a.stop_ptr) {
+    stop_lo = a.stop_ptr[row];
+    stop_hi = a.stop_ptr[row + 1];
+  }
   uint32_t* dist = lds;  // node u: bits 16 (u & 1) .. of word u / 2
   uint32_t* near = lds + DWp;
   uint32_t* far = near + NB;
@@ -1522,6 +1527,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     s_nign = 0u;
     s_ovf = 0u;
     s_inf = 0u;
+    s_stop = 0u;
   }
   __syncthreads();
   if (s.n_ign) {
@@ -1568,6 +1574,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   const uint32_t delta = a.delta;
   uint32_t T = delta;
   uint32_t mpar = 0;
+  uint32_t stop_m = 0;  // > 0: stopped with every node at distance <= stop_m final
   bool ovf = false;
   for (;;) {
     uint32_t far_min = kInf;
@@ -1684,8 +1691,21 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     if (m == kInf) break;  // far set empty: done
     T = m + delta;
     const uint32_t npar = mpar ^ 1u;
-    if (tid == 0) s_min[npar] = kInf;
+    if (tid == 0) {
+      s_min[npar] = kInf;
+      // every node at distance <= m is final (m: the least unsettled one);
+      // once the targets are among them, no trace to them reads further
+      if (stop_hi > stop_lo) {
+        bool done = true;
+        for (uint32_t q = stop_lo; q < stop_hi && done; ++q) done = get(a.stop_nodes[q]) <= m;
+        if (done) s_stop = m;
+      }
+    }
     __syncthreads();
+    if (s_stop) {
+      stop_m = s_stop;
+      break;
+    }
     uint32_t local_min = kInf, promoted = 0;
     for (uint32_t w2 = tid; w2 < NB; w2 += nthr) {
       const uint32_t fb = far[w2];
@@ -1717,8 +1737,11 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     inf |= d == kInf;
     __builtin_nontemporal_store(d, &od[i]);
   }
-  if (s_ovf) {  // exact unless a node ended unreached: then the HBM kernel redoes the row
-    if (inf) s_inf = 1u;
+  // exact unless a node ended unreached; stopped early, exact up to stop_m
+  // unless the spill table overflowed below it (dropped candidates are all
+  // >= 0xFFFE): otherwise the HBM kernel redoes the row
+  if (s_ovf && !(stop_m && stop_m < kD16Spill)) {
+    if (inf || stop_m) s_inf = 1u;
     __syncthreads();
     if (tid == 0 && s_inf) {
       const uint32_t k = atomicAdd(&a.ovf_rows[0], 1u);

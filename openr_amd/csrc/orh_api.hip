@@ -2532,6 +2532,9 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     const size_t o_vis = take(size_t{P} * kKspHashCap);
     const size_t o_st = take(size_t{P} * kKspStackCap * (sizeof(orh::KspFrame) / 4));
     const size_t o_ovf = take(size_t{std::max(S, P)} + 1);
+    // early-stop targets of the searches: the k = 1 row of a source stops once
+    // all its pairs' destinations are final, a k = 2 row once its pair's is
+    const size_t o_sp1 = take(S + 1), o_sn1 = take(P), o_sp2 = take(P + 1);
     rc = ensure_bytes(ctx, &ctx->d_ksp, &ctx->d_ksp_cap, off * 4);
     if (rc) return rc;
     uint32_t* D = reinterpret_cast<uint32_t*>(ctx->d_ksp);
@@ -2544,6 +2547,19 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     ORH_HIP(ctx, hipMemcpyAsync(D + o_rp, rowp.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemcpyAsync(D + o_ip, ip.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemcpyAsync(D + o_s1, srcs.data(), S * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    const char* stop_e = getenv("ORH_KSP_STOP");  // 0: full searches (A/B)
+    const bool stop = !(stop_e && stop_e[0] == '0');
+    std::vector<uint32_t> sp1(S + 1, 0), sn1(P), sp2(P + 1);
+    if (stop) {
+      for (uint32_t i = 0; i < P; ++i) ++sp1[row1[i] + 1];
+      for (uint32_t r = 0; r < S; ++r) sp1[r + 1] += sp1[r];
+      std::vector<uint32_t> fill(sp1.begin(), sp1.end() - 1);
+      for (uint32_t i = 0; i < P; ++i) sn1[fill[row1[i]]++] = h_dst[c0 + i];
+      for (uint32_t i = 0; i <= P; ++i) sp2[i] = i;
+      ORH_HIP(ctx, hipMemcpyAsync(D + o_sp1, sp1.data(), (S + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
+      ORH_HIP(ctx, hipMemcpyAsync(D + o_sn1, sn1.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
+      ORH_HIP(ctx, hipMemcpyAsync(D + o_sp2, sp2.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    }
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
     // both searches: the HBM frontier kernel, distances only (u32 labels)
     orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
@@ -2578,10 +2594,13 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.rank_out = g->d_rank_out;
     a.dist_only = 1;
     a.ovf_rows = D + o_ovf;
-    // k = 1 rows: the sources' plain SPFs (LinkState::getSpfResult)
+    // k = 1 rows: the sources' plain SPFs (LinkState::getSpfResult), as far
+    // as their pairs' destinations (the rows feed the k = 1 traces only)
     a.n_out = S;
     a.srcs = D + o_s1;
     a.out_dist = D + o_d1;
+    a.stop_ptr = stop ? D + o_sp1 : nullptr;
+    a.stop_nodes = stop ? D + o_sn1 : nullptr;
     fp.block = block_for(S);
     const orh_counters c_before = ctx->counters;
     mark(1);
@@ -2620,6 +2639,8 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.ignore_links = D + o_ign;
     a.out_dist = D + o_d2;
     a.row_mask = D + o_need;
+    a.stop_ptr = stop ? D + o_sp2 : nullptr;
+    a.stop_nodes = stop ? D + o_dst : nullptr;
     fp.block = block_for(P);
     e = search(a, P);
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
