@@ -66,10 +66,6 @@ struct RepairArgs {
   // copy only the requests the seed queued for repair (queue 0): the others'
   // rows are their sources' base rows, which the caller reads from the job
   uint32_t share_base;
-  // slot tier: near / far bucket width of its delta-stepping relaxation
-  // (ORH_WHATIF_PUSH=0: the chaotic sweeps of tiers 1-2 instead)
-  uint32_t delta;
-  uint32_t slot_push;
 };
 // queue index the slot tier drains (the full search's list)
 uint32_t repair_slot_queue(const RepairArgs& a);

@@ -135,34 +135,9 @@ __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t
 // caps cap_a / cap_e (LDS, or a global slot with whole-graph caps). Returns
 // |A|, or ~0u when A or its edge list outgrows the caps. The membership
 // bitmap must be all zero on entry; the caller clears it afterwards.
-// wave-wide minimum (DPP row shifts and broadcasts, as spf_kernels.hip)
-__device__ inline uint32_t wave_min_u32(uint32_t v) {
-#define ORH_DPP_MIN(ctrl, rmask)                                                          \
-  v = min(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(                            \
-                 static_cast<int>(kInfD), static_cast<int>(v), ctrl, rmask, 0xF, false)))
-  ORH_DPP_MIN(0x111, 0xF);
-  ORH_DPP_MIN(0x112, 0xF);
-  ORH_DPP_MIN(0x114, 0xF);
-  ORH_DPP_MIN(0x118, 0xF);
-  ORH_DPP_MIN(0x142, 0xA);
-  ORH_DPP_MIN(0x143, 0xC);
-#undef ORH_DPP_MIN
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
-}
-
-// Shared state of the slot tier's push relaxation (LDS): near / far bitmaps
-// over A's indices, the pending-work count and the far bounds
-struct PushLds {
-  uint32_t* near;
-  uint32_t* far;
-  uint32_t* s_work;
-  uint32_t* s_min;  // [2]
-};
-
-template <int K, bool kPush = false>
+template <int K>
 __device__ uint32_t repair_one(const RepairArgs& a, uint32_t r, uint32_t* base, uint32_t cap_a, uint32_t cap_e,
-                               uint32_t* s_cnt, uint32_t* s_ecnt, uint32_t* s_ovf, uint32_t* s_flag,
-                               const PushLds* pl = nullptr) {
+                               uint32_t* s_cnt, uint32_t* s_ecnt, uint32_t* s_ovf, uint32_t* s_flag) {
   const uint32_t N = a.n_nodes;
   const uint32_t tid = threadIdx.x, B = blockDim.x;
   // state: labels u64[cap_a] | boundary labels u64[cap_a] | edges uint2[cap_e] |
@@ -248,151 +223,6 @@ __device__ uint32_t repair_one(const RepairArgs& a, uint32_t r, uint32_t* base, 
     if (bits[p >> 5] & (1u << (p & 31u))) inside(p, w);
     else outside(p, q2, w);
   };
-  if constexpr (kPush) {
-    // Slot tier (A up to the whole graph): delta-stepping pushed along A's
-    // out-records instead of chaotic sweeps over its in-edge lists, which
-    // take as many whole-A sweeps as A's longest relaxation chain. Labels
-    // start at the boundary meets and descend in the same lattice (smaller
-    // distance replaces, equal ORs; any change re-queues the node), so the
-    // fixpoint is the chaotic form's, bit for bit.
-    for (uint32_t k = tid; k < n; k += B) {
-      const uint32_t v = alist[k];
-      unsigned long long bl = kInfLab;
-      for_records<K>(a.recs, v, [&](const uint2& rec, uint32_t q) {
-        pred(rec, q, [](uint32_t, uint32_t) {}, [&](uint32_t p, uint32_t q2, uint32_t w) {
-          const uint32_t dp = bd[p];
-          if (dp == kInfD) return;
-          bl = meet(bl, static_cast<uint64_t>(dp) + w, p == s ? (1u << a.rank_out[q2]) : bn[p]);
-        });
-      });
-      lab[k] = bl;
-    }
-    const uint32_t NBa = (n + 31) / 32;
-    uint32_t* near = pl->near;
-    uint32_t* far = pl->far;
-    for (uint32_t i = tid; i < 2 * NBa; i += B) near[i] = 0u;  // near | far, contiguous
-    if (tid == 0) {
-      *pl->s_work = 0u;
-      pl->s_min[0] = kInfD;
-      pl->s_min[1] = kInfD;
-    }
-    bar();
-    uint32_t local_min = kInfD;
-    for (uint32_t k = tid; k < n; k += B) {  // every finite boundary label starts in far
-      const uint32_t d = static_cast<uint32_t>(
-          __hip_atomic_load(&lab[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
-      if (d == kInfD) continue;
-      atomicOr(&far[k >> 5], 1u << (k & 31u));
-      local_min = min(local_min, d);
-    }
-    {
-      const uint32_t wm = wave_min_u32(local_min);
-      if ((tid & 63u) == 0 && wm != kInfD) atomicMin(&pl->s_min[0], wm);
-    }
-    bar();
-    const uint32_t delta = a.delta;
-    uint32_t mpar = 0;
-    for (;;) {
-      const uint32_t m = pl->s_min[mpar];
-      if (m == kInfD) break;  // far set empty: done (every thread read the same value)
-      const uint32_t T = m + delta;
-      const uint32_t npar = mpar ^ 1u;
-      if (tid == 0) pl->s_min[npar] = kInfD;
-      bar();
-      uint32_t fmin = kInfD, promoted = 0;
-      for (uint32_t w2 = tid; w2 < NBa; w2 += B) {
-        const uint32_t fb = far[w2];
-        uint32_t promote = 0u;
-        for (uint32_t q = fb; q; q &= q - 1) {
-          const uint32_t b = __builtin_ctz(q);
-          const uint32_t d = static_cast<uint32_t>(
-              __hip_atomic_load(&lab[w2 * 32 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32);
-          if (d < T) promote |= 1u << b;
-          else fmin = min(fmin, d);
-        }
-        if (promote) {
-          far[w2] = fb & ~promote;
-          near[w2] = promote;  // the near set is empty between buckets
-          promoted += __builtin_popcount(promote);
-        }
-      }
-      if (promoted) atomicAdd(pl->s_work, promoted);
-      bar();  // the bucket's count is complete before anyone drains it
-      auto merge = [&](uint32_t ui, uint32_t nd, uint32_t cnh) {
-        unsigned long long cl = __hip_atomic_load(&lab[ui], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (;;) {
-          const uint32_t cd = static_cast<uint32_t>(cl >> 32);
-          if (nd > cd) return;
-          const unsigned long long nl = nd < cd ? ((static_cast<unsigned long long>(nd) << 32) | cnh) : (cl | cnh);
-          if (nl == cl) return;
-          const unsigned long long old = atomicCAS(&lab[ui], cl, nl);
-          if (old == cl) break;
-          cl = old;
-        }
-        const uint32_t bit = 1u << (ui & 31u);
-        if (nd < T) {
-          atomicAdd(pl->s_work, 1u);  // counted before the bit is visible
-          const uint32_t old = atomicOr(&near[ui >> 5], bit);
-          atomicAnd(&far[ui >> 5], ~bit);
-          if (old & bit) atomicSub(pl->s_work, 1u);  // already queued
-        } else {
-          atomicOr(&far[ui >> 5], bit);
-          fmin = min(fmin, nd);
-        }
-      };
-      uint32_t wi = tid, bits_w = 0, wbase = 0;
-      for (;;) {
-        while (!bits_w && wi < NBa) {
-          bits_w = __hip_atomic_load(&near[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (bits_w) bits_w = atomicExch(&near[wi], 0u);  // at least the bits seen: only we clear
-          wbase = wi * 32;
-          wi += B;
-        }
-        const bool have = bits_w != 0u;
-        uint32_t k = 0;
-        if (have) {
-          k = wbase + __builtin_ctz(bits_w);
-          bits_w &= bits_w - 1;
-        } else if (wi >= NBa) {
-          wi = tid;  // words exhausted: rescan them next time
-        }
-        if (__builtin_amdgcn_ballot_w64(have) == 0ull) {
-          const uint32_t pending = __builtin_amdgcn_readfirstlane(
-              __hip_atomic_load(pl->s_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-          if (pending == 0u) break;
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        if (have) {
-          const uint32_t p = alist[k];
-          if (!a.ovl[p]) {  // p != s (s is never in A): transit unless overloaded
-            const unsigned long long lp = __hip_atomic_load(&lab[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t dp = static_cast<uint32_t>(lp >> 32), mp = static_cast<uint32_t>(lp);
-            for_records<K>(a.recs, p, [&](const uint2& rec, uint32_t q) {
-              const uint32_t u = rec.x & ORH_REC_COL_MASK;
-              if (!(bits[u >> 5] & (1u << (u & 31u)))) return;  // outside A: its row stands
-              if (n_ign && is_ignored(ign, n_ign, a.link[q])) return;
-              merge(on[u], dp + (metric ? rec.y : 1u), mp);
-            });
-          }
-          atomicSub(pl->s_work, 1u);
-        }
-      }
-      {
-        const uint32_t wm = wave_min_u32(fmin);
-        if ((tid & 63u) == 0 && wm != kInfD) atomicMin(&pl->s_min[npar], wm);
-      }
-      mpar = npar;
-      bar();  // bucket drained everywhere; far bound folded
-    }
-    for (uint32_t k = tid; k < n; k += B) {  // (atomic loads: the CAS results live in L2, not this CU's L1)
-      const uint32_t v = alist[k];
-      const unsigned long long l = __hip_atomic_load(&lab[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      od[v] = static_cast<uint32_t>(l >> 32);
-      on[v] = static_cast<uint32_t>(l);
-    }
-    return n;
-  }
   for (uint32_t k = tid; k < n; k += B) {
     const uint32_t v = alist[k];
     uint32_t cnt = 0;
@@ -520,8 +350,6 @@ void whatif_repair_kernel(RepairArgs a, uint32_t cap_a, uint32_t cap_e, uint32_t
   if (kSlot && a.info)
     for (uint32_t i = blockIdx.x * B + tid; i < skip; i += gridDim.x * B)
       a.info[a.queues[static_cast<size_t>(q) * a.n_req + i]] = kWhatifTierSearch;
-  __shared__ uint32_t s_work, s_min[2];
-  PushLds pl{lds, lds + NB, &s_work, s_min};  // slot tier: bucket bitmaps in dynamic LDS
   for (;;) {
     if (tid == 0) {
       const uint32_t i = atomicAdd(&a.counters[2 * q + 1], 1u) + skip;
@@ -530,9 +358,7 @@ void whatif_repair_kernel(RepairArgs a, uint32_t cap_a, uint32_t cap_e, uint32_t
     bar();
     const uint32_t r = s_req;
     if (r == ~0u) break;
-    const uint32_t n = kSlot && a.slot_push
-        ? repair_one<K, kSlot>(a, r, base, cap_a, cap_e, &s_cnt, &s_ecnt, &s_ovf, s_flag, &pl)
-        : repair_one<K>(a, r, base, cap_a, cap_e, &s_cnt, &s_ecnt, &s_ovf, s_flag);
+    const uint32_t n = repair_one<K>(a, r, base, cap_a, cap_e, &s_cnt, &s_ecnt, &s_ovf, s_flag);
     if (tid == 0) {
       if (n != ~0u) {
         if (a.info) a.info[r] = kTier | (n << 3);
@@ -634,14 +460,11 @@ hipError_t launch_repair_back_split(const RepairArgs& a, uint32_t ell_k, size_t 
   if (s3 != s) {
     if ((e = hipEventRecord(mid, s)) != hipSuccess || (e = hipStreamWaitEvent(s3, mid, 0)) != hipSuccess) return e;
   }
-  // the slot tier's push relaxation keeps its near / far bitmaps in LDS
-  const size_t lds3 = a.slot_push ? 2 * 4 * static_cast<size_t>((a.n_nodes + 31) / 32) : 0;
-  if (lds3 > lds_limit) return hipErrorInvalidValue;
   if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), lds3, s3, a,
+    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), lds3, s3, a,
+    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
                        a.n_nodes, a.n_recs, q2 + 1u);
   return hipGetLastError();
 }

@@ -1375,14 +1375,6 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   ra.n_recs = g->n_recs;
   ra.n_cu = ctx->n_cu;
   ra.share_base = (job->flags & ORH_WHATIF_SHARE_BASE) ? 1u : 0u;
-  {
-    const bool uniform = g->min_out == g->max_out;
-    ra.delta = uniform ? std::max<uint32_t>(1u, g->max_out)
-                       : std::max<uint32_t>(1u, static_cast<uint32_t>(
-                                                    static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
-    const char* pe = getenv("ORH_WHATIF_PUSH");
-    ra.slot_push = (pe && pe[0] == '0') ? 0u : 1u;
-  }
   // ORH_WHATIF_FULL=n (A/B, default 0): the slot tier's queue goes to full
   // searches first, up to n rows (labels within 1 GB). C4: 79 requests per
   // job searched in full 30.7-31.2 ms against 29.6 ms in slots

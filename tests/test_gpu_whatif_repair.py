@@ -302,36 +302,3 @@ def test_c4_shared_base_rows(hip):
     for i, (d, m) in rows[False].items():
         np.testing.assert_array_equal(rows[True][i][0], d, err_msg=f"request {i} dist")
         np.testing.assert_array_equal(rows[True][i][1], m, err_msg=f"request {i} nh")
-
-
-def test_c4_slot_tier_push_vs_sweeps(hip, monkeypatch):
-    """The slot tier's delta-stepping push (default) against its chaotic
-    sweeps (ORH_WHATIF_PUSH=0) on every slot-tier request of the C4 job:
-    the same lattice fixpoint, so bit-identical rows (the sweeps are pinned
-    to the oracle by test_c4_bench_batch_vs_oracle's largest sets)."""
-    from openr_amd.workloads import C4_WHATIF_CHUNK, c4_wan, c4_what_if_job
-    adj, _ = c4_wan()
-    als_h, _ = load_topology(hip, adj, [])
-    ls = als_h[A]._impl
-    names = ls.node_names()
-    links = ls.link_ids()
-    srcs, idx, sets = c4_what_if_job([lid for lid, _ in links], names)
-    big = ls.what_if_batch(srcs, idx, sets, C4_WHATIF_CHUNK)
-    big.run()
-    big.sync()
-    info = big.info()
-    slot = [int(i) for i in np.nonzero((info & 7) == 3)[0]]
-    assert len(slot) > 20
-    del big
-    rows = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("ORH_WHATIF_PUSH", mode)
-        sub = ls.what_if_batch(srcs, [idx[i] for i in slot], [sets[i] for i in slot], len(slot))
-        sub.run()
-        sub.sync()
-        assert np.array_equal(sub.info(), info[slot])
-        rows.append([sub.fetch(k) for k in range(len(slot))])
-        del sub
-    for k, i in enumerate(slot):
-        np.testing.assert_array_equal(rows[0][k][0], rows[1][k][0], err_msg=f"request {i} dist")
-        np.testing.assert_array_equal(rows[0][k][1], rows[1][k][1], err_msg=f"request {i} nh")
