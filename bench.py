@@ -291,7 +291,8 @@ def main():
 
 # newest committed PMC summary of this command (tools/profile.sh +
 # tools/pmc_summary.py), per sweep launch
-PMC_PROFILES = [os.path.join(ROOT, "profiles", "r03", "pmc.json"),
+PMC_PROFILES = [os.path.join(ROOT, "profiles", "r04", "pmc.json"),
+                os.path.join(ROOT, "profiles", "r03", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r02", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r01", "v6_pmc.json")]
 PMC_PROFILE = next((p for p in PMC_PROFILES if os.path.exists(p)), PMC_PROFILES[-1])
