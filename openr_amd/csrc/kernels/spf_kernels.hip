@@ -2159,6 +2159,11 @@ struct LvlVec<16> {
   }
 };
 template <>
+struct LvlVec<8> {
+  typedef uint2 T;
+  __device__ static uint32_t byte(const uint2& x, uint32_t k) { return ((k < 4 ? x.x : x.y) >> ((k & 3u) * 8u)) & 0xFFu; }
+};
+template <>
 struct LvlVec<4> {
   typedef uint32_t T;
   __device__ static uint32_t byte(const uint32_t& x, uint32_t k) { return (x >> (k * 8u)) & 0xFFu; }
@@ -2246,6 +2251,8 @@ __global__ __launch_bounds__(kBlock) ORH_HOP_ATTR void first_hop_lvl_kernel(HopA
     auto words_of = [](const Vec& x, uint32_t (&w)[kWords]) {
       if constexpr (kLvlPer == 16) {
         w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      } else if constexpr (kLvlPer == 8) {
+        w[0] = x.x; w[1] = x.y;
       } else {
         w[0] = x;
       }
@@ -2341,7 +2348,7 @@ __global__ __launch_bounds__(kBlock) ORH_HOP_ATTR void first_hop_lvl_kernel(HopA
       }  // entry group
 #pragma unroll
       for (uint32_t k = 0; k < kLvlPer; ++k) acc[k] |= (pk[k / 4] >> ((k & 3u) * 8u)) & 0xFFu;
-      if (kLvlPer == 16 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
+      if (kLvlPer >= 8 && W == 1 && v0 + kLvlPer <= N && (N & 3u) == 0) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4* o = reinterpret_cast<u32x4*>(nh + v0);
 #pragma unroll
@@ -2713,7 +2720,16 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
       return e && atoi(e) == 1;
     }();
     const bool wide = !narrow && static_cast<uint64_t>(t16) * a.n_out >= 8192;
-    a.tiles = wide ? t16 : (a.n_nodes + kBlock * 4 - 1) / (kBlock * 4);
+    // 8 nodes per thread for large batches (104 VGPRs, 8-byte row loads):
+    // one C2 sweep's first hops 0.323 -> 0.292 ms against 16 per thread (158
+    // VGPRs), the 4-lane step the same (profiles/r04/r_hop_nodes_ab.txt);
+    // ORH_HOP_NODES=16 (A/B): the 16-node form
+    static const uint32_t wide_nodes = [] {
+      const char* e = getenv("ORH_HOP_NODES");
+      return (e && atoi(e) == 16) ? 16u : 8u;
+    }();
+    const uint32_t per = wide ? wide_nodes : 4u;
+    a.tiles = (a.n_nodes + kBlock * per - 1) / (kBlock * per);
     a.tile_split = 1;
     while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;
     uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
@@ -2738,10 +2754,11 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
       const uint64_t cap = (static_cast<uint64_t>(n_cu) * per_cu) & ~uint64_t{7};
       if (cap >= 8 && cap < g2) g2 = cap;
     }
-    if (nodes_per_thread) *nodes_per_thread = wide ? 16 : 4;
+    if (nodes_per_thread) *nodes_per_thread = per;
     if (split) *split = a.tile_split;
-    return wide ? launch(first_hop_lvl_kernel<16>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
-                : launch(first_hop_lvl_kernel<4>, a, static_cast<uint32_t>(g2), kBlock, lds, s);
+    return per == 16 ? launch(first_hop_lvl_kernel<16>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
+         : per == 8  ? launch(first_hop_lvl_kernel<8>, a, static_cast<uint32_t>(g2), kBlock, lds, s)
+                     : launch(first_hop_lvl_kernel<4>, a, static_cast<uint32_t>(g2), kBlock, lds, s);
   }
   if (nodes_per_thread) *nodes_per_thread = 1;
   if (split) *split = a.tiles;

@@ -66,7 +66,7 @@ def test_c2_sweep_first_hops_exact(hip, oracle, variant):
     """The bench's own sweeps (C2, all 10,000 sources in one launch): the
     grid itself (variant 0) and two of the timed what-if variants (the grid
     with one seeded link drained, bench.drain_what_if_link: SKIP records in
-    the MS-BFS and in first_hop_lvl_kernel<16>). Dist rows and first-hop
+    the MS-BFS and in first_hop_lvl_kernel<8>). Dist rows and first-hop
     masks of 300 sources compared in full: the four corners, the edges'
     midpoints, the centre, both ends of the drained link and their
     neighbours, and seeded others."""
@@ -90,7 +90,7 @@ def test_c2_sweep_first_hops_exact(hip, oracle, variant):
     info = _sweep_tables(als_h[A], als_o[A], names, check)
     assert info["variant"] == MSBFS and info["mask_bits"] == 32, info
     assert info["batch_sources"] == 32, info
-    assert info["hop_nodes"] == 16, info  # first_hop_lvl_kernel<16>, as benched
+    assert info["hop_nodes"] == 8, info  # first_hop_lvl_kernel<8>, as benched
 
 
 @pytest.mark.parametrize("variant", [0, 7])
@@ -112,7 +112,7 @@ def test_c2_sweep_all_sources_exact(hip, oracle, variant):
     sweep.run()
     sweep.sync()
     info = sweep.info()
-    assert info["variant"] == MSBFS and info["hop_nodes"] == 16, info
+    assert info["variant"] == MSBFS and info["hop_nodes"] == 8, info
     order = ls_h._impl.node_names()
     W = sweep.words
     for lo in range(0, n * n, 1000):
@@ -146,7 +146,7 @@ def test_c2_sweep_opt_in_variants(hip, oracle, monkeypatch, env):
     assert info["batch_sources"] == (40 if wide else 32), info
 
 
-@pytest.mark.parametrize("length,metric,hop_nodes", [(4100, 3, 16), (300, 1, 4)])
+@pytest.mark.parametrize("length,metric,hop_nodes", [(4100, 3, 8), (300, 1, 4)])
 def test_ladder_deep_levels(hip, oracle, length, metric, hop_nodes):
     """BFS depth beyond the u8 level encoding (levels >= 254 are written to
     the distance rows directly and read back through them)."""
