@@ -503,7 +503,10 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     // frontier reads go out back to back before any is consumed. The skip
     // variant tests single slices (G = 1): its active band is a slice or two
     // per wave, and a group of 4 would do 2-4x the reads the band needs
-    constexpr int G = kSkip ? 1 : 4;
+#ifndef ORH_MS_GROUP
+#define ORH_MS_GROUP 4  // (A/B builds: owned nodes whose frontier reads go out together)
+#endif
+    constexpr int G = kSkip ? 1 : (J % ORH_MS_GROUP == 0 ? ORH_MS_GROUP : 4);
 #pragma unroll
     for (int j0 = 0; j0 < J; j0 += G) {
       const uint32_t sl = slice;
