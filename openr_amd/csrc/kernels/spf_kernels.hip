@@ -123,6 +123,18 @@ __device__ inline bool live(const SpfArgs& a, const Src& s, const uint2& r, uint
   return !ignored(s.ign, s.n_ign, l);
 }
 
+// live() with the record's link id already loaded (searches with ignore sets
+// fetch the ids together with the records: one round trip, not two)
+__device__ inline bool live_link(const Src& s, const uint2& r, uint32_t l) {
+  if (r.x & (ORH_REC_SKIP | ORH_REC_CONT)) return false;
+  if (!s.n_ign) return true;
+  if (s.filt) {
+    const uint32_t h = ign_hash(l, s.fshift);
+    if (!((s.filt[h >> 5] >> (h & 31u)) & 1u)) return true;
+  }
+  return !ignored(s.ign, s.n_ign, l);
+}
+
 template <int K>
 __device__ inline void load_recs(const SpfArgs& a, uint32_t v, uint2 (&rec)[K]) {
   const uint2* slots = a.recs + static_cast<size_t>(v) * K;
@@ -1246,10 +1258,13 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* 
   constexpr bool kNh = sizeof(L) == 8;
   uint2 rec[G][K];
   L lv[G];
+  uint32_t lk[G][K];  // link ids (ignore sets), loaded with the records
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (g >= c) break;
     load_recs<K>(a, vs[g], rec[g]);
+#pragma unroll
+    for (int j = 0; j < K; ++j) lk[g][j] = s.n_ign ? a.link[vs[g] * K + j] : 0u;
     lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   L cl[G][K];
@@ -1259,7 +1274,7 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* 
     const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
+      ok[g][j] = transit && live_link(s, rec[g][j], lk[g][j]);
       if (ok[g][j])
         cl[g][j] = __hip_atomic_load(&lab[rec[g][j].x & ORH_REC_COL_MASK], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -1648,9 +1663,13 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
       if (c > 0) {
         // the group's records in flight together, then the neighbours' words
         uint2 rec[G][K];
+        uint32_t lk[G][K];  // link ids (ignore sets), loaded with the records
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g) {
           if (g < c) load_recs<K>(a, vs[g], rec[g]);
+#pragma unroll
+          for (int j = 0; j < K; ++j) lk[g][j] = (g < c && s.n_ign) ? a.link[vs[g] * K + j] : 0u;
+        }
         uint32_t dv[G], nw[G][K];
         bool ok[G][K];
 #pragma unroll
@@ -1659,7 +1678,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
           const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
 #pragma unroll
           for (int j = 0; j < K; ++j) {
-            ok[g][j] = transit && live(a, s, rec[g][j], vs[g] * K + j);
+            ok[g][j] = transit && live_link(s, rec[g][j], lk[g][j]);
             nw[g][j] = ok[g][j] ? dist[(rec[g][j].x & ORH_REC_COL_MASK) >> 1] : 0u;
           }
         }

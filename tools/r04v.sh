@@ -18,3 +18,7 @@ for V in base g2 g5 g10; do
   step "$OUT/step_$V.log" env LD_LIBRARY_PATH=$L T=32 LANES=4 timeout -k 10 300 python -u tools/lanes_probe.py
 done
 echo "r04v done"
+# latency plan (1,024 threads when every batch has a CU) vs 512 threads for a shard
+step "$OUT/strong_lat1.log" timeout -k 10 300 python -u tools/strong_rehearsal.py 100 1 2 4 8
+step "$OUT/strong_lat0.log" env ORH_MS_LATENCY=0 timeout -k 10 300 python -u tools/strong_rehearsal.py 100 1 2 4 8
+echo "r04v strong done"
