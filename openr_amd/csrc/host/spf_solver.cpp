@@ -1014,7 +1014,34 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
       e.nexthops.insert(std::move(node));
     }
   } else {
-    insertTemplates(m, v4, metric, nullptr, nullptr, e.nexthops, noAction);
+    // Routes with the same first-hop mask, metric and family get the same
+    // nexthop set from the same insertion sequence: it is built once per
+    // selection and worker thread and then copied. A copy of a libstdc++
+    // unordered_set keeps the bucket count and node order (hash codes cached
+    // in the nodes), so it iterates exactly as the set built in place - the
+    // reference's order (a30). C3: ~2,400 distinct sets for 100k routes.
+    struct NhCache {
+      uint64_t gen = 0;
+      std::unordered_map<std::string, NextHopSet> sets;
+    };
+    thread_local NhCache cache;
+    if (cache.gen != selGen_) {
+      cache.sets.clear();
+      cache.gen = selGen_;
+    }
+    std::string key(reinterpret_cast<const char*>(m), selWords_ * 4u);
+    key.append(reinterpret_cast<const char*>(&metric), 4);
+    key.push_back(v4 ? '4' : '6');
+    auto it = cache.sets.find(key);
+    if (it != cache.sets.end()) {
+      e.nexthops = it->second;
+    } else if (cache.sets.size() < (1u << 16)) {
+      NextHopSet built;
+      insertTemplates(m, v4, metric, nullptr, nullptr, built, noAction);
+      e.nexthops = cache.sets.emplace(std::move(key), std::move(built)).first->second;
+    } else {
+      insertTemplates(m, v4, metric, nullptr, nullptr, e.nexthops, noAction);
+    }
   }
   uint32_t cnt = 0;
   const AdvRef* advs = ps.advs(pid, &cnt);
