@@ -995,53 +995,88 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
   // (RibPolicy.cpp:117-141); a weight of 0 drops the nexthop, and s only
   // applies when some nexthop keeps a weight (the kernel checked)
   const uint32_t s = devPol_.on ? devPol_.stmt[pid] : ORH_POL_NONE;
-  if (s < ORH_POL_MAX_STMTS) {
-    // the reference builds the route (weights 0), then the policy moves the
-    // kept nexthops into a new set in the first set's iteration order
-    // (RibPolicy.cpp:116-141): the same two sets here, so the result
-    // iterates in the reference's order; weights from the device decision
-    thread_local std::vector<std::pair<const NextHopThrift*, int32_t>> wts;
-    wts.clear();
-    NextHopSet built;
-    insertTemplates(m, v4, metric, &devPol_.weight[s], &wts, built, noAction);
-    while (!built.empty()) {
-      auto node = built.extract(built.begin());  // node addresses are stable
-      int32_t w = 0;
-      for (const auto& [p, pw] : wts)
-        if (p == &node.value()) w = pw;
-      if (w <= 0) continue;
-      node.value().weight = w;
-      e.nexthops.insert(std::move(node));
+  // the nexthop set as the reference builds it: templates inserted in
+  // getNextHopsThrift's order, and for a policy statement the set rebuilt
+  // with its weights in the first set's iteration order
+  auto buildSet = [&](NextHopSet& out) {
+    if (s < ORH_POL_MAX_STMTS) {
+      // the reference builds the route (weights 0), then the policy moves
+      // the kept nexthops into a new set in the first set's iteration order
+      // (RibPolicy.cpp:116-141): the same two sets here, so the result
+      // iterates in the reference's order; weights from the device decision
+      thread_local std::vector<std::pair<const NextHopThrift*, int32_t>> wts;
+      wts.clear();
+      NextHopSet built;
+      insertTemplates(m, v4, metric, &devPol_.weight[s], &wts, built, noAction);
+      while (!built.empty()) {
+        auto node = built.extract(built.begin());  // node addresses are stable
+        int32_t w = 0;
+        for (const auto& [p, pw] : wts)
+          if (p == &node.value()) w = pw;
+        if (w <= 0) continue;
+        node.value().weight = w;
+        out.insert(std::move(node));
+      }
+    } else {
+      insertTemplates(m, v4, metric, nullptr, nullptr, out, noAction);
     }
-  } else {
-    // Routes with the same first-hop mask, metric and family get the same
-    // nexthop set from the same insertion sequence: it is built once per
-    // selection and worker thread and then copied. A copy of a libstdc++
-    // unordered_set keeps the bucket count and node order (hash codes cached
-    // in the nodes), so it iterates exactly as the set built in place - the
-    // reference's order (a30). C3: ~2,400 distinct sets for 100k routes.
-    struct NhCache {
-      uint64_t gen = 0;
-      std::unordered_map<std::string, NextHopSet> sets;
-    };
-    thread_local NhCache cache;
-    if (cache.gen != selGen_) {
-      cache.sets.clear();
-      cache.gen = selGen_;
+  };
+  // Routes with the same first-hop mask, metric, family and policy statement
+  // get the same set from the same insertion sequence: it is built once per
+  // selection and worker thread and then copied. A copy of a libstdc++
+  // unordered_set keeps the bucket count and node order, so it iterates
+  // exactly as the set built in place - the reference's order (a30). C3:
+  // ~2,400 distinct sets for 100k routes.
+  struct NhKey {  // mask words, metric, family + statement (inline: no allocation)
+    uint32_t w[8];
+    uint32_t n;
+    bool operator==(const NhKey& o) const { return n == o.n && std::memcmp(w, o.w, n * 4) == 0; }
+  };
+  struct NhKeyHash {
+    size_t operator()(const NhKey& k) const {
+      uint64_t h = 0x9E3779B97F4A7C15ull ^ k.n;
+      for (uint32_t i = 0; i < k.n; ++i) h = (h ^ k.w[i]) * 0x100000001B3ull;
+      return static_cast<size_t>(h ^ (h >> 29));
     }
-    std::string key(reinterpret_cast<const char*>(m), selWords_ * 4u);
-    key.append(reinterpret_cast<const char*>(&metric), 4);
-    key.push_back(v4 ? '4' : '6');
+  };
+  struct NhCache {
+    uint64_t gen = 0;
+    const void* pol = nullptr;  // the DevicePolicy decision the statements index
+    uint32_t hits = 0, misses = 0;
+    std::unordered_map<NhKey, NextHopSet, NhKeyHash> sets;
+  };
+  thread_local NhCache cache;
+  if (cache.gen != selGen_ || cache.pol != &devPol_) {
+    cache.sets.clear();
+    cache.gen = selGen_;
+    cache.pol = &devPol_;
+    cache.hits = cache.misses = 0;
+  }
+  // off when the words do not fit the key, or once the sets turn out to be
+  // mostly distinct (a miss builds the set and stores a copy)
+  static const bool enabled = [] {  // ORH_NH_CACHE=0 (A/B): every set built in place
+    const char* e = std::getenv("ORH_NH_CACHE");
+    return !(e && e[0] == '0');
+  }();
+  const bool use = enabled && selWords_ + 2 <= 8 && cache.sets.size() < (1u << 16) &&
+                   !(cache.misses >= 512 && cache.hits < cache.misses);
+  if (use) {
+    NhKey key;
+    key.n = selWords_ + 2;
+    std::memcpy(key.w, m, selWords_ * 4u);
+    key.w[selWords_] = static_cast<uint32_t>(metric);
+    key.w[selWords_ + 1] = (v4 ? 4u : 6u) | (s << 8);
     auto it = cache.sets.find(key);
     if (it != cache.sets.end()) {
+      ++cache.hits;
       e.nexthops = it->second;
-    } else if (cache.sets.size() < (1u << 16)) {
-      NextHopSet built;
-      insertTemplates(m, v4, metric, nullptr, nullptr, built, noAction);
-      e.nexthops = cache.sets.emplace(std::move(key), std::move(built)).first->second;
     } else {
-      insertTemplates(m, v4, metric, nullptr, nullptr, e.nexthops, noAction);
+      ++cache.misses;
+      buildSet(e.nexthops);
+      cache.sets.emplace(key, e.nexthops);
     }
+  } else {
+    buildSet(e.nexthops);
   }
   uint32_t cnt = 0;
   const AdvRef* advs = ps.advs(pid, &cnt);
