@@ -515,10 +515,13 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     // frontier reads go out back to back before any is consumed. The skip
     // variant tests single slices (G = 1): its active band is a slice or two
     // per wave, and a group of 4 would do 2-4x the reads the band needs
+// owned nodes whose frontier reads go out together: 2 (round 4: one C2 sweep
+// 0.859 -> 0.823 ms and the 4-lane step 25.6 -> 25.0 ms against 4; 5: no
+// change; 10: slower - profiles/r04/v_ms_group_ab.txt). A/B builds: -DORH_MS_GROUP
 #ifndef ORH_MS_GROUP
-#define ORH_MS_GROUP 4  // (A/B builds: owned nodes whose frontier reads go out together)
+#define ORH_MS_GROUP 2
 #endif
-    constexpr int G = kSkip ? 1 : (J % ORH_MS_GROUP == 0 ? ORH_MS_GROUP : 4);
+    constexpr int G = kSkip ? 1 : (J % ORH_MS_GROUP == 0 ? ORH_MS_GROUP : 2);
 #pragma unroll
     for (int j0 = 0; j0 < J; j0 += G) {
       const uint32_t sl = slice;
