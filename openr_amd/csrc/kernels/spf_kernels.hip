@@ -2757,6 +2757,12 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
     a.tiles = (a.n_nodes + kBlock * per - 1) / (kBlock * per);
     a.tile_split = 1;
     while (a.tile_split < a.tiles && static_cast<uint64_t>(a.tile_split) * a.n_out < 8192) ++a.tile_split;
+    // ORH_HOP_SPLIT=n (A/B): at least n workgroups per source (tile phases)
+    static const uint32_t split_min = [] {
+      const char* e = getenv("ORH_HOP_SPLIT");
+      return e ? static_cast<uint32_t>(std::max(1, atoi(e))) : 1u;
+    }();
+    a.tile_split = std::max(a.tile_split, std::min(split_min, a.tiles));
     uint64_t g2 = static_cast<uint64_t>(a.tile_split) * a.n_out;
     if (g2 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     a.n_logical = static_cast<uint32_t>(g2);
