@@ -99,7 +99,7 @@ __device__ inline void for_records(const uint2* recs, uint32_t v, F&& f) {
 
 constexpr uint32_t kCopyTile = 256 * 16;  // u32 elements of a row per copy workgroup
 
-// base rows -> request rows; vec (1, 2): every row is 16-byte aligned (N % 4 == 0
+// base rows -> request rows; vec: every row is 16-byte aligned (N % 4 == 0
 // and aligned buffers), so a thread moves uint4s
 __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t tiles, uint32_t vec) {
   uint32_t r = blockIdx.x / tiles;
@@ -115,35 +115,11 @@ __global__ __launch_bounds__(256) void whatif_copy_kernel(RepairArgs a, uint32_t
   uint32_t* dd = a.out_dist + r * N;
   uint32_t* dn = a.out_nh + r * N;
   const size_t lo = static_cast<size_t>(t) * kCopyTile, hi = min(lo + kCopyTile, N);
-  if (vec == 1) {  // one load/store pair at a time
+  if (vec) {
     typedef uint32_t v4 __attribute__((ext_vector_type(4)));
     for (size_t i = lo / 4 + threadIdx.x; i < hi / 4; i += 256) {
       __builtin_nontemporal_store(reinterpret_cast<const v4*>(sd)[i], reinterpret_cast<v4*>(dd) + i);
       __builtin_nontemporal_store(reinterpret_cast<const v4*>(sn)[i], reinterpret_cast<v4*>(dn) + i);
-    }
-  } else if (vec) {  // ORH_WHATIF_COPY=1 (A/B)
-    // all eight 16-byte loads are issued before the first store: the rows
-    // may alias as far as the compiler knows, so a load/store loop would
-    // wait out one HBM round trip per pair
-    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-    constexpr int kPer = kCopyTile / 4 / 256;
-    const size_t lo4 = lo / 4, hi4 = hi / 4;
-    v4 x[kPer], y[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const size_t i = lo4 + threadIdx.x + k * 256;
-      if (i < hi4) {
-        x[k] = reinterpret_cast<const v4*>(sd)[i];
-        y[k] = reinterpret_cast<const v4*>(sn)[i];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const size_t i = lo4 + threadIdx.x + k * 256;
-      if (i < hi4) {
-        __builtin_nontemporal_store(x[k], reinterpret_cast<v4*>(dd) + i);
-        __builtin_nontemporal_store(y[k], reinterpret_cast<v4*>(dn) + i);
-      }
     }
   } else {
     for (size_t i = lo + threadIdx.x; i < hi; i += 256) {
@@ -446,9 +422,7 @@ hipError_t launch_repair_front(const RepairArgs& a, uint32_t ell_k, size_t lds_l
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   const uint32_t vec = (a.n_nodes & 3u) == 0 && al(a.base_dist) && al(a.base_nh) && al(a.out_dist) &&
                        al(a.out_nh);
-  const char* cp = getenv("ORH_WHATIF_COPY");
-  const uint32_t mode = vec ? (cp && atoi(cp) == 1 ? 2u : 1u) : 0u;
-  hipLaunchKernelGGL(whatif_copy_kernel, dim3(static_cast<uint32_t>(grid)), dim3(256), 0, s, a, tiles, mode);
+  hipLaunchKernelGGL(whatif_copy_kernel, dim3(static_cast<uint32_t>(grid)), dim3(256), 0, s, a, tiles, vec);
   return hipGetLastError();
 }
 
