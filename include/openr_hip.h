@@ -184,6 +184,16 @@ int orh_memcpy_h2d(orh_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
  * rows to a caller-owned buffer, e.g. the RCCL all-gather of a central RIB) */
 int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes);
 
+/* verification utility (no reference counterpart): per row r < n_rows of
+ * dist [n_rows*n] / nh [n_rows*n*words], the 64-bit digest
+ *   sum over v < n of mix(v, dist[r][v], nh[r][v][0..words))  (mod 2^64)
+ * into d_out[r], asynchronously on the context stream. Equal rows give equal
+ * digests whatever produced them, so a batch too large to copy out (the C4
+ * what-if job: 262,144 rows x 50,000 nodes) is compared row by row with
+ * another run or an independent checker (mix: tests/helpers.py row_digest). */
+int orh_row_digest(orh_ctx* ctx, const uint32_t* d_dist, const uint32_t* d_nh, uint32_t words, uint32_t n,
+                   uint32_t n_rows, uint64_t* d_out);
+
 /* ---- graph mirror (one per area LinkState) ---------------------------- */
 int orh_graph_create(orh_ctx* ctx, orh_graph** out_graph);
 int orh_graph_destroy(orh_graph* g);
@@ -423,6 +433,12 @@ typedef struct orh_select_out {
 /* asynchronous on the context stream; the area table is copied */
 int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
                      const orh_select_area* h_areas, const orh_select_out* out);
+/* the same for the prefix ids [pid_lo, pid_hi) only (a prefix shard of a
+ * route build): out arrays are still indexed by prefix id
+ * (sized for pid_hi), entries outside the range are not written */
+int orh_route_select_range(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
+                           const orh_select_area* h_areas, uint32_t pid_lo, uint32_t pid_hi,
+                           const orh_select_out* out);
 /* Keyed compare of two selection outputs of the same prefix set (the device
  * half of DecisionRouteDb::calculateUpdate, Decision.cpp:108-143): prefix p
  * < n_prefix whose record (status, metric, best, mask words) differs from
@@ -469,6 +485,10 @@ typedef struct orh_policy {
 } orh_policy;
 int orh_route_policy(orh_prefix_set* ps, uint32_t n_prefix, const orh_select_out* sel,
                      const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated);
+/* the same for the prefix ids [pid_lo, pid_hi) only (a prefix shard): d_out
+ * indexed by prefix id, *d_invalidated counts the range's routes */
+int orh_route_policy_range(orh_prefix_set* ps, uint32_t pid_lo, uint32_t pid_hi, const orh_select_out* sel,
+                           const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated);
 
 #ifdef __cplusplus
 }

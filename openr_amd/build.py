@@ -30,7 +30,8 @@ HIP_SRCS = [os.path.join(CSRC, "orh_api.hip"), os.path.join(CSRC, "kernels", "sp
             os.path.join(CSRC, "kernels", "ksp_kernels.hip")]
 HOST_SRCS = [os.path.join(CSRC, "host", f) for f in ("link_state.cpp", "prefix_state.cpp", "spf_solver.cpp",
                                                    "rib_policy.cpp", "thrift_compact.cpp",
-                                                   "decision_ingest.cpp", "multi_device.cpp", "host_py.cpp")]
+                                                   "decision_ingest.cpp", "multi_device.cpp", "whatif_batch.cpp",
+                                                   "host_py.cpp")]
 
 
 def _hipcc() -> str:
@@ -45,14 +46,6 @@ def _stale(target: str, deps) -> bool:
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
-
-
-def _deps(srcs, hdr_dirs):
-    out = list(srcs)
-    for d in hdr_dirs:
-        for root, _, files in os.walk(d):
-            out += [os.path.join(root, f) for f in files if f.endswith((".h", ".hpp"))]
-    return out
 
 
 def _run(cmd):
@@ -98,13 +91,26 @@ def build_hip_lib(force: bool = False) -> str:
 
 
 def build_host_module(force: bool = False) -> str:
+    """One object per host source (rebuilt when it or a header it includes
+    changed), compiled in parallel, then one shared link against libopenr_hip."""
     import pybind11
-    deps = _deps(HOST_SRCS, [os.path.join(CSRC, "host"), os.path.join(ROOT, "include")]) + [HIP_LIB]
-    if force or _stale(HOST_MOD, deps):
-        tmp = HOST_MOD + ".tmp"
-        _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+    obj_dir = os.path.join(LIB_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    objs = [os.path.join(obj_dir, os.path.basename(s) + ".o") for s in HOST_SRCS]
+    todo = [(s, o) for s, o in zip(HOST_SRCS, objs) if force or _stale(o, sorted(_includes(s)))]
+
+    def compile_one(so):
+        src, obj = so
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-c",
               f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-              f"-I{os.path.join(ROOT, 'include')}", "-o", tmp] + HOST_SRCS +
+              f"-I{os.path.join(ROOT, 'include')}", "-o", obj + ".tmp", src])
+        os.replace(obj + ".tmp", obj)
+
+    with ThreadPoolExecutor(max(1, min(8, len(todo)))) as ex:
+        list(ex.map(compile_one, todo))
+    if force or todo or _stale(HOST_MOD, objs + [HIP_LIB]):
+        tmp = HOST_MOD + ".tmp"
+        _run(["g++", "-shared", "-fPIC", "-o", tmp] + objs +
              [f"-L{LIB_DIR}", "-lopenr_hip", "-Wl,-rpath,$ORIGIN/lib"])
         os.replace(tmp, HOST_MOD)
     return HOST_MOD

@@ -396,144 +396,6 @@ class SpfSweep {
   uint32_t* dNh_{nullptr};
 };
 
-// batched link-failure what-if SPFs through a what-if job (orh_whatif_*):
-// requests (source index, ignored link ids) over a fixed source list, run in
-// chunks of `chunk` requests into one device row buffer (the C4 shape,
-// 4,096 links x 64 sources = 262,144 runSpf(src, true, {link}));
-// run() = the sources' plain searches + every chunk, asynchronously
-class WhatIfBatch {
- public:
-  WhatIfBatch(const LinkState& ls, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
-              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric,
-              bool shareBase = false)
-      : useLinkMetric_(useLinkMetric), shareBase_(shareBase) {
-    if (srcIdx.size() != ignore.size()) throw std::invalid_argument("WhatIfBatch: one ignore set per request");
-    if (chunk == 0) throw std::invalid_argument("WhatIfBatch: chunk must be positive");
-    for (const auto& s : srcs) {
-      auto id = ls.nodeId(s);
-      if (!id) throw std::invalid_argument("WhatIfBatch: unknown source " + s);
-      srcs_.push_back(*id);
-    }
-    for (uint32_t i : srcIdx)
-      if (i >= srcs_.size()) throw std::invalid_argument("WhatIfBatch: source index out of range");
-    srcIdx_ = srcIdx;
-    // per chunk: ignore CSR rebased to the chunk
-    const size_t n = srcIdx.size();
-    chunk_ = static_cast<uint32_t>(std::min<size_t>(chunk, std::max<size_t>(n, 1)));
-    for (size_t c0 = 0; c0 < n; c0 += chunk_) {
-      const size_t c1 = std::min(n, c0 + chunk_);
-      std::vector<uint32_t> ptr{0}, links;
-      for (size_t i = c0; i < c1; ++i) {
-        links.insert(links.end(), ignore[i].begin(), ignore[i].end());
-        ptr.push_back(static_cast<uint32_t>(links.size()));
-      }
-      if (links.empty()) links.push_back(0);  // non-null pointer
-      chunks_.push_back({c0, c1, std::move(ptr), std::move(links)});
-    }
-    graph_ = ls.deviceGraph();
-    ctx_ = ls.context();
-    orh_graph_info(graph_, &n_, &edges_);
-    // up to three row buffers, cycled between chunks, so a chunk's repairs
-    // (which write into its rows) overlap the next two chunks' copies
-    const size_t rows = static_cast<size_t>(chunk_) * n_;
-    nBuf_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(chunks_.size(), kBufs)));
-    for (int b = 0; b < nBuf_; ++b)
-      if (orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dDist_[b])) != ORH_OK ||
-          orh_device_alloc(ctx_, rows * 4, reinterpret_cast<void**>(&dNh_[b])) != ORH_OK)
-        throw std::runtime_error("WhatIfBatch: device allocation failed");
-    if (orh_device_alloc(ctx_, std::max<size_t>(n, 1) * 4, reinterpret_cast<void**>(&dInfo_)) != ORH_OK)
-      throw std::runtime_error("WhatIfBatch: device allocation failed");
-  }
-  ~WhatIfBatch() {
-    if (job_) orh_whatif_destroy(job_);
-    for (int b = 0; b < nBuf_; ++b) {
-      orh_device_free(ctx_, dDist_[b]);
-      orh_device_free(ctx_, dNh_[b]);
-    }
-    orh_device_free(ctx_, dInfo_);
-  }
-  void run() {  // asynchronous on the context stream: the base searches, then every chunk
-    if (!job_) {
-      if (orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
-                            &job_) != ORH_OK)
-        throw std::runtime_error(std::string("orh_whatif_create: ") + orh_last_error(ctx_));
-      if (shareBase_ && orh_whatif_set_flags(job_, ORH_WHATIF_SHARE_BASE) != ORH_OK)
-        throw std::runtime_error(std::string("orh_whatif_set_flags: ") + orh_last_error(ctx_));
-    } else if (orh_whatif_refresh(job_) != ORH_OK) {
-      throw std::runtime_error(std::string("orh_whatif_refresh: ") + orh_last_error(ctx_));
-    }
-    for (const auto& c : chunks_) {
-      const uint32_t nr = static_cast<uint32_t>(c.hi - c.lo);
-      const int b = static_cast<int>((&c - chunks_.data()) % nBuf_);  // cycle the row buffers
-      if (orh_whatif_run(job_, nr, srcIdx_.data() + c.lo, c.ptr.data(), c.links.data(), dDist_[b], dNh_[b],
-                         dInfo_ + c.lo) != ORH_OK)
-        throw std::runtime_error(std::string("orh_whatif_run: ") + orh_last_error(ctx_));
-    }
-    if (orh_whatif_flush(job_) != ORH_OK)
-      throw std::runtime_error(std::string("orh_whatif_flush: ") + orh_last_error(ctx_));
-  }
-  double lastMs() {
-    double ms = 0;
-    if (!job_ || orh_whatif_elapsed_ms(job_, &ms) != ORH_OK) throw std::runtime_error("orh_whatif_elapsed_ms failed");
-    return ms;
-  }
-  void sync() {
-    if (orh_sync(ctx_) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
-  }
-  py::array_t<uint32_t> info() {
-    py::array_t<uint32_t> out(srcIdx_.size());
-    orh_memcpy_d2h(ctx_, out.mutable_data(), dInfo_, srcIdx_.size() * 4);
-    return out;
-  }
-  // rows of request i; only the last chunk's rows are still in the buffer
-  py::tuple fetch(size_t i) {
-    const auto& last = chunks_.back();
-    if (i < last.lo || i >= last.hi) throw std::out_of_range("WhatIfBatch.fetch: not in the last chunk");
-    const size_t r = i - last.lo;
-    const int b = static_cast<int>((chunks_.size() - 1) % nBuf_);
-    const uint32_t* d = dDist_[b] + r * n_;
-    const uint32_t* m = dNh_[b] + r * n_;
-    if (shareBase_) {  // a request whose source row stands reads the job's base row
-      uint32_t inf = 0;
-      orh_memcpy_d2h(ctx_, &inf, dInfo_ + i, 4);
-      if (ORH_WHATIF_TIER(inf) == 0) {
-        const uint32_t *bd = nullptr, *bn = nullptr;
-        if (orh_whatif_base_rows(job_, &bd, &bn) != ORH_OK) throw std::runtime_error(orh_last_error(ctx_));
-        d = bd + static_cast<size_t>(srcIdx_[i]) * n_;
-        m = bn + static_cast<size_t>(srcIdx_[i]) * n_;
-      }
-    }
-    py::array_t<uint32_t> dist(n_), nh(n_);
-    orh_memcpy_d2h(ctx_, dist.mutable_data(), d, n_ * 4ull);
-    orh_memcpy_d2h(ctx_, nh.mutable_data(), m, n_ * 4ull);
-    return py::make_tuple(dist, nh);
-  }
-  size_t requests() const { return srcIdx_.size(); }
-  uint32_t chunk() const { return chunk_; }
-  uint32_t nodes() const { return n_; }
-  uint32_t edges() const { return edges_; }
-
- private:
-  struct Chunk {
-    size_t lo, hi;
-    std::vector<uint32_t> ptr, links;
-  };
-  bool useLinkMetric_;
-  bool shareBase_;
-  std::vector<uint32_t> srcs_, srcIdx_;
-  std::vector<Chunk> chunks_;
-  uint32_t chunk_{1};
-  orh_graph* graph_{nullptr};
-  orh_ctx* ctx_{nullptr};
-  orh_whatif* job_{nullptr};
-  uint32_t n_{0}, edges_{0};
-  static constexpr size_t kBufs = 3;
-  int nBuf_{1};
-  uint32_t* dDist_[kBufs] = {};
-  uint32_t* dNh_[kBufs] = {};
-  uint32_t* dInfo_{nullptr};
-};
-
 // ---- canonical route-db digest --------------------------------------------
 // Per route: fields serialised in order (integers little-endian, strings and
 // lists length-prefixed, optionals with a presence byte, nexthops sorted by
@@ -750,6 +612,12 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              return out;
            })
+      .def("get_kth_path_ids",  // getKthPaths as LinkState link ids
+           [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
+             py::list out;
+             for (const auto& p : s.getKthPathIds(a, b, k)) out.append(py::cast(p));
+             return out;
+           })
       .def("walk_kth_paths",  // the reference-typed getKthPaths (LinkRef handles) walked
                               // as selectBestPathsKsp2 does (Decision.cpp:1035-1076):
                               // per link from `src` (metric from the near end, near
@@ -956,7 +824,21 @@ PYBIND11_MODULE(_openr_host, m) {
              return new MultiDeviceSweep(s, srcs, useLinkMetric);
            },
            py::arg("srcs"), py::arg("use_link_metric") = true, py::return_value_policy::take_ownership,
-           py::keep_alive<0, 1>());
+           py::keep_alive<0, 1>())
+      .def("what_if_batch",
+           [](const ReplicatedLinkState& s, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
+              const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric,
+              bool shareBase) {
+             return new MultiDeviceWhatIf(s, srcs, srcIdx, ignore, chunk, useLinkMetric, shareBase);
+           },
+           py::arg("srcs"), py::arg("src_idx"), py::arg("ignore"), py::arg("chunk") = 4096,
+           py::arg("use_link_metric") = true, py::arg("share_base") = false,
+           py::return_value_policy::take_ownership, py::keep_alive<0, 1>())
+      .def("kth_paths_batch",
+           [](const ReplicatedLinkState& s, const std::vector<std::pair<std::string, std::string>>& pairs) {
+             return new MultiDeviceKthPaths(s, pairs);
+           },
+           py::arg("pairs"), py::return_value_policy::take_ownership, py::keep_alive<0, 1>());
   py::class_<MultiDeviceSweep>(m, "MultiDeviceSweep")
       .def("run", &MultiDeviceSweep::run)
       .def("run_block", &MultiDeviceSweep::runBlock, py::arg("block"))
@@ -980,16 +862,131 @@ PYBIND11_MODULE(_openr_host, m) {
         return py::make_tuple(dist, nh);
       });
 
+  // every area on several devices, the route build sharded over them by
+  // prefix (multi_device.h)
+  py::class_<ReplicatedAreaLinkStates>(m, "ReplicatedAreaLinkStates")
+      .def(py::init<const std::vector<int>&>(), py::arg("devices"))
+      .def("update_adjacency_database",
+           [](ReplicatedAreaLinkStates& s, py::tuple db, uint64_t up, uint64_t down) {
+             return changeToWire(s.updateAdjacencyDatabase(adjDbFromWire(db), up, down));
+           },
+           py::arg("db"), py::arg("hold_up_ttl") = 0, py::arg("hold_down_ttl") = 0)
+      .def("delete_adjacency_database",
+           [](ReplicatedAreaLinkStates& s, const std::string& area, const std::string& n) {
+             return changeToWire(s.deleteAdjacencyDatabase(area, n));
+           })
+      .def_property_readonly("replicas", &ReplicatedAreaLinkStates::replicas)
+      .def("route_builder",
+           [](const ReplicatedAreaLinkStates& s, const std::string& me, bool v4, bool orderedFib, bool bgpDryRun,
+              bool bestRoute) { return new ShardedRouteBuilder(s, me, v4, orderedFib, bgpDryRun, bestRoute); },
+           py::arg("my_node"), py::arg("enable_v4"), py::arg("enable_ordered_fib") = false,
+           py::arg("bgp_dry_run") = false, py::arg("enable_best_route_selection") = false,
+           py::return_value_policy::take_ownership, py::keep_alive<0, 1>());
+  py::class_<ShardedRouteBuilder>(m, "ShardedRouteBuilder")
+      .def_property_readonly("shards", &ShardedRouteBuilder::shards)
+      .def("build_route_db_digest",
+           [](ShardedRouteBuilder& b, const std::string& me, const PrefixState& ps) -> py::object {
+             auto db = b.buildRouteDb(me, ps);
+             if (!db) return py::none();
+             return routeDbDigest(*db);
+           })
+      .def("build_route_db",
+           [](ShardedRouteBuilder& b, const std::string& me, const PrefixState& ps) -> py::object {
+             auto db = b.buildRouteDb(me, ps);
+             if (!db) return py::none();
+             return routeDbToWire(*db);
+           })
+      .def("time_build_route_db",  // (seconds, routes, per-shard ms, merge ms)
+           [](ShardedRouteBuilder& b, const std::string& me, const PrefixState& ps) {
+             double sec = 0;
+             size_t n = 0;
+             {
+               py::gil_scoped_release nogil;
+               const auto t0 = std::chrono::steady_clock::now();
+               auto db = b.buildRouteDb(me, ps);
+               sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+               n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
+             }
+             std::vector<double> shardMs;
+             for (size_t r = 0; r < b.shards(); ++r) shardMs.push_back(b.lastShardMs(r));
+             return py::make_tuple(sec, n, shardMs, b.lastMergeMs());
+           })
+      .def("time_build_shard",  // shard r alone: (seconds, routes)
+           [](ShardedRouteBuilder& b, size_t r, const std::string& me, const PrefixState& ps) {
+             py::gil_scoped_release nogil;
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = b.buildShard(r, me, ps);
+             const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
+             return std::make_pair(sec, n);
+           });
+
+  // batched link-failure what-if SPFs (whatif_batch.h)
   py::class_<WhatIfBatch>(m, "WhatIfBatch")
       .def("run", &WhatIfBatch::run)
       .def("last_ms", &WhatIfBatch::lastMs)
       .def("sync", &WhatIfBatch::sync)
-      .def("info", &WhatIfBatch::info)
-      .def("fetch", &WhatIfBatch::fetch)
+      .def("release", &WhatIfBatch::release)
+      .def("set_digests", &WhatIfBatch::setDigests, py::arg("on") = true)
+      .def("info",
+           [](const WhatIfBatch& b) {
+             py::array_t<uint32_t> out(b.requests());
+             b.info(out.mutable_data());
+             return out;
+           })
+      .def("digests",
+           [](const WhatIfBatch& b) {
+             py::array_t<uint64_t> out(b.requests());
+             b.digests(out.mutable_data());
+             return out;
+           })
+      .def("fetch",
+           [](const WhatIfBatch& b, size_t i) {
+             py::array_t<uint32_t> dist(b.nodes()), nh(b.nodes());
+             b.fetch(i, dist.mutable_data(), nh.mutable_data());
+             return py::make_tuple(dist, nh);
+           })
       .def_property_readonly("requests", &WhatIfBatch::requests)
       .def_property_readonly("chunk", &WhatIfBatch::chunk)
       .def_property_readonly("nodes", &WhatIfBatch::nodes)
       .def_property_readonly("edges", &WhatIfBatch::edges);
+
+  // a what-if job / KSP2 batch split over devices by source (multi_device.h)
+  py::class_<MultiDeviceWhatIf>(m, "MultiDeviceWhatIf")
+      .def("run", &MultiDeviceWhatIf::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_block", &MultiDeviceWhatIf::runBlock, py::arg("block"))
+      .def("sync", &MultiDeviceWhatIf::sync)
+      .def("release", &MultiDeviceWhatIf::release, py::arg("block"))
+      .def("set_digests", &MultiDeviceWhatIf::setDigests, py::arg("on") = true)
+      .def("last_ms", &MultiDeviceWhatIf::lastMs, py::arg("block"))
+      .def("source_block", &MultiDeviceWhatIf::sourceBlock)
+      .def("block_requests", &MultiDeviceWhatIf::blockRequests)
+      .def_property_readonly("blocks", &MultiDeviceWhatIf::blocks)
+      .def_property_readonly("requests", &MultiDeviceWhatIf::requests)
+      .def("info",
+           [](const MultiDeviceWhatIf& b) {
+             py::array_t<uint32_t> out(b.requests());
+             b.info(out.mutable_data());
+             return out;
+           })
+      .def("digests", [](const MultiDeviceWhatIf& b) {
+        py::array_t<uint64_t> out(b.requests());
+        b.digests(out.mutable_data());
+        return out;
+      });
+  py::class_<MultiDeviceKthPaths>(m, "MultiDeviceKthPaths")
+      .def("run", &MultiDeviceKthPaths::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_block", &MultiDeviceKthPaths::runBlock, py::arg("block"))
+      .def("last_ms", &MultiDeviceKthPaths::lastMs, py::arg("block"))
+      .def("block_pairs", &MultiDeviceKthPaths::blockPairs)
+      .def_property_readonly("blocks", &MultiDeviceKthPaths::blocks)
+      .def_property_readonly("pairs", &MultiDeviceKthPaths::pairs)
+      .def_property_readonly("device_pairs", &MultiDeviceKthPaths::devicePairs)
+      .def("paths", [](const MultiDeviceKthPaths& b, size_t i, size_t k) {
+        py::list out;
+        for (const auto& p : b.paths(i, k)) out.append(py::cast(p));
+        return out;
+      });
 
   // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
   // ---- thrift Compact wire -----------------------

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <exception>
@@ -14,6 +15,7 @@
 #include <functional>
 #include <malloc.h>
 #include <mutex>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -40,6 +42,9 @@ class WorkerPool {
       fn(0, 0, n);
       return;
     }
+    // one job at a time: callers on other threads (multi-device builds drive
+    // each device from its own thread) queue here and then get the whole pool
+    std::lock_guard<std::mutex> turn(callerMu_);
     struct Mark {
       Mark() { inJob_ = true; }
       ~Mark() { inJob_ = false; }
@@ -131,6 +136,7 @@ class WorkerPool {
   }
 
   std::vector<std::thread> workers_;
+  std::mutex callerMu_;
   std::mutex mu_;
   std::condition_variable cv_, done_;
   const std::function<void(size_t, size_t, size_t)>* job_{nullptr};
@@ -140,5 +146,26 @@ class WorkerPool {
   std::exception_ptr err_;
   static inline thread_local bool inJob_ = false;
 };
+
+// parts[w] -> into, shard by shard on the pool (ShardedMap parts: nodes are
+// spliced, no entry is copied); a key in two parts is a duplicate route
+// (RouteUpdate.h:39 CHECK)
+template <class Map>
+void mergeParts(Map& into, std::vector<Map>& parts, WorkerPool& pool) {
+  std::atomic<bool> dup{false};
+  pool.parallelFor(Map::kShards, [&](size_t, size_t b, size_t e) {
+    for (size_t s = b; s < e; ++s) {
+      auto& dst = into.shard(s);
+      size_t n = dst.size();
+      for (auto& p : parts) n += p.shard(s).size();
+      dst.reserve(n);
+      for (auto& p : parts) {
+        dst.merge(p.shard(s));
+        if (!p.shard(s).empty()) dup = true;
+      }
+    }
+  });
+  if (dup) throw std::logic_error("duplicate unicast route");
+}
 
 }  // namespace openr_amd

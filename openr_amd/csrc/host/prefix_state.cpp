@@ -23,7 +23,8 @@ void check(orh_ctx* ctx, int rc, const char* what) {
 }  // namespace
 
 PrefixState::~PrefixState() {
-  if (dev_) orh_prefix_destroy(dev_);
+  for (auto& m : mirrors_)
+    if (m->dev) orh_prefix_destroy(m->dev);
 }
 
 std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
@@ -142,6 +143,14 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
     isDirty_[pid] = 1;
     dirty_.push_back(pid);
   }
+  for (auto& m : mirrors_) {  // every device mirror re-uploads it at its next sync
+    if (m->full) continue;
+    if (m->isDirty.size() <= pid) m->isDirty.resize(cidrOf_.size(), 0);
+    if (!m->isDirty[pid]) {
+      m->isDirty[pid] = 1;
+      m->dirty.push_back(pid);
+    }
+  }
 }
 
 // the device record of one advertisement
@@ -156,23 +165,64 @@ orh_adv PrefixState::advRecord(const NodeAndArea& na, const PrefixEntry& e) cons
   return orh_adv{nameIds_.at(na.first), meta, e.pathPreference, e.sourcePreference, e.distance};
 }
 
+void PrefixState::buildRecords(const std::vector<uint32_t>* ids, std::vector<uint32_t>& ptr,
+                               std::vector<orh_adv>& recs, std::vector<uint8_t>& fl) const {
+  const size_t n = ids ? ids->size() : cidrOf_.size();
+  ptr.assign(n + 1, 0);
+  fl.assign(n, 0);
+  auto& pool = WorkerPool::instance();
+  auto each = [&](auto&& fn) {
+    if (n >= 16384 && pool.size() > 1) {
+      pool.parallelFor(n, [&](size_t, size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) fn(i);
+      });
+    } else {
+      for (size_t i = 0; i < n; ++i) fn(i);
+    }
+  };
+  each([&](size_t i) {
+    const uint32_t pid = ids ? (*ids)[i] : static_cast<uint32_t>(i);
+    if (!live_[pid]) return;
+    ptr[i + 1] = run_[pid].second;
+    fl[i] = cidrOf_[pid].first.size() == 4 ? ORH_PFX_V4 : 0;
+  });
+  for (size_t i = 0; i < n; ++i) ptr[i + 1] += ptr[i];
+  recs.resize(ptr[n]);
+  each([&](size_t i) {
+    const uint32_t pid = ids ? (*ids)[i] : static_cast<uint32_t>(i);
+    if (!live_[pid]) return;
+    const AdvRef* a = advPool_.data() + run_[pid].first;
+    for (uint32_t k = 0; k < ptr[i + 1] - ptr[i]; ++k) recs[ptr[i] + k] = advRecord(*a[k].key, *a[k].entry);
+  });
+}
+
 orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
   if (areas_.size() > ORH_ADV_AREA_MASK + 1)
     throw std::runtime_error("PrefixState: more than 256 areas for the device mirror");
-  if (dev_ && devCtx_ != ctx) {
-    orh_prefix_destroy(dev_);
-    dev_ = nullptr;
+  std::lock_guard<std::mutex> lock(syncMu_);
+  Mirror* m = nullptr;
+  for (auto& x : mirrors_)
+    if (x->ctx == ctx) m = x.get();
+  if (!m) {
+    auto fresh = std::make_unique<Mirror>();
+    fresh->ctx = ctx;
+    check(ctx, orh_prefix_create(ctx, &fresh->dev), "orh_prefix_create");
+    m = fresh.get();
+    mirrors_.push_back(std::move(fresh));
   }
-  if (!dev_) {
-    check(ctx, orh_prefix_create(ctx, &dev_), "orh_prefix_create");
-    devCtx_ = ctx;
-    devFull_ = true;
-    namesOrdered_ = areasOrdered_ = 0;
-  }
-  auto& self = const_cast<PrefixState&>(*this);  // dirty list: bookkeeping only
-  // host pool mostly garbage: renumber every prefix (device reloaded too)
-  if (advPool_.size() > 4096 && advPool_.size() > 2 * advLive_) devFull_ = true;
-  if (devFull_) {
+  auto& self = const_cast<PrefixState&>(*this);  // dirty lists: bookkeeping only
+  // 1. the host runs (advertisements per prefix id in device numbering order).
+  // Host pool mostly garbage: renumber every prefix (and reload every device
+  // mirror, whose pools hold the same garbage)
+  if (advPool_.size() > 4096 && advPool_.size() > 2 * advLive_) hostFull_ = true;
+  // the records the host pass built, reused by the mirrors that need exactly
+  // those prefixes (every mirror, when one device builds)
+  bool builtAll = false;
+  std::vector<uint32_t> bPtr;
+  std::vector<orh_adv> bRecs;
+  std::vector<uint8_t> bFl;
+  std::vector<uint32_t> bIds;
+  if (hostFull_) {
     // every prefix's run, in pid order: counts, offsets, then the records,
     // each pass on the worker pool for large states (C5: 1M prefixes)
     const uint32_t n = static_cast<uint32_t>(cidrOf_.size());
@@ -212,12 +262,17 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
         ++k;
       }
     });
-    check(ctx, orh_prefix_load(dev_, static_cast<uint32_t>(cidrOf_.size()), ptr.data(), recs.data(),
-                               fl.data()),
-          "orh_prefix_load");
-    devFull_ = false;
+    hostFull_ = false;
+    builtAll = true;
+    bPtr = std::move(ptr);
+    bRecs = std::move(recs);
+    bFl = std::move(fl);
+    for (auto& x : mirrors_) {
+      x->full = true;
+      x->dirty.clear();
+      x->isDirty.clear();
+    }
   } else if (!dirty_.empty()) {
-    const auto t0 = std::chrono::steady_clock::now();
     // the dirty prefixes' runs appended to the host pool in dirty order (the
     // numbering the device delta uses): counts, offsets, then the records,
     // on the worker pool for large deltas
@@ -263,20 +318,35 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
         ++k;
       }
     });
-    const auto t1 = std::chrono::steady_clock::now();
-    check(ctx, orh_prefix_apply_delta(dev_, static_cast<uint32_t>(dirty_.size()), dirty_.data(),
-                                      ptr.data(), recs.data(), fl.data()),
-          "orh_prefix_apply_delta");
-    if (std::getenv("ORH_ROUTE_PROF")) {  // phase times (see spf_solver.cpp)
-      const auto t2 = std::chrono::steady_clock::now();
-      std::fprintf(stderr, "route-prof   sync: %zu dirty prefixes, runs %.3f ms, device delta %.3f ms\n", dirty_.size(),
-                   std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                   std::chrono::duration<double, std::milli>(t2 - t1).count());
-    }
+    bIds = dirty_;
+    bPtr = std::move(ptr);
+    bRecs = std::move(recs);
+    bFl = std::move(fl);
   }
   for (uint32_t pid : dirty_) self.isDirty_[pid] = 0;
   self.dirty_.clear();
-  if (namesOrdered_ != names_.size() || areasOrdered_ != areas_.size()) {
+  // 2. this context's device mirror
+  if (m->full) {
+    if (!builtAll) buildRecords(nullptr, bPtr, bRecs, bFl);
+    check(ctx, orh_prefix_load(m->dev, static_cast<uint32_t>(cidrOf_.size()), bPtr.data(), bRecs.data(),
+                               bFl.data()),
+          "orh_prefix_load");
+    m->full = false;
+  } else if (!m->dirty.empty()) {
+    const auto t1 = std::chrono::steady_clock::now();
+    if (m->dirty != bIds) buildRecords(&m->dirty, bPtr, bRecs, bFl);
+    check(ctx, orh_prefix_apply_delta(m->dev, static_cast<uint32_t>(m->dirty.size()), m->dirty.data(),
+                                      bPtr.data(), bRecs.data(), bFl.data()),
+          "orh_prefix_apply_delta");
+    if (std::getenv("ORH_ROUTE_PROF")) {  // phase times (see spf_solver.cpp)
+      const auto t2 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "route-prof   sync: %zu dirty prefixes, device delta %.3f ms\n", m->dirty.size(),
+                   std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
+  }
+  for (uint32_t pid : m->dirty) m->isDirty[pid] = 0;
+  m->dirty.clear();
+  if (m->namesOrdered != names_.size() || m->areasOrdered != areas_.size()) {
     // std::set<NodeAndArea> order = byte order of the names, then areas
     auto ranks = [](const std::vector<std::string>& v) {
       std::vector<uint32_t> idx(v.size()), rank(v.size());
@@ -286,13 +356,13 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
       return rank;
     };
     const auto nr = ranks(names_), ar = ranks(areas_);
-    check(ctx, orh_prefix_set_order(dev_, static_cast<uint32_t>(names_.size()), nr.data(),
+    check(ctx, orh_prefix_set_order(m->dev, static_cast<uint32_t>(names_.size()), nr.data(),
                                     static_cast<uint32_t>(areas_.size()), ar.data()),
           "orh_prefix_set_order");
-    namesOrdered_ = static_cast<uint32_t>(names_.size());
-    areasOrdered_ = static_cast<uint32_t>(areas_.size());
+    m->namesOrdered = static_cast<uint32_t>(names_.size());
+    m->areasOrdered = static_cast<uint32_t>(areas_.size());
   }
-  return dev_;
+  return m->dev;
 }
 
 }  // namespace openr_amd

@@ -36,26 +36,6 @@ struct RouteProf {
   }
 };
 
-// parts[w] -> into, shard by shard on the pool; a key in two parts is a
-// duplicate route (RouteUpdate.h:39 CHECK)
-template <class Map>
-void mergeParts(Map& into, std::vector<Map>& parts, WorkerPool& pool) {
-  std::atomic<bool> dup{false};
-  pool.parallelFor(Map::kShards, [&](size_t, size_t b, size_t e) {
-    for (size_t s = b; s < e; ++s) {
-      auto& dst = into.shard(s);
-      size_t n = dst.size();
-      for (auto& p : parts) n += p.shard(s).size();
-      dst.reserve(n);
-      for (auto& p : parts) {
-        dst.merge(p.shard(s));
-        if (!p.shard(s).empty()) dup = true;
-      }
-    }
-  });
-  if (dup) throw std::logic_error("duplicate unicast route");
-}
-
 MplsAction mpls(int32_t code, std::optional<int32_t> swap = std::nullopt,
                 std::optional<std::vector<int32_t>> push = std::nullopt) {
   // createMplsAction + checkMplsAction (Util.cpp:482-512, :793-803)
@@ -884,8 +864,10 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
   const auto meName = ps.nameId(me);
   uint32_t flags = (enableBestRouteSelection_ ? ORH_SELECT_BEST_ROUTE : 0u) |
       (enableV4_ ? ORH_SELECT_V4 : 0u);
-  if (orh_route_select(set, meName ? *meName : ORH_NO_NODE, flags,
-                       static_cast<uint32_t>(order.size()), sel.data(), &out) != ORH_OK)
+  // a prefix shard selects (and copies back) its own block of prefix ids only
+  const auto [pidLo, pidHi] = shardRange(n);
+  if (orh_route_select_range(set, meName ? *meName : ORH_NO_NODE, flags, static_cast<uint32_t>(order.size()),
+                             sel.data(), pidLo, pidHi, &out) != ORH_OK)
     throw std::runtime_error(std::string("orh_route_select: ") + orh_last_error(ctx));
   {
     uint32_t np = 0, live = 0;
@@ -894,6 +876,7 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     for (const auto& sa : sel) areasWithRow += sa.d_dist ? 1 : 0;
     lastSelectBytes_ = 8ull * np + 20ull * live + 4ull * live * areasWithRow +
         static_cast<uint64_t>(np) * (9 + 4ull * words);
+    if (np) lastSelectBytes_ = lastSelectBytes_ * (pidHi - pidLo) / np;  // the shard's share
   }
   prof.mark(" select: launch");
   const bool canDiff = diff && hadPrev && dSelPrev_ && prevWords_ == words && prevLayout_ == layout &&
@@ -938,10 +921,11 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     selMetric_.resize(n);
     selBest_.resize(n);
     selMask_.resize(static_cast<size_t>(n) * words);
-    if (orh_memcpy_d2h(ctx, selStatus_.data(), out.d_status, n) != ORH_OK ||
-        orh_memcpy_d2h(ctx, selMetric_.data(), out.d_metric, 4ull * n) != ORH_OK ||
-        orh_memcpy_d2h(ctx, selBest_.data(), out.d_best, 4ull * n) != ORH_OK ||
-        orh_memcpy_d2h(ctx, selMask_.data(), out.d_mask, 4ull * n * words) != ORH_OK)
+    const size_t lo = pidLo, cnt = pidHi - pidLo;
+    if (orh_memcpy_d2h(ctx, selStatus_.data() + lo, out.d_status + lo, cnt) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selMetric_.data() + lo, out.d_metric + lo, 4ull * cnt) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selBest_.data() + lo, out.d_best + lo, 4ull * cnt) != ORH_OK ||
+        orh_memcpy_d2h(ctx, selMask_.data() + lo * words, out.d_mask + lo * words, 4ull * cnt * words) != ORH_OK)
       throw std::runtime_error(std::string("route select copy-out: ") + orh_last_error(ctx));
   }
   prof.mark(" select: copy-out");
@@ -1148,23 +1132,35 @@ bool SpfSolver::policyOnDevice(const PrefixState& ps, RibPolicy& policy) {
   pol.h_pfx_stmts = pfxStmts.data();
   pol.h_keep = keep.data();
   orh_ctx* ctx = selCtx_;
+  // a device failure here leaves the decision to the host: the caller then
+  // runs RibPolicy::applyPolicy over the built routes (same result)
+  auto hostPath = [&](const char* what) {
+    std::fprintf(stderr, "openr_amd: %s failed (%s); RibPolicy applied on the host\n", what, orh_last_error(ctx));
+    devPol_.reset();
+    return false;
+  };
   const size_t need = n + 64;  // out bytes | invalidated (aligned)
   if (need > dPolOutCap_) {
+    const size_t cap = std::max(need, 2 * dPolOutCap_);
     if (dPolOut_) orh_device_free(ctx, dPolOut_);
     dPolOut_ = nullptr;
-    dPolOutCap_ = std::max(need, 2 * dPolOutCap_);
-    if (orh_device_alloc(ctx, dPolOutCap_, reinterpret_cast<void**>(&dPolOut_)) != ORH_OK)
-      throw std::runtime_error("route policy: device allocation failed");
+    dPolOutCap_ = 0;
+    if (orh_device_alloc(ctx, cap, reinterpret_cast<void**>(&dPolOut_)) != ORH_OK)
+      return hostPath("route policy: device allocation");
+    dPolOutCap_ = cap;
   }
   uint32_t* dInv = reinterpret_cast<uint32_t*>(dPolOut_ + ((n + 15) & ~size_t{15}));
   const orh_select_out sel = selOut(dSelPrev_, n, words);
-  if (orh_route_policy(ps.syncDevice(ctx), n, &sel, &pol, dPolOut_, dInv) != ORH_OK)
-    throw std::runtime_error(std::string("orh_route_policy: ") + orh_last_error(ctx));
+  // a prefix shard decides (and counts the invalidated routes of) its own
+  // block only
+  const auto [lo, hi] = shardRange(n);
+  if (orh_route_policy_range(ps.syncDevice(ctx), lo, hi, &sel, &pol, dPolOut_, dInv) != ORH_OK)
+    return hostPath("orh_route_policy");
   devPol_.stmt.resize(n);
   uint32_t inv = 0;
-  if (orh_memcpy_d2h(ctx, devPol_.stmt.data(), dPolOut_, n) != ORH_OK ||
+  if (orh_memcpy_d2h(ctx, devPol_.stmt.data() + lo, dPolOut_ + lo, hi - lo) != ORH_OK ||
       orh_memcpy_d2h(ctx, &inv, dInv, 4) != ORH_OK)
-    throw std::runtime_error(std::string("route policy copy-out: ") + orh_last_error(ctx));
+    return hostPath("route policy copy-out");
   devPol_.deviceInvalidated = inv;
   devPol_.policy = &policy;
   devPol_.on = true;
@@ -1261,17 +1257,27 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   if (devPolicy) prof.mark("policy (device)");
   bool labelsDone = false;  // node-label routes built by the pipelined path
   std::vector<const Cidr*> keys;
+  // static unicast routes go to the shard of their prefix id (shard 0 when
+  // PrefixState lacks the prefix)
+  auto ownsStatic = [&](const Cidr& prefix) {
+    if (shardWorld_ <= 1) return true;
+    auto pid = ps.pidOf(prefix);
+    return pid ? ownsPid(*pid, ps.numPrefixIds()) : shardRank_ == 0;
+  };
   if (dev) {
     const uint32_t n = ps.numPrefixIds();
+    // a prefix shard materialises its own block of prefix ids [pidLo, pidHi)
+    const auto [pidLo, pidHi] = shardRange(n);
+    const uint32_t nOwn = pidHi - pidLo;
     uint64_t nHost = 0, nDev = 0;
-    for (uint32_t pid = 0; pid < n; ++pid) {
+    for (uint32_t pid = pidLo; pid < pidHi; ++pid) {
       if (!ps.prefixLive(pid)) continue;
       if (selStatus_[pid] == ORH_SEL_HOST) ++nHost; else ++nDev;
     }
     deviceSelected_ = nDev;
     hostSelected_ = nHost;
     auto one = [&](uint32_t pid, decltype(db.unicastRoutes)& out) {
-      if (!ps.prefixLive(pid) || !ownsPid(pid, n)) return;
+      if (!ps.prefixLive(pid)) return;
       if (selStatus_[pid] == ORH_SEL_ROUTE) {
         RibUnicastEntry e = materialize(pid, ps);
         Cidr k = e.prefix;
@@ -1286,17 +1292,20 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     };
     // one area with nexthop templates: unicast routes and node-label
     // candidates in one pool pass, then the two output maps are assembled
-    // concurrently (their insertion is the sequential part of the build)
+    // concurrently (their insertion is the sequential part of the build);
+    // node labels belong to shard 0
     const AreaWork* tw = nullptr;
     if (als.size() == 1)
       for (const auto& w : areaWork_)
         if (w.ls == &als.begin()->second && w.words) tw = &w;
-    if (!hasKsp && tw && shardWorld_ == 1 && n >= kParallelMin && pool.size() > 1) {
+    if (!hasKsp && tw && nOwn >= kParallelMin && pool.size() > 1) {
       const auto& [area, ls] = *als.begin();
       const SpfRow& myRow = ls.getSpfRow(me);
       std::vector<const AdjacencyDatabase*> dbs;
-      dbs.reserve(ls.getAdjacencyDatabases().size());
-      for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
+      if (shardRank_ == 0) {
+        dbs.reserve(ls.getAdjacencyDatabases().size());
+        for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
+      }
       std::vector<std::optional<RibMplsEntry>> cand(dbs.size());
       auto label = [&, &area = area, &ls = ls](size_t i) {
         const AdjacencyDatabase& adjDb = *dbs[i];
@@ -1326,16 +1335,16 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         cand[i] = std::move(entry);
       };
       std::vector<decltype(db.unicastRoutes)> parts(pool.size());
-      pool.parallelFor(n + dbs.size(), [&](size_t w, size_t b, size_t e) {
+      pool.parallelFor(nOwn + dbs.size(), [&](size_t w, size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) {
-          if (i < n) one(static_cast<uint32_t>(i), parts[w]);
-          else label(i - n);
+          if (i < nOwn) one(pidLo + static_cast<uint32_t>(i), parts[w]);
+          else label(i - nOwn);
         }
       });
       prof.mark("unicast + labels (pool)");
       mergeParts(db.unicastRoutes, parts, pool);
       for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
-        if (db.unicastRoutes.count(prefix)) continue;
+        if (db.unicastRoutes.count(prefix) || !ownsStatic(prefix)) continue;
         RibUnicastEntry se;
         se.prefix = prefix;
         se.nexthops.insert(nhs.begin(), nhs.end());
@@ -1345,36 +1354,38 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       prof.mark("unicast merge");
       // duplicate labels: the smaller node name wins among the nodes with a
       // route (:675-688); labels are resolved shard by shard on the pool
-      std::vector<std::vector<uint32_t>> byShard(MplsRouteMap::kShards);
-      for (size_t i = 0; i < dbs.size(); ++i) {
-        const int32_t lbl = dbs[i]->nodeLabel;
-        if (lbl == 0 || !isMplsLabelValid(lbl) || !cand[i]) continue;
-        byShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
-      }
-      pool.parallelFor(MplsRouteMap::kShards, [&](size_t, size_t b, size_t e) {
-        for (size_t sh = b; sh < e; ++sh) {
-          std::unordered_map<int32_t, uint32_t> win;
-          win.reserve(byShard[sh].size());
-          for (uint32_t i : byShard[sh]) {
-            auto [it, fresh] = win.emplace(dbs[i]->nodeLabel, i);
-            if (!fresh && dbs[i]->thisNodeName < dbs[it->second]->thisNodeName) it->second = i;
-          }
-          auto& dst = db.mplsRoutes.shard(sh);
-          dst.reserve(dst.size() + win.size() + 1);
-          for (auto& [lbl, i] : win) dst.emplace(lbl, std::move(*cand[i]));
+      if (!dbs.empty()) {
+        std::vector<std::vector<uint32_t>> byShard(MplsRouteMap::kShards);
+        for (size_t i = 0; i < dbs.size(); ++i) {
+          const int32_t lbl = dbs[i]->nodeLabel;
+          if (lbl == 0 || !isMplsLabelValid(lbl) || !cand[i]) continue;
+          byShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
         }
-      });
-      prof.mark("label map");
+        pool.parallelFor(MplsRouteMap::kShards, [&](size_t, size_t b, size_t e) {
+          for (size_t sh = b; sh < e; ++sh) {
+            std::unordered_map<int32_t, uint32_t> win;
+            win.reserve(byShard[sh].size());
+            for (uint32_t i : byShard[sh]) {
+              auto [it, fresh] = win.emplace(dbs[i]->nodeLabel, i);
+              if (!fresh && dbs[i]->thisNodeName < dbs[it->second]->thisNodeName) it->second = i;
+            }
+            auto& dst = db.mplsRoutes.shard(sh);
+            dst.reserve(dst.size() + win.size() + 1);
+            for (auto& [lbl, i] : win) dst.emplace(lbl, std::move(*cand[i]));
+          }
+        });
+        prof.mark("label map");
+      }
       labelsDone = true;
-    } else if (!hasKsp && n >= kParallelMin && pool.size() > 1) {
+    } else if (!hasKsp && nOwn >= kParallelMin && pool.size() > 1) {
       std::vector<decltype(db.unicastRoutes)> parts(pool.size());
-      pool.parallelFor(n, [&](size_t w, size_t b, size_t e) {
-        for (size_t pid = b; pid < e; ++pid) one(static_cast<uint32_t>(pid), parts[w]);
+      pool.parallelFor(nOwn, [&](size_t w, size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) one(pidLo + static_cast<uint32_t>(i), parts[w]);
       });
       prof.mark("unicast (pool)");
       mergeParts(db.unicastRoutes, parts, pool);
     } else {
-      for (uint32_t pid = 0; pid < n; ++pid) one(pid, db.unicastRoutes);
+      for (uint32_t pid = pidLo; pid < pidHi; ++pid) one(pid, db.unicastRoutes);
     }
   } else if (!mplsOnly) {
     keys.reserve(ps.prefixes().size());
@@ -1407,11 +1418,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   }
   if (!labelsDone && !mplsOnly) {
     for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
-      if (db.unicastRoutes.count(prefix)) continue;
-      if (shardWorld_ > 1) {  // the shard of its prefix id, shard 0 if PrefixState lacks it
-        auto pid = ps.pidOf(prefix);
-        if (pid ? !ownsPid(*pid, ps.numPrefixIds()) : shardRank_ != 0) continue;
-      }
+      if (db.unicastRoutes.count(prefix) || !ownsStatic(prefix)) continue;
       RibUnicastEntry e;
       e.prefix = prefix;
       e.nexthops.insert(nhs.begin(), nhs.end());
@@ -1423,10 +1430,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   if (policyActive) {
     uint64_t updated = 0, onDevice = 0;
     if (devPolicy) {
-      const uint32_t n = ps.numPrefixIds();
-      for (uint32_t pid = 0; pid < n; ++pid)
-        if (ps.prefixLive(pid) && ownsPid(pid, n) && selStatus_[pid] == ORH_SEL_ROUTE &&
-            devPol_.stmt[pid] != ORH_POL_HOST) {
+      const auto [pidLo, pidHi] = shardRange(ps.numPrefixIds());
+      for (uint32_t pid = pidLo; pid < pidHi; ++pid)
+        if (ps.prefixLive(pid) && selStatus_[pid] == ORH_SEL_ROUTE && devPol_.stmt[pid] != ORH_POL_HOST) {
           ++onDevice;
           updated += devPol_.stmt[pid] < ORH_POL_MAX_STMTS;
         }

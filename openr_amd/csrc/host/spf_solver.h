@@ -13,6 +13,8 @@
 #include <atomic>
 #include <deque>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <set>
 
 #include "link_state.h"
@@ -51,7 +53,8 @@ class PrefixState {
   size_t ksp2Entries() const { return ksp2Entries_; }
 
   // ---- device mirror (used by SpfSolver) ----
-  // brings the mirror on `ctx` up to date; returns it
+  // brings the mirror on `ctx` up to date (one mirror per context: a route
+  // build sharded over devices keeps one per device); returns it
   orh_prefix_set* syncDevice(orh_ctx* ctx) const;
   uint32_t numPrefixIds() const { return static_cast<uint32_t>(cidrOf_.size()); }
   const Cidr& prefixOf(uint32_t pid) const { return cidrOf_[pid]; }
@@ -124,10 +127,22 @@ class PrefixState {
   mutable std::vector<AdvRef> advPool_;
   mutable std::vector<std::pair<uint32_t, uint32_t>> run_;  // pid -> (offset, count)
   mutable size_t advLive_{0};
-  mutable orh_prefix_set* dev_{nullptr};
-  mutable orh_ctx* devCtx_{nullptr};
-  mutable bool devFull_{true};
-  mutable uint32_t namesOrdered_{0}, areasOrdered_{0};
+  mutable bool hostFull_{true};  // every run rebuilt at the next sync (pool renumbered)
+  // one device mirror per context (a route build sharded over devices keeps
+  // one per device); each tracks the prefixes changed since its own last sync
+  struct Mirror {
+    orh_ctx* ctx{nullptr};
+    orh_prefix_set* dev{nullptr};
+    bool full{true};
+    uint32_t namesOrdered{0}, areasOrdered{0};
+    std::vector<uint32_t> dirty;
+    std::vector<uint8_t> isDirty;
+  };
+  mutable std::vector<std::unique_ptr<Mirror>> mirrors_;
+  mutable std::mutex syncMu_;
+  // device records of pids `ids` (all pids when ids is null) from the host runs
+  void buildRecords(const std::vector<uint32_t>* ids, std::vector<uint32_t>& ptr, std::vector<orh_adv>& recs,
+                    std::vector<uint8_t>& fl) const;
 };
 
 // unordered_map<string, LinkState>; nodes are stable so LinkState can stay
@@ -360,11 +375,16 @@ class SpfSolver {
   uint32_t shardRank_{0}, shardWorld_{1};
   double lastSelectMs_{0};
   uint64_t lastSelectBytes_{0};
-  bool ownsPid(uint32_t pid, uint32_t n) const {
-    if (shardWorld_ <= 1) return true;
+  // this solver's contiguous block of the prefix ids [0, n)
+  std::pair<uint32_t, uint32_t> shardRange(uint32_t n) const {
+    if (shardWorld_ <= 1) return {0u, n};
     const uint64_t base = n / shardWorld_, rem = n % shardWorld_;
     const uint64_t lo = shardRank_ * base + std::min<uint64_t>(shardRank_, rem);
     const uint64_t hi = lo + base + (shardRank_ < rem ? 1 : 0);
+    return {static_cast<uint32_t>(lo), static_cast<uint32_t>(hi)};
+  }
+  bool ownsPid(uint32_t pid, uint32_t n) const {
+    const auto [lo, hi] = shardRange(n);
     return pid >= lo && pid < hi;
   }
 

@@ -22,6 +22,7 @@ struct SelArea {
 };
 
 struct RouteSelectArgs {
+  uint32_t pid_lo;    // prefixes [pid_lo, n_prefix)
   uint32_t n_prefix;
   const uint2* hdr;  // per prefix {pool offset, count | prefix flags << 16}
   const orh_adv* adv;
@@ -59,6 +60,7 @@ hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s);
 
 // RibPolicy over a selection (route_policy_kernel; see orh_route_policy)
 struct RoutePolicyArgs {
+  uint32_t pid_lo;  // prefixes [pid_lo, n_prefix)
   uint32_t n_prefix, words;
   const uint2* hdr;
   const orh_adv* adv;

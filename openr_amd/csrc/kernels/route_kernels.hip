@@ -42,7 +42,7 @@ __device__ inline bool key_less(int32_t pa, int32_t sa, int32_t da, int32_t pb, 
 }  // namespace
 
 __global__ __launch_bounds__(kSelBlock) void route_select_kernel(RouteSelectArgs a) {
-  const uint32_t p = blockIdx.x * kSelBlock + threadIdx.x;
+  const uint32_t p = a.pid_lo + blockIdx.x * kSelBlock + threadIdx.x;
   if (p >= a.n_prefix) return;
   const uint2 h = a.hdr[p];
   const uint32_t off = h.x, cnt = h.y & 0xFFFFu, pflags = h.y >> 16;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kSelBlock) void route_diff_kernel(RouteDiffArgs a) 
 // streams the selection records (status, best, mask: 5 + 4 W bytes per prefix)
 // plus one advertisement gather and writes one byte.
 __global__ __launch_bounds__(kSelBlock) void route_policy_kernel(RoutePolicyArgs a) {
-  const uint32_t p = blockIdx.x * kSelBlock + threadIdx.x;
+  const uint32_t p = a.pid_lo + blockIdx.x * kSelBlock + threadIdx.x;
   if (p >= a.n_prefix) return;
   uint32_t res = ORH_POL_NONE, inv = 0;
   if (a.status[p] == ORH_SEL_ROUTE) {
@@ -306,9 +306,9 @@ __global__ __launch_bounds__(kSelBlock) void route_policy_kernel(RoutePolicyArgs
 }
 
 hipError_t launch_route_policy(const RoutePolicyArgs& a, hipStream_t s) {
-  if (a.n_prefix == 0) return hipSuccess;
-  hipLaunchKernelGGL(route_policy_kernel, dim3((a.n_prefix + kSelBlock - 1) / kSelBlock), dim3(kSelBlock), 0,
-                     s, a);
+  if (a.n_prefix <= a.pid_lo) return hipSuccess;
+  hipLaunchKernelGGL(route_policy_kernel, dim3((a.n_prefix - a.pid_lo + kSelBlock - 1) / kSelBlock),
+                     dim3(kSelBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -319,8 +319,8 @@ hipError_t launch_route_diff(const RouteDiffArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_route_select(const RouteSelectArgs& a, hipStream_t s) {
-  if (a.n_prefix == 0) return hipSuccess;
-  const uint32_t grid = (a.n_prefix + kSelBlock - 1) / kSelBlock;
+  if (a.n_prefix <= a.pid_lo) return hipSuccess;
+  const uint32_t grid = (a.n_prefix - a.pid_lo + kSelBlock - 1) / kSelBlock;
   hipLaunchKernelGGL(route_select_kernel, dim3(grid), dim3(kSelBlock), 0, s, a);
   return hipGetLastError();
 }

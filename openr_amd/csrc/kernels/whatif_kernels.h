@@ -87,4 +87,9 @@ hipError_t launch_repair_back(const RepairArgs& a, uint32_t ell_k, size_t lds_li
 hipError_t launch_repair_back_split(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s,
                                     hipStream_t s3, hipEvent_t mid);
 
+// per row r < rows: the digest of (dist[r][v], nh[r][v][0..words)) over v < n
+// (row_digest_kernel), into out[r]
+hipError_t launch_row_digest(const uint32_t* dist, const uint32_t* nh, uint32_t words, uint32_t n,
+                             uint32_t rows, uint64_t* out, hipStream_t s);
+
 }  // namespace orh

@@ -479,4 +479,55 @@ hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, 
   return e != hipSuccess ? e : launch_repair_back(a, ell_k, lds_limit, s);
 }
 
+namespace {
+
+// ---- row digests (verification of whole batches) ---------------------------
+// digest(row) = sum over v of mix(v, dist[v], nh[v][0..words)) mod 2^64: an
+// order-free sum of a strong per-node hash, so equal rows give equal digests
+// however they were produced, and one digest per row checks a batch whose rows
+// do not fit the host (C4: 262,144 rows of 50,000 nodes). tests/helpers.py
+// row_digest restates it in numpy.
+__device__ inline uint64_t fmix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) row_digest_kernel(const uint32_t* __restrict__ dist,
+                                                         const uint32_t* __restrict__ nh, uint32_t words,
+                                                         uint32_t n, unsigned long long* __restrict__ out) {
+  const size_t row = blockIdx.x;
+  const uint32_t* d = dist + row * n;
+  const uint32_t* m = nh + row * static_cast<size_t>(n) * words;
+  uint64_t acc = 0;
+  for (uint32_t v = threadIdx.x; v < n; v += blockDim.x) {
+    uint64_t h = fmix64(static_cast<uint64_t>(v) * 0x9E3779B97F4A7C15ull + d[v]);
+    for (uint32_t k = 0; k < words; ++k)
+      h = fmix64(h ^ (static_cast<uint64_t>(m[static_cast<size_t>(v) * words + k]) +
+                      static_cast<uint64_t>(k) * 0xC2B2AE3D27D4EB4Full));
+    acc += h;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(acc), o));
+    const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(acc >> 32), o));
+    acc += (static_cast<uint64_t>(hi) << 32) | lo;
+  }
+  __shared__ uint64_t part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[row] = part[0] + part[1] + part[2] + part[3];
+}
+
+}  // namespace
+
+hipError_t launch_row_digest(const uint32_t* dist, const uint32_t* nh, uint32_t words, uint32_t n,
+                             uint32_t rows, uint64_t* out, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(row_digest_kernel, dim3(rows), dim3(256), 0, s, dist, nh, words, n,
+                     reinterpret_cast<unsigned long long*>(out));
+  return hipGetLastError();
+}
+
 }  // namespace orh

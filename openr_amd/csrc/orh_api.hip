@@ -665,6 +665,15 @@ int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes) {
   return ORH_OK;
 }
 
+int orh_row_digest(orh_ctx* ctx, const uint32_t* d_dist, const uint32_t* d_nh, uint32_t words, uint32_t n,
+                   uint32_t n_rows, uint64_t* d_out) {
+  if (!ctx || words == 0 || (n_rows && (!d_dist || !d_nh || !d_out))) return ORH_E_INVALID;
+  if (n_rows == 0) return ORH_OK;
+  ORH_HIP(ctx, hipSetDevice(ctx->device));
+  ORH_HIP(ctx, orh::launch_row_digest(d_dist, d_nh, words, n, n_rows, d_out, ctx->stream));
+  return ORH_OK;
+}
+
 int orh_graph_create(orh_ctx* ctx, orh_graph** out) {
   if (!ctx || !out) return ORH_E_INVALID;
   auto* g = new (std::nothrow) orh_graph();
@@ -2894,10 +2903,19 @@ int orh_prefix_info(const orh_prefix_set* ps, uint32_t* n_prefix, uint32_t* n_li
 
 int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
                      const orh_select_area* areas, const orh_select_out* out) {
+  if (!ps) return ORH_E_INVALID;
+  return orh_route_select_range(ps, me_name, flags, n_areas, areas, 0, static_cast<uint32_t>(ps->hdr.size()), out);
+}
+
+int orh_route_select_range(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint32_t n_areas,
+                           const orh_select_area* areas, uint32_t pid_lo, uint32_t pid_hi,
+                           const orh_select_out* out) {
   if (!ps || !out || (n_areas && !areas)) return ORH_E_INVALID;
   orh_ctx* ctx = ps->ctx;
-  const uint32_t n_prefix = static_cast<uint32_t>(ps->hdr.size());
-  if (n_prefix == 0) return ORH_OK;
+  if (pid_lo > pid_hi || pid_hi > ps->hdr.size())
+    return fail(ctx, ORH_E_INVALID, "orh_route_select_range: range beyond the prefix set");
+  const uint32_t n_prefix = pid_hi;
+  if (pid_lo == pid_hi) return ORH_OK;
   if (n_areas > orh::kMaxSelectAreas)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_route_select: more than 32 areas");
   if (!out->d_status || !out->d_metric || !out->d_best || (out->total_words && !out->d_mask))
@@ -2921,6 +2939,7 @@ int orh_route_select(orh_prefix_set* ps, uint32_t me_name, uint32_t flags, uint3
   ORH_HIP(ctx, hipMemcpyAsync(ps->d_areas, ps->h_areas.data(), n_areas * sizeof(orh::SelArea),
                               hipMemcpyHostToDevice, ctx->stream));
   orh::RouteSelectArgs a{};
+  a.pid_lo = pid_lo;
   a.n_prefix = n_prefix;
   a.hdr = ps->d_hdr;
   a.adv = ps->d_pool;
@@ -2980,11 +2999,17 @@ int orh_route_diff(orh_prefix_set* ps, uint32_t n_prefix, uint32_t prev_n, const
 
 int orh_route_policy(orh_prefix_set* ps, uint32_t n_prefix, const orh_select_out* sel,
                      const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated) {
+  return orh_route_policy_range(ps, 0, n_prefix, sel, pol, d_out, d_invalidated);
+}
+
+int orh_route_policy_range(orh_prefix_set* ps, uint32_t pid_lo, uint32_t n_prefix, const orh_select_out* sel,
+                           const orh_policy* pol, uint8_t* d_out, uint32_t* d_invalidated) {
   if (!ps || !sel || !pol || !d_out || !d_invalidated) return ORH_E_INVALID;
   orh_ctx* ctx = ps->ctx;
   if (pol->n_stmts > ORH_POL_MAX_STMTS)
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_route_policy: more than 32 statements");
-  if (n_prefix > ps->hdr.size()) return fail(ctx, ORH_E_INVALID, "orh_route_policy: n_prefix beyond the set");
+  if (n_prefix > ps->hdr.size() || pid_lo > n_prefix)
+    return fail(ctx, ORH_E_INVALID, "orh_route_policy: prefix range beyond the set");
   if (pol->total_words != sel->total_words)
     return fail(ctx, ORH_E_INVALID, "orh_route_policy: mask widths differ");
   if (!sel->d_status || !sel->d_best || (sel->total_words && !sel->d_mask) ||
@@ -3013,6 +3038,7 @@ int orh_route_policy(orh_prefix_set* ps, uint32_t n_prefix, const orh_select_out
   ORH_HIP(ctx, hipMemcpyAsync(ps->d_pol, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipMemsetAsync(d_invalidated, 0, sizeof(uint32_t), ctx->stream));
   orh::RoutePolicyArgs a{};
+  a.pid_lo = pid_lo;
   a.n_prefix = n_prefix;
   a.words = sel->total_words;
   a.hdr = ps->d_hdr;

@@ -85,3 +85,31 @@ def assert_digests_equal(solver_h, solver_o, me, als_h, ps_h, als_o, ps_o):
         raise AssertionError(f"{len(bad)} routes differ (first canonical index {bad[0]} "
                              f"of {h[0]} unicast + {h[1]} mpls)")
     return h[0] + h[1]
+
+
+_M1, _M2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+_G, _K = 0x9E3779B97F4A7C15, 0xC2B2AE3D27D4EB4F
+
+
+def _fmix64(z):
+    import numpy as np
+    z = z ^ (z >> np.uint64(30))
+    z = z * np.uint64(_M1)
+    z = z ^ (z >> np.uint64(27))
+    z = z * np.uint64(_M2)
+    return z ^ (z >> np.uint64(31))
+
+
+def row_digest(dist, nh):
+    """orh_row_digest (include/openr_hip.h) of one row, restated in numpy:
+    sum over v of mix(v, dist[v], nh[v][0..words)) mod 2^64. dist: [N] u32,
+    nh: [N] or [N, words] u32."""
+    import numpy as np
+    dist = np.asarray(dist, dtype=np.uint64)
+    nh = np.asarray(nh, dtype=np.uint64).reshape(len(dist), -1)
+    v = np.arange(len(dist), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = _fmix64(v * np.uint64(_G) + dist)
+        for k in range(nh.shape[1]):
+            h = _fmix64(h ^ (nh[:, k] + np.uint64(k) * np.uint64(_K)))
+        return int(np.sum(h, dtype=np.uint64))
