@@ -9,12 +9,32 @@
 #include <thread>
 
 #include "oracle_decision.h"
+#include "oracle_fast.h"
 #include "oracle_rib_policy.h"
 
 namespace py = pybind11;
 using namespace oracle;
 
 namespace {
+
+// fn(i) for i < n on `threads` threads (interleaved), the first exception rethrown
+template <class F>
+void parallelOver(size_t n, int threads, F&& fn) {
+  threads = std::max(1, std::min<int>(threads, static_cast<int>(std::max<size_t>(n, 1))));
+  std::vector<std::thread> ws;
+  std::vector<std::exception_ptr> errs(threads);
+  for (int t = 0; t < threads; ++t)
+    ws.emplace_back([&, t] {
+      try {
+        for (size_t i = t; i < n; i += threads) fn(i);
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
+    });
+  for (auto& w : ws) w.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
 
 std::string bytesOf(const py::handle& h) { return h.cast<std::string>(); }
 
@@ -615,6 +635,90 @@ PYBIND11_MODULE(openr_oracle, m) {
              for (auto v : sums) checksum += v;
              return std::make_pair(sec, checksum);
            });
+
+  // the independent fast checker (oracle_fast.h): parity at the configs'
+  // full sizes, validated against the faithful LinkState above
+  py::class_<FastChecker>(m, "FastChecker")
+      .def(py::init<const LinkState&, const std::vector<std::string>&>(), py::arg("link_state"),
+           py::arg("order"))
+      .def_property_readonly("nodes", &FastChecker::nodes)
+      .def_property_readonly("links", &FastChecker::links)
+      .def("link_index", &FastChecker::linkIndex)
+      .def("link_desc", &FastChecker::linkDesc)
+      .def("neighbours", &FastChecker::neighbours)
+      .def("spf_rows",  // dist [S][N] (u32, 0xFFFFFFFF absent) and first-hop masks [S][N][W]
+           [](const FastChecker& f, std::vector<uint32_t> srcs, std::vector<std::vector<uint32_t>> ignores,
+              int threads) {
+             if (!ignores.empty() && ignores.size() != srcs.size())
+               throw std::invalid_argument("spf_rows: one ignore list per source");
+             const size_t S = srcs.size(), N = f.nodes();
+             std::vector<FastChecker::Row> rows(S);
+             {
+               py::gil_scoped_release rel;
+               parallelOver(S, threads, [&](size_t i) {
+                 static const std::vector<uint32_t> none;
+                 f.spf(srcs[i], ignores.empty() ? none : ignores[i], rows[i]);
+               });
+             }
+             size_t W = 1;
+             for (const auto& r : rows) W = std::max<size_t>(W, r.words);
+             py::array_t<uint32_t> dist({S, N}), nh({S, N, W});
+             uint32_t* pd = dist.mutable_data();
+             uint32_t* pn = nh.mutable_data();
+             std::fill(pn, pn + S * N * W, 0u);
+             for (size_t i = 0; i < S; ++i)
+               for (size_t v = 0; v < N; ++v) {
+                 pd[i * N + v] = rows[i].dist[v] == ~0ull ? 0xFFFFFFFFu : static_cast<uint32_t>(rows[i].dist[v]);
+                 for (uint32_t k = 0; k < rows[i].words; ++k)
+                   pn[(i * N + v) * W + k] = rows[i].nh[v * rows[i].words + k];
+               }
+             return py::make_tuple(dist, nh);
+           },
+           py::arg("srcs"), py::arg("ignores") = std::vector<std::vector<uint32_t>>{}, py::arg("threads") = 8)
+      .def("row_digests",  // orh_row_digest of each runSpf(srcs[i], true, ignores[i]) row
+           [](const FastChecker& f, std::vector<uint32_t> srcs, std::vector<std::vector<uint32_t>> ignores,
+              int threads) {
+             if (!ignores.empty() && ignores.size() != srcs.size())
+               throw std::invalid_argument("row_digests: one ignore list per source");
+             py::array_t<uint64_t> out(srcs.size());
+             uint64_t* po = out.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               parallelOver(srcs.size(), threads, [&](size_t i) {
+                 static const std::vector<uint32_t> none;
+                 FastChecker::Row r;
+                 f.spf(srcs[i], ignores.empty() ? none : ignores[i], r);
+                 po[i] = FastChecker::digest(r);
+               });
+             }
+             return out;
+           },
+           py::arg("srcs"), py::arg("ignores") = std::vector<std::vector<uint32_t>>{}, py::arg("threads") = 8)
+      .def("kth_paths",  // per pair (k = 1 paths, k = 2 paths), each path a list of link descriptors
+           [](const FastChecker& f, std::vector<std::pair<uint32_t, uint32_t>> pairs, int threads) {
+             std::vector<std::vector<std::vector<uint32_t>>> k1(pairs.size()), k2(pairs.size());
+             {
+               py::gil_scoped_release rel;
+               parallelOver(pairs.size(), threads,
+                            [&](size_t i) { f.kthPaths(pairs[i].first, pairs[i].second, k1[i], k2[i]); });
+             }
+             auto conv = [&](const std::vector<std::vector<uint32_t>>& ps) {
+               py::list out;
+               for (const auto& p : ps) {
+                 py::list path;
+                 for (uint32_t l : p) {
+                   const auto& [a, ifa, b, ifb] = f.linkDesc(l);
+                   path.append(py::make_tuple(a, ifa, b, ifb));
+                 }
+                 out.append(path);
+               }
+               return out;
+             };
+             py::list out;
+             for (size_t i = 0; i < pairs.size(); ++i) out.append(py::make_tuple(conv(k1[i]), conv(k2[i])));
+             return out;
+           },
+           py::arg("pairs"), py::arg("threads") = 8);
 
   m.def("path_a_in_path_b", [](std::vector<py::tuple> a, std::vector<py::tuple> b) {
     auto mk = [](const std::vector<py::tuple>& v) {
