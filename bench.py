@@ -273,9 +273,17 @@ def main():
             ls.update_adjacency_database(db)
             return solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3
 
-        out["build_route_db_ms"] = round(median_ms(cold, 7), 3)
-        out["build_route_db_warm_ms"] = round(median_ms(
-            lambda: solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3, 7), 3)
+        st0 = cgroup_cpu_stat()
+        cold_ms = [cold() for _ in range(7)]
+        st1 = cgroup_cpu_stat()
+        warm_ms = [solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3 for _ in range(7)]
+        st2 = cgroup_cpu_stat()
+        out["build_route_db_ms"] = round(statistics.median(cold_ms), 3)
+        out["build_route_db_warm_ms"] = round(statistics.median(warm_ms), 3)
+        out["build_route_db_runs"] = {"cold_ms": spread(cold_ms), "warm_ms": spread(warm_ms),
+                                      "host_pool_threads": hip.module.host_threads(),
+                                      "cgroup_throttling": {"cold": throttle_delta(st0, st1),
+                                                            "warm": throttle_delta(st1, st2)}}
         db.adjacencies[0].metric = 1
         ls.update_adjacency_database(db)
 
@@ -330,6 +338,32 @@ def cgroup_cpu_quota():
         return None if q == "max" else max(1, int(int(q) / int(period)))
     except (OSError, ValueError):
         return None
+
+
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (None where the file is absent)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f if line.strip())}
+    except (OSError, ValueError):
+        return None
+
+
+def throttle_delta(a, b):
+    """CFS throttling between two cpu.stat snapshots: periods, throttled
+    periods and throttled time (the quota's cost to the host pool)."""
+    if not a or not b:
+        return None
+    return {"nr_periods": b.get("nr_periods", 0) - a.get("nr_periods", 0),
+            "nr_throttled": b.get("nr_throttled", 0) - a.get("nr_throttled", 0),
+            "throttled_ms": round((b.get("throttled_usec", 0) - a.get("throttled_usec", 0)) / 1e3, 3)}
+
+
+def spread(xs):
+    """median, min, max and (max - min) / median of repeated timings (ms)."""
+    m = statistics.median(xs)
+    return {"median": round(m, 3), "min": round(min(xs), 3), "max": round(max(xs), 3),
+            "spread": round((max(xs) - min(xs)) / m, 3) if m else None}
 
 
 def usable_cpus():

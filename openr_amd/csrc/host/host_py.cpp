@@ -989,6 +989,8 @@ PYBIND11_MODULE(_openr_host, m) {
       });
 
   // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
+  m.def("host_threads", [] { return WorkerPool::instance().size(); },
+        "threads of the host worker pool (the caller included)");
   // ---- thrift Compact wire -----------------------
   m.def("route_db_thrift", [](py::tuple db, const std::string& node) {  // DecisionRouteDb::toThrift
     return py::bytes(compact::routeDatabase(routeDbFromWire(db), node));

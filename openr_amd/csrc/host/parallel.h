@@ -13,8 +13,11 @@
 #include <exception>
 #include <climits>
 #include <functional>
+#include <cstdio>
+#include <cstring>
 #include <malloc.h>
 #include <mutex>
+#include <sched.h>
 #include <stdexcept>
 #include <thread>
 #include <vector>
@@ -78,9 +81,28 @@ class WorkerPool {
  private:
   WorkerPool() {
     tuneAllocator();
-    size_t t = std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+    // the caller plus workers: at most 16, and one CPU of the process's share
+    // left to the HIP runtime's threads (a cgroup quota below the affinity
+    // mask throttles a pool that fills it: profiles/r05/ cpu.stat A/B)
+    size_t t = std::min<size_t>(16, usableCpus() > 2 ? usableCpus() - 1 : usableCpus());
     if (const char* e = std::getenv("ORH_HOST_THREADS")) t = std::max(1, std::atoi(e));
     for (size_t i = 1; i < t; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  // CPUs this process may use: the affinity mask, capped by the cgroup v2
+  // quota (cpu.max "quota period")
+  static size_t usableCpus() {
+    size_t n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {};
+      long period = 0;
+      if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+        n = std::min<size_t>(n, static_cast<size_t>(std::max(1L, std::atol(q) / period)));
+      std::fclose(f);
+    }
+    return n;
   }
   // Route databases are millions of small heap objects built and freed on
   // every rebuild. glibc by default returns freed arena tops to the kernel

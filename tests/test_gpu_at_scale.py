@@ -57,7 +57,8 @@ def test_c4_ksp2_all_benched_pairs(c4):
             if got != [[LinkDesc(*l) for l in p] for p in paths]:
                 bad.append((s, d, k))
     assert not bad, f"{len(bad)} of {2 * len(kp)} path lists differ, first {bad[:3]}"
-    assert sum(len(k1) for k1, _ in want) > len(kp)  # non-trivial: most pairs have paths
+    # non-trivial: every pair has a first path and most have a second
+    assert all(k1 for k1, _ in want) and sum(1 for _, k2 in want if k2) > 0.8 * len(kp)
 
 
 def test_c4_what_if_job_vs_checker(c4):
