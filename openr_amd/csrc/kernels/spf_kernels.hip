@@ -689,234 +689,6 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
 #endif
 }
 
-// ---------------------------------------------------------------------------
-// phase 1a'': the same multi-source BFS over ONE visited array (round 5)
-// ---------------------------------------------------------------------------
-// spf_msbfs_kernel keeps two frontier arrays (this level's and the next) so a
-// level can be read and written at once. Here LDS holds one array f[u] = the
-// bits u holds so far (0 once an overloaded u has passed level 0), and a level
-// is two phases split by barriers: read (nx(v) = OR over live records v -> u
-// of f[u], & ~visited(v)), then publish (f[v] = visited(v)). Reading whole
-// visited masks instead of frontiers is exact: a bit that u already held one
-// level earlier reached every neighbour of a transit u by now, so it is in
-// visited(v) and drops out of nx(v). What it buys:
-//   - half the LDS per batch (C2: 40 KB), so three workgroups fit a CU;
-//   - a fixed array, so the ELL columns are pre-scaled to LDS byte addresses
-//     (16 bits each: (N + 1) * sizeof(M) < 64 KiB): a frontier read is one
-//     VALU extract and a ds_read, against an extract, a scale and a base add;
-//   - wave-uniform scalar tests for the rare per-node cases (overloaded
-//     owners, ELL overflow lists, levels >= 254) instead of per-lane exec
-//     juggling, and the progress flag as a wave ballot.
-// The arrival log, the level-block assembly and the outputs are those of
-// spf_msbfs_kernel (same scratch layout: ms_finalize_kernel reads either).
-template <int K, class M, int J>
-#ifndef ORH_MS1_WAVES
-#define ORH_MS1_WAVES 6
-#endif
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ORH_MS1_WAVES))) void spf_msbfs1_kernel(
-    SpfArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  constexpr uint32_t kS = MsMask<M>::kS;
-  typedef typename MsMask<M>::V V;
-  constexpr int KH = (K + 1) / 2;
-  const uint32_t N = a.n_nodes;
-  const uint32_t tid = threadIdx.x, B = blockDim.x;
-  // f spans every owned slot (J * B >= N entries, the slots past N hold a
-  // full mask nobody reads) and then the always-zero entry, so publishing
-  // needs no bounds test
-  const uint32_t NZ = J * B;
-  const uint32_t b0 = blockIdx.x * a.ms_width;
-  const uint32_t S = min(a.ms_width, a.n_rows - b0);
-  const V full = S >= 8 * sizeof(V) ? ~V(0) : (V(1) << S) - V(1);
-  __shared__ uint32_t s_prog[2];
-  M* f = reinterpret_cast<M*>(lds);
-  const char* fb = reinterpret_cast<const char*>(lds);
-  uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
-  const uint32_t lane = tid & 63u, wave = tid >> 6, waves = B >> 6;
-  uint64_t* const wlog = a.ms_log + (static_cast<size_t>(blockIdx.x) * waves + wave) * J * 64u * kS;
-  uint32_t wcnt = 0;  // events in this wave's log (wave-uniform)
-  __shared__ uint32_t s_wcnt[16];
-  const uint32_t lanebits = lane << 8;
-
-  for (uint32_t i = tid; i <= NZ; i += B) f[i] = 0;
-  if (tid < 2) s_prog[tid] = 0u;
-  __syncthreads();
-  if (tid < S) {  // sources may repeat: OR the bits in
-    const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
-    const uintptr_t byte = reinterpret_cast<uintptr_t>(f + src) + tid / 8u;
-    atomicOr(reinterpret_cast<uint32_t*>(byte & ~uintptr_t(3)), 1u << ((byte & 3u) * 8u + (tid & 7u)));
-  }
-  // ELL columns as LDS byte addresses, two per register; per owned node j
-  // (wave-uniform bits): some lane's node is overloaded / has an overflow list
-  uint32_t col[J][KH];
-  V vis[J];
-  uint32_t ovlm = 0u, ovfm = 0u;  // per lane, bit j
-  constexpr uint32_t kE = sizeof(M);
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const uint32_t v = j * B + tid;
-#pragma unroll
-    for (int h = 0; h < KH; ++h) col[j][h] = (NZ * kE) | ((NZ * kE) << 16);
-    vis[j] = full;
-    if (v < N) {
-      const uint2* slots = a.recs + static_cast<size_t>(v) * K;
-      uint2 r[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) r[k] = slots[k];
-#pragma unroll
-      for (int h = 0; h < KH; ++h)
-        col[j][h] = ms_col(r[2 * h], NZ) * kE | ((2 * h + 1 < K ? ms_col(r[2 * h + 1], NZ) : NZ) * kE << 16);
-      if (r[0].x & ORH_REC_ROW_OVL) ovlm |= 1u << j;
-      if (r[K - 1].x & ORH_REC_CONT) ovfm |= 1u << j;
-    }
-  }
-  uint32_t ovl_any = 0u, ovf_any = 0u;  // wave-uniform
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    ovl_any |= (__builtin_amdgcn_ballot_w64((ovlm >> j) & 1u) != 0u ? 1u : 0u) << j;
-    ovf_any |= (__builtin_amdgcn_ballot_w64((ovfm >> j) & 1u) != 0u ? 1u : 0u) << j;
-  }
-  ovl_any = __builtin_amdgcn_readfirstlane(ovl_any);
-  ovf_any = __builtin_amdgcn_readfirstlane(ovf_any);
-  __syncthreads();
-  // one arrival event per node that gained bits; returns the wave's ballot
-  auto log_events = [&](int j, V nx, uint32_t lvbits) -> uint64_t {
-    const uint64_t m = __builtin_amdgcn_ballot_w64(nx != 0u);
-    if (!m) return 0;
-    if (nx) {
-      const uint32_t pos = wcnt + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-      wlog[pos] = (static_cast<uint64_t>(nx) << 32) | (lanebits | lvbits | (static_cast<uint32_t>(j) << 14));
-    }
-    wcnt += static_cast<uint32_t>(__builtin_popcountll(m));
-    return m;
-  };
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const uint32_t v = j * B + tid;
-    if (v < N) vis[j] = f[v];  // level 0: the sources
-    log_events(j, v < N ? vis[j] : V(0), 0u);
-  }
-  const uint32_t w0 = a.w0;
-  char* const fw = reinterpret_cast<char*>(lds);
-  const uint32_t strideB = B * kE;
-  for (uint32_t level = 1;; ++level) {
-    uint32_t me = tid;
-    // opaque per level: the rare per-node tests stay in their scalar branches
-    // instead of being hoisted as J exec masks
-    asm volatile("" : "+v"(me), "+v"(ovlm), "+v"(ovfm));
-    const uint32_t myb = me * kE;
-    const uint32_t lvbits = min(level, kLvlDirect);
-    const bool deep = level >= kLvlDirect;  // wave-uniform
-    bool prog = false;   // wave-uniform
-    uint32_t act = 0u;   // wave-uniform: node slots j read this level
-    // phase 1: read, in groups of G owned nodes whose reads go out together
-    constexpr int G = J % ORH_MS_GROUP == 0 ? ORH_MS_GROUP : 2;
-#pragma unroll
-    for (int j0 = 0; j0 < J; j0 += G) {
-      bool open = false;
-#pragma unroll
-      for (int g = 0; g < G; ++g) open |= vis[j0 + g] != full;
-      if (!__builtin_amdgcn_ballot_w64(open)) continue;
-      act |= ((1u << G) - 1u) << j0;
-      V acc[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int h = 0; h < KH; ++h) asm volatile("" : "+v"(col[j0 + g][h]));
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        acc[g] = 0u;
-#pragma unroll
-        for (int h = 0; h < KH; ++h) {
-          acc[g] |= *reinterpret_cast<const M*>(fb + (col[j0 + g][h] & 0xFFFFu));
-          if (2 * h + 1 < K) acc[g] |= *reinterpret_cast<const M*>(fb + (col[j0 + g][h] >> 16));
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int j = j0 + g;
-        const uint32_t v = j * B + me;
-        if ((ovf_any >> j) & 1u) {  // some lane's node continues into the overflow area
-          if ((ovfm >> j) & 1u) {
-            const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
-            const uint2* ov = a.recs + (last.x & ORH_REC_COL_MASK);
-#pragma unroll 1
-            for (uint32_t q = 0; q < last.y; ++q) {
-              const uint32_t r = ov[q].x;
-              if (!(r & ORH_REC_SKIP)) acc[g] |= f[r & ORH_REC_COL_MASK];
-            }
-          }
-        }
-        const V nx = acc[g] & ~vis[j];  // 0 for every v >= N (visited = full)
-        vis[j] |= nx;
-        const uint64_t m = log_events(j, nx, lvbits);
-        prog |= m != 0u;
-        if (deep && m) {  // deep levels: the distance row directly
-          if (nx) {
-            const uint32_t vh = a.host_of[v];
-#pragma unroll 1
-            for (V q = nx; q; q &= q - 1) {
-              const uint32_t b = MsMask<M>::ctz(q);
-              dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + b])[vh] = level * w0;
-            }
-          }
-        }
-      }
-    }
-    // every level that makes progress adds >= 1 visited bit: at most S * N
-    // levels
-    if (prog && lane == 0) s_prog[level & 1u] = 1u;
-    lds_barrier();
-    if (!s_prog[level & 1u]) break;
-    if (tid == 0) s_prog[(level + 1u) & 1u] = 0u;  // read last level, after its first barrier
-    // phase 2: publish the visited masks of the slots read (no transit
-    // through an overloaded node: it publishes 0)
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      if (!((act >> j) & 1u)) continue;
-      V x = vis[j];
-      if ((ovl_any >> j) & 1u) x = ((ovlm >> j) & 1u) ? V(0) : x;
-      *reinterpret_cast<M*>(fw + myb + j * strideB) = static_cast<M>(x);
-    }
-    lds_barrier();
-  }
-  {
-    // the logs -> node-major level blocks (as spf_msbfs_kernel)
-    if (lane == 0) s_wcnt[wave] = wcnt;
-    __syncthreads();
-    constexpr uint32_t kP = kS + 4, kQ = kS / 16;
-    uint8_t* blk = reinterpret_cast<uint8_t*>(lds);
-    const uint32_t nw32 = J * 64u * kP / 4u;
-    for (uint32_t w = 0; w < waves; ++w) {
-      for (uint32_t i = tid; i < nw32; i += B) lds[i] = ~0u;
-      __syncthreads();
-      const uint32_t n_ev = s_wcnt[w];
-      const uint64_t* wl = a.ms_log + (static_cast<size_t>(blockIdx.x) * waves + w) * J * 64u * kS;
-      for (uint32_t e0 = tid; e0 < n_ev; e0 += 8u * B) {
-        uint64_t x[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) x[u] = e0 + u * B < n_ev ? wl[e0 + u * B] : 0ull;
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) {
-          uint8_t* nb = blk + ((static_cast<uint32_t>(x[u]) >> 8) & 0x7FFu) * kP;  // (j * 64 + lane) * kP
-          const uint8_t lv = static_cast<uint8_t>(x[u] & 0xFFu);
-          for (V q = static_cast<V>(x[u] >> 32); q; q &= q - 1) nb[MsMask<M>::ctz(q)] = lv;
-        }
-      }
-      __syncthreads();
-      for (uint32_t i = tid; i < J * 64u * kQ; i += B) {
-        const uint32_t node = i / kQ, q = i % kQ;  // node = j * 64 + lane
-        const uint32_t v = (node >> 6) * B + w * 64u + (node & 63u);
-        const uint32_t* src = lds + node * (kP / 4u) + q * 4u;
-        if (v < N)
-          reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS)[q] = make_uint4(src[0], src[1], src[2], src[3]);
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // node-major level bytes -> host-order u32 distance rows, one workgroup per
 // (batch, 256-node host tile); per source bit b the 256 stores of a row are
 // contiguous
@@ -2730,14 +2502,6 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
   return p;
 }
 
-static bool ms_one() {
-  static const bool on = [] {
-    const char* e = getenv("ORH_MS_ONE");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
 template <int K, class M, int J>
 static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_rows, hipStream_t s) {
   if (a.ms_width == 0 || a.ms_width > MsMask<M>::kS) return hipErrorInvalidValue;
@@ -2754,15 +2518,6 @@ static hipError_t launch_ms_j(const SpfPlan& plan, const SpfArgs& a, uint32_t n_
   const SpfArgs& b = a;
   if (a.ms_bw)
     return launch(spf_msbfs_kernel<K, M, J, true>, b, batches, plan.block, lds, s);
-  // one visited array (spf_msbfs1_kernel) when its byte addresses fit the
-  // 16-bit column slots; ORH_MS_ONE=0: the two-array kernel (A/B)
-  if constexpr (sizeof(M) <= 4) {
-    const size_t f_bytes = (static_cast<size_t>(J) * plan.block + 1) * sizeof(M);
-    if (f_bytes <= 65536 && ms_one()) {
-      const size_t lds1 = std::max<size_t>((f_bytes + 15) & ~size_t{15}, size_t{J} * 64 * (MsMask<M>::kS + 4));
-      return launch(spf_msbfs1_kernel<K, M, J>, b, batches, plan.block, lds1, s);
-    }
-  }
   return launch(spf_msbfs_kernel<K, M, J, false>, b, batches, plan.block, lds, s);
 }
 
