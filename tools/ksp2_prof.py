@@ -1,31 +1,34 @@
-"""C4 KSP2 batch broken down: plain SPFs of the sources (k = 1 rows), the
-k = 1 traces, and the k = 2 re-runs + traces (prefetch_kth_paths)."""
-import os, sys, time
+"""The benched C4 KSP2 batch (1,024 pairs, prefetchKthPaths) broken down by
+ORH_KSP_PROF (host and device time per stage, on stderr), next to the same
+batch through MultiDeviceKthPaths on one context (orh_ksp2_batch + path
+parsing, no memo): python tools/ksp2_prof.py"""
+import os
+import sys
+import time
+
+os.environ.setdefault("ORH_KSP_PROF", "1")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from openr_amd import host_backend
-from openr_amd.facade import load_topology
-from openr_amd.types import K_TESTING_AREA as A
-from openr_amd.workloads import c4_wan, c4_ksp2_pairs
+from openr_amd import host_backend  # noqa: E402
+from openr_amd.facade import load_topology  # noqa: E402
+from openr_amd.types import K_TESTING_AREA as A  # noqa: E402
+from openr_amd.workloads import C4_KSP2_PAIRS, C4_SEED, c4_ksp2_pairs, c4_wan  # noqa: E402
 
 hip = host_backend()
 adj, _ = c4_wan()
-for rep in range(2):
-    als, _ = load_topology(hip, adj, [])
-    ls = als[A]._impl
-    kp = c4_ksp2_pairs(ls.node_names(), 256)
-    t0 = time.perf_counter()
-    ls.prefetch_spf_results([a for a, _ in kp])
-    t1 = time.perf_counter()
-    for a, b in kp:
-        ls.get_kth_paths(a, b, 1)
-    t2 = time.perf_counter()
-    ls.prefetch_kth_paths(kp)
-    t3 = time.perf_counter()
-    print(f"rep {rep}: k=1 SPFs {1e3*(t1-t0):.2f} ms, k=1 traces {1e3*(t2-t1):.2f} ms, "
-          f"k=2 SPFs + traces {1e3*(t3-t2):.2f} ms, total {1e3*(t3-t0):.2f} ms", flush=True)
-
-# device time alone for the k = 1 batch (plain rows of the same sources, no host copies)
-sw = ls.what_if_sweep([a for a, _ in kp], [[] for _ in kp])
-sw.run(); sw.sync()
-sw.run(); sw.sync()
-print(f"k=1 batch device only: {sw.last_ms():.3f} ms ({len(kp)} rows)", flush=True)
+als, _ = load_topology(hip, adj, [])
+ls = als[A]._impl
+names = ls.node_names()
+kp = c4_ksp2_pairs(names, C4_KSP2_PAIRS)
+ls.prefetch_kth_paths(c4_ksp2_pairs(names, 64, seed=C4_SEED + 99))
+print("--- benched batch", flush=True)
+sys.stderr.flush()
+t0 = time.perf_counter()
+ls.prefetch_kth_paths(kp)
+print(f"prefetch_kth_paths: {1e3 * (time.perf_counter() - t0):.3f} ms wall", flush=True)
+rls = hip.module.ReplicatedLinkState(A, [0])
+for db in adj:
+    rls.update_adjacency_database(db.to_wire())
+mk = rls.kth_paths_batch(kp)
+for _ in range(3):
+    mk.run()
+    print(f"MultiDeviceKthPaths (1 context): {mk.last_ms(0):.3f} ms wall", flush=True)
