@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <tuple>
 #include <utility>
 
 namespace openr_amd {
@@ -33,6 +34,13 @@ inline size_t pairHash(const std::string& a, const std::string& b) {
 struct StrPairHash {
   size_t operator()(const std::pair<std::string, std::string>& p) const {
     return pairHash(p.first, p.second);
+  }
+};
+
+// memo keys (src, dst, k) of getKthPaths; lookup only, never iteration order
+struct KthKeyHash {
+  size_t operator()(const std::tuple<std::string, std::string, size_t>& k) const {
+    return hash128to64(pairHash(std::get<0>(k), std::get<1>(k)), std::get<2>(k));
   }
 };
 

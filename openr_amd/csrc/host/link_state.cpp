@@ -718,7 +718,9 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
   std::vector<std::pair<std::string, std::string>> host;
   std::vector<uint32_t> hs, hd;
   {
-    std::set<std::pair<std::string, std::string>> seen;
+    std::unordered_set<std::pair<std::string, std::string>, StrPairHash> seen;
+    seen.reserve(pairs.size());
+    kthPaths_.reserve(kthPaths_.size() + 2 * pairs.size());
     for (const auto& pr : pairs) {
       if (!seen.insert(pr).second) continue;
       const bool m1 = kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{1})) != 0;

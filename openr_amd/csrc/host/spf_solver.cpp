@@ -4,6 +4,7 @@
 #include "parallel.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <ctime>
@@ -1276,7 +1277,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     }
     deviceSelected_ = nDev;
     hostSelected_ = nHost;
-    auto one = [&](uint32_t pid, decltype(db.unicastRoutes)& out) {
+    using RouteMap = decltype(db.unicastRoutes);
+    auto one = [&](uint32_t pid, RouteMap::Shard& out) {
       if (!ps.prefixLive(pid)) return;
       if (selStatus_[pid] == ORH_SEL_ROUTE) {
         RibUnicastEntry e = materialize(pid, ps);
@@ -1334,15 +1336,22 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         }
         cand[i] = std::move(entry);
       };
-      std::vector<decltype(db.unicastRoutes)> parts(pool.size());
-      pool.parallelFor(nOwn + dbs.size(), [&](size_t w, size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) {
-          if (i < nOwn) one(pidLo + static_cast<uint32_t>(i), parts[w]);
-          else label(i - nOwn);
-        }
-      });
-      prof.mark("unicast + labels (pool)");
-      mergeParts(db.unicastRoutes, parts, pool);
+      {
+        std::vector<RouteMap> parts(pool.size());
+        pool.parallelFor(nOwn + dbs.size(), [&](size_t w, size_t b, size_t e) {
+          for (size_t i = b; i < e; ++i) {
+            if (i < nOwn) {
+              const uint32_t pid = pidLo + static_cast<uint32_t>(i);
+              if (ps.prefixLive(pid)) one(pid, parts[w].shard(RouteMap::shardOf(ps.prefixOf(pid))));
+            } else {
+              label(i - nOwn);
+            }
+          }
+        });
+        prof.mark("unicast + labels (pool)");
+        mergeParts(db.unicastRoutes, parts, pool);
+        prof.mark("unicast merge");
+      }
       for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
         if (db.unicastRoutes.count(prefix) || !ownsStatic(prefix)) continue;
         RibUnicastEntry se;
@@ -1351,21 +1360,21 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         hostPolicy(se);
         db.unicastRoutes.emplace(prefix, std::move(se));
       }
-      prof.mark("unicast merge");
+      prof.mark("unicast statics");
       // duplicate labels: the smaller node name wins among the nodes with a
       // route (:675-688); labels are resolved shard by shard on the pool
       if (!dbs.empty()) {
-        std::vector<std::vector<uint32_t>> byShard(MplsRouteMap::kShards);
+        std::vector<std::vector<uint32_t>> byLabelShard(MplsRouteMap::kShards);
         for (size_t i = 0; i < dbs.size(); ++i) {
           const int32_t lbl = dbs[i]->nodeLabel;
           if (lbl == 0 || !isMplsLabelValid(lbl) || !cand[i]) continue;
-          byShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
+          byLabelShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
         }
         pool.parallelFor(MplsRouteMap::kShards, [&](size_t, size_t b, size_t e) {
           for (size_t sh = b; sh < e; ++sh) {
             std::unordered_map<int32_t, uint32_t> win;
-            win.reserve(byShard[sh].size());
-            for (uint32_t i : byShard[sh]) {
+            win.reserve(byLabelShard[sh].size());
+            for (uint32_t i : byLabelShard[sh]) {
               auto [it, fresh] = win.emplace(dbs[i]->nodeLabel, i);
               if (!fresh && dbs[i]->thisNodeName < dbs[it->second]->thisNodeName) it->second = i;
             }
@@ -1378,14 +1387,22 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       }
       labelsDone = true;
     } else if (!hasKsp && nOwn >= kParallelMin && pool.size() > 1) {
-      std::vector<decltype(db.unicastRoutes)> parts(pool.size());
+      // contiguous pid ranges per worker into per-worker maps, then spliced
+      std::vector<RouteMap> parts(pool.size());
       pool.parallelFor(nOwn, [&](size_t w, size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) one(pidLo + static_cast<uint32_t>(i), parts[w]);
+        for (size_t i = b; i < e; ++i) {
+          const uint32_t pid = pidLo + static_cast<uint32_t>(i);
+          if (ps.prefixLive(pid)) one(pid, parts[w].shard(RouteMap::shardOf(ps.prefixOf(pid))));
+        }
       });
       prof.mark("unicast (pool)");
       mergeParts(db.unicastRoutes, parts, pool);
+      prof.mark("unicast merge");
     } else {
-      for (uint32_t pid = pidLo; pid < pidHi; ++pid) one(pid, db.unicastRoutes);
+      for (uint32_t pid = pidLo; pid < pidHi; ++pid) {
+        if (!ps.prefixLive(pid)) continue;
+        one(pid, db.unicastRoutes.shard(RouteMap::shardOf(ps.prefixOf(pid))));
+      }
     }
   } else if (!mplsOnly) {
     keys.reserve(ps.prefixes().size());

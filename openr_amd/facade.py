@@ -248,6 +248,9 @@ def load_topology(backend: Backend, adj_dbs, prefixes, als=None, ps=None, lane: 
         ps = backend.prefix_state()
     for db in adj_dbs:
         als[db.area].update_adjacency_database(db)
-    for node, area, entry in prefixes:
-        ps.update_prefix(node, area, entry)
+    # PrefixState::updatePrefix for every advertisement, in order, a chunk per
+    # call (no changed-prefix set is built for the caller)
+    chunk = 1 << 16
+    for i in range(0, len(prefixes), chunk):
+        ps._impl.update_prefixes([(node, area, entry.to_wire()) for node, area, entry in prefixes[i:i + chunk]])
     return als, ps

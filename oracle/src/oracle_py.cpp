@@ -767,6 +767,16 @@ PYBIND11_MODULE(openr_oracle, m) {
                out.append(py::make_tuple(py::bytes(c.first), c.second));
              return out;
            })
+      .def("update_prefixes",  // [(node, area, entry)]: update_prefix in order, one call
+           [](PrefixState& s, py::list items) {
+             size_t n = 0;
+             for (auto it : items) {
+               auto t = it.cast<py::tuple>();
+               n += s.updatePrefix(t[0].cast<std::string>(), t[1].cast<std::string>(),
+                                   entryFromWire(t[2].cast<py::tuple>())).size();
+             }
+             return n;
+           })
       .def("delete_prefix",
            [](PrefixState& s, const std::string& node, const std::string& area, py::bytes addr,
               int32_t len) {

@@ -15,12 +15,16 @@ from openr_amd.workloads import C5_AREAS, C5_TAG, c5_multi_area  # noqa: E402
 
 hip = host_backend()
 areas, pfx = c5_multi_area()
+t0 = time.perf_counter()
 als, ps = load_topology(hip, [db for a in C5_AREAS for db in areas[a]], pfx)
+print(f"load {time.perf_counter() - t0:.3f} s", flush=True)
 solver = hip.spf_solver("me", True, enable_best_route_selection=True)
 policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
     0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
 rib = hip.module.DecisionRib()
 os.environ["ORH_ROUTE_PROF"] = "1"
+for rep in range(3):  # buildRouteDb alone (the leg's build_route_db_ms)
+    print("build", rep, solver._impl.time_build_route_db("me", als._impl, ps._impl), flush=True)
 print("first", rib.rebuild_routes(solver._impl, "me", als._impl, ps._impl, True, [], policy._impl, wire=False),
       flush=True)
 rng = random.Random(55)
