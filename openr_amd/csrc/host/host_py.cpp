@@ -1192,6 +1192,8 @@ PYBIND11_MODULE(_openr_host, m) {
              }
              return n;
            })
+      .def("set_tag_set_id_limit", &PrefixState::setTagSetIdLimit)
+      .def_property_readonly("num_tag_sets", &PrefixState::numTagSets)
       .def("delete_prefix",
            [](PrefixState& s, const std::string& node, const std::string& area, py::bytes addr,
               int32_t len) {

@@ -53,9 +53,14 @@ uint32_t PrefixState::internTagSet(const std::set<std::string>& tags) {
   auto [it, inserted] = tagSetIds_.emplace(tags, 0u);
   if (inserted) {
     tagSets_.push_back(&it->first);
-    it->second = static_cast<uint32_t>(std::min<size_t>(tagSets_.size(), ORH_ADV_TAGSET_OVF));
+    it->second = tagSets_.size() < tagIdLimit_ ? static_cast<uint32_t>(tagSets_.size()) : ORH_ADV_TAGSET_OVF;
   }
   return it->second;
+}
+
+void PrefixState::setTagSetIdLimit(uint32_t limit) {
+  if (!tagSets_.empty()) throw std::logic_error("setTagSetIdLimit: tag sets already interned");
+  tagIdLimit_ = std::clamp<uint32_t>(limit, 1u, ORH_ADV_TAGSET_OVF);
 }
 
 uint32_t PrefixState::tagSetId(const std::set<std::string>& tags) const {

@@ -15,6 +15,7 @@
 #include <list>
 #include <stdexcept>
 #include <tuple>
+#include <unordered_set>
 
 namespace openr_amd {
 
@@ -1108,7 +1109,7 @@ bool SpfSolver::policyOnDevice(const PrefixState& ps, RibPolicy& policy) {
     if (!st[s].prefixSet().empty()) pol.stmt_prefixes |= 1u << s;
   }
   // tag set id -> statements whose tag matcher it meets (id 0: no tags)
-  const uint32_t nts = std::min<uint32_t>(ps.numTagSets(), ORH_ADV_TAGSET_OVF - 1) + 1;
+  const uint32_t nts = std::min<uint32_t>(ps.numTagSets(), ps.tagSetIdLimit() - 1) + 1;
   std::vector<uint32_t> tagStmts(nts, 0u);
   if (pol.stmt_tags) {
     for (uint32_t t = 1; t < nts; ++t)
@@ -1639,6 +1640,10 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
   // the policy decided on the device for the materialised routes (as in
   // buildRouteDbWithPolicy); host-path and static routes take applyAction
   const bool devPolicy = applyPolicy && policyOnDevice(ps, *policy);
+  // the full rebuild counts the policy's invalidated routes over the whole
+  // DB (RibPolicy.cpp:149-150 via Decision.cpp:1895); without the device's
+  // count of every selected route the delta cannot, so the caller rebuilds
+  if (applyPolicy && !devPolicy) return std::nullopt;
   if (devPolicy) prof.mark("policy (device)");
   auto staticRoute = [&](const Cidr& p) -> std::optional<RibUnicastEntry> {
     auto it = staticUnicastRoutes_.find(p);
@@ -1757,7 +1762,29 @@ std::optional<DecisionRouteUpdate> SpfSolver::buildRouteDelta(const std::string&
   }
   // the device counted every selected route, as the reference's full rebuild
   // counts every route it applies the policy to (RibPolicy.cpp:149-150)
-  if (devPolicy) invalidated += devPol_.deviceInvalidated + devPol_.hostInvalidated;
+  if (devPolicy) {
+    // routes whose tag set has no device id (ORH_POL_HOST) take applyAction as
+    // they materialise: the ones not rebuilt above are materialised to count
+    pool.parallelFor(n, [&](size_t, size_t b, size_t e) {
+      for (size_t pid = b; pid < e; ++pid)
+        if (!want[pid] && selStatus_[pid] == ORH_SEL_ROUTE && devPol_.stmt[pid] == ORH_POL_HOST &&
+            ps.prefixLive(static_cast<uint32_t>(pid)))
+          (void)materialize(static_cast<uint32_t>(pid), ps);
+    });
+    invalidated += devPol_.deviceInvalidated + devPol_.hostInvalidated;
+    // and every static route the full DB holds that no item above rebuilt:
+    // its prefix has no live id, or a live id with no route, and was not
+    // withdrawn since psStamp (buildRouteDbImpl applies the policy to each)
+    std::unordered_set<Cidr, CidrHash> gone;
+    if (!staticUnicastRoutes_.empty()) gone.insert(deleted.begin(), deleted.end());
+    for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
+      const auto pid = ps.pidOf(prefix);
+      const bool live = pid && ps.prefixLive(*pid);
+      if (live ? (want[*pid] || selStatus_[*pid] != ORH_SEL_NONE) : gone.count(prefix) != 0) continue;
+      auto r = staticRoute(prefix);
+      policy->applyAction(*r, &invalidated);
+    }
+  }
   if (policy) policy->addInvalidated(invalidated);
   devPol_.on = false;
   // MPLS routes: unchanged inputs (no topology or static change since the

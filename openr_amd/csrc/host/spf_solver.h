@@ -96,6 +96,11 @@ class PrefixState {
   uint32_t tagSetId(const std::set<std::string>& tags) const;
   uint32_t numTagSets() const { return static_cast<uint32_t>(tagSets_.size()); }
   const std::set<std::string>& tagSet(uint32_t id) const { return *tagSets_[id - 1]; }
+  // tag sets from the limit-th on share ORH_ADV_TAGSET_OVF (their routes take
+  // RibPolicy on the host: ORH_POL_HOST); tests lower the limit to reach that
+  // path, before the first tagged advertisement
+  uint32_t tagSetIdLimit() const { return tagIdLimit_; }
+  void setTagSetIdLimit(uint32_t limit);
 
  private:
   void touch(const Cidr& prefix, bool erased);
@@ -123,6 +128,7 @@ class PrefixState {
   std::vector<std::string> names_, areas_;
   std::map<std::set<std::string>, uint32_t> tagSetIds_;
   std::vector<const std::set<std::string>*> tagSets_;  // id - 1 -> set (map nodes are stable)
+  uint32_t tagIdLimit_{ORH_ADV_TAGSET_OVF};
 
   mutable std::vector<AdvRef> advPool_;
   mutable std::vector<std::pair<uint32_t, uint32_t>> run_;  // pid -> (offset, count)

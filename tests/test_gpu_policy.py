@@ -16,6 +16,8 @@ included, plus the invalidated-routes counters.
   the same topology with mixed tag sets, prefix matchers, neighbour weights,
   zero weights (dropped nexthops, invalidated routes), an inert statement,
   SR_MPLS prefixes (host path) and a static route    full canonical DBs
+  tag sets past the device's ids (ORH_POL_HOST), and 33 statements (host
+  applyPolicy)                                       full canonical DBs
   C5 at 1M prefixes with the UCMP statement         whole-DB digests
   DecisionRib full rebuilds (whole and delta) with the policy vs the oracle
 """
@@ -45,8 +47,11 @@ def _ucmp():
                                RibRouteActionWeight(0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))]
 
 
-def _build_both(hip, oracle, adj, pfx, stmts, me="me", best_route=True, static=None):
-    als_h, ps_h = load_topology(hip, adj, pfx)
+def _build_both(hip, oracle, adj, pfx, stmts, me="me", best_route=True, static=None, tag_id_limit=None):
+    ps_h = hip.prefix_state()
+    if tag_id_limit is not None:
+        ps_h._impl.set_tag_set_id_limit(tag_id_limit)
+    als_h, ps_h = load_topology(hip, adj, pfx, ps=ps_h)
     als_o, ps_o = load_topology(oracle, adj, pfx)
     sh = hip.spf_solver(me, True, enable_best_route_selection=best_route)
     so = oracle.spf_solver(me, True, enable_best_route_selection=best_route)
@@ -57,12 +62,16 @@ def _build_both(hip, oracle, adj, pfx, stmts, me="me", best_route=True, static=N
     po = oracle.rib_policy(stmts, 3600)
     h = sh.build_route_db_with_policy(me, als_h, ps_h, ph)
     o = so.build_route_db_with_policy(me, als_o, ps_o, po)
-    return h, o, ph, po
+    # the same build once more, for the policy statistics (routes decided on
+    # the device; the counters of a separate policy object)
+    stats = sh._impl.time_build_route_db_with_policy(me, als_h._impl, ps_h._impl,
+                                                     hip.rib_policy(stmts, 3600)._impl)
+    return h, o, ph, po, stats
 
 
 @pytest.mark.parametrize("best_route", [False, True])
 def test_c5_ucmp_policy_small(hip, oracle, best_route):
-    h, o, ph, po = _build_both(hip, oracle, *_c5(3000), _ucmp(), best_route=best_route)
+    h, o, ph, po, _ = _build_both(hip, oracle, *_c5(3000), _ucmp(), best_route=best_route)
     assert h is not None and o is not None
     assert h.canonical_full() == o.canonical_full()
     assert ph.invalidated_routes == po.invalidated_routes
@@ -103,20 +112,61 @@ def _mixed_statements(prefixes, seed):
 
 
 @pytest.mark.parametrize("seed", [1, 2])
+def _static(i):
+    """A static route for a prefix no node advertises, via B0."""
+    sp = IpPrefix(BinaryAddress(bytes([0xfc, 0x99, 0, i] + [0] * 12)), 64)
+    snh = NextHopThrift(BinaryAddress(bytes([0xfe, 0x80] + [0] * 13 + [7]), "static0"), 0, None, 0, "B",
+                        "B0")
+    return sp, snh
+
+
+def _fillers(k):
+    """k statements whose prefix matchers name prefixes nobody advertises."""
+    return [RibPolicyStatement(f"f{i}", [IpPrefix(BinaryAddress(bytes([0xfd, 0x77, i] + [0] * 13)), 48)],
+                               None, RibRouteActionWeight(1, {}, {})) for i in range(k)]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
 def test_c5_mixed_policy_small(hip, oracle, seed):
     adj, pfx = _c5(3000, _mixed_retag(seed))
     stmts = _mixed_statements(pfx, seed)
-    # a static route (host policy path) for a prefix no node advertises
-    sp = IpPrefix(BinaryAddress(bytes([0xfc, 0x99] + [0] * 14)), 64)
-    snh = NextHopThrift(BinaryAddress(bytes([0xfe, 0x80] + [0] * 13 + [7]), "static0"), 0, None, 0, "B",
-                        "B0")
-    h, o, ph, po = _build_both(hip, oracle, adj, pfx, stmts + [RibPolicyStatement(
+    # a static route (host policy path)
+    sp, snh = _static(0)
+    h, o, ph, po, stats = _build_both(hip, oracle, adj, pfx, stmts + [RibPolicyStatement(
         "static", [sp], None, RibRouteActionWeight(6, {}, {}))], static=[(sp, [snh])])
     assert h.canonical_full() == o.canonical_full()
     assert ph.invalidated_routes == po.invalidated_routes > 0
     assert h.unicastRoutes[sp].nextHops[0].weight == 6
     weights = {nh.weight for r in h.unicastRoutes.values() for nh in r.nextHops}
     assert {0, 1, 2, 3, 4, 5, 9}.issubset(weights)
+    assert stats[4] > 0.8 * stats[1]  # most routes decided on the device
+
+
+def test_c5_policy_tag_ids_saturated(hip, oracle):
+    """Tag sets beyond the device's id space (ORH_ADV_TAGSET_OVF; the limit is
+    lowered so 2 of the 5 sets get ids): their routes come back ORH_POL_HOST
+    from route_policy_kernel and take RibPolicy::applyAction on the host as
+    they materialise - the result and the counters are the reference's."""
+    adj, pfx = _c5(3000, _mixed_retag(3))
+    stmts = _mixed_statements(pfx, 3)
+    h, o, ph, po, stats = _build_both(hip, oracle, adj, pfx, stmts, tag_id_limit=3)
+    assert h.canonical_full() == o.canonical_full()
+    assert ph.invalidated_routes == po.invalidated_routes > 0
+    _, routes, updated, invalidated, on_device, _ = stats
+    assert invalidated == po.invalidated_routes
+    assert 0 < on_device < 0.7 * routes  # tagged routes of 3 sets went to the host
+
+
+def test_c5_policy_33_statements(hip, oracle):
+    """More statements than the device's masks hold (ORH_POL_MAX_STMTS = 32):
+    RibPolicy::applyPolicy over the built database on the host."""
+    adj, pfx = _c5(3000, _mixed_retag(4))
+    stmts = _fillers(28) + _mixed_statements(pfx, 4)
+    assert len(stmts) == 33
+    h, o, ph, po, stats = _build_both(hip, oracle, adj, pfx, stmts)
+    assert h.canonical_full() == o.canonical_full()
+    assert ph.invalidated_routes == po.invalidated_routes > 0
+    assert stats[4] == 0 and stats[3] == po.invalidated_routes
 
 
 def test_c5_ucmp_policy_1m_digest(hip, oracle):
@@ -142,26 +192,46 @@ def test_c5_ucmp_policy_1m_digest(hip, oracle):
     assert updated == dh[0]
 
 
-def test_decision_rib_rebuild_with_policy(hip, oracle):
+@pytest.mark.parametrize("variant", ["device", "tag_ids_saturated", "33_statements"])
+def test_decision_rib_rebuild_with_policy(hip, oracle, variant):
     """DecisionRib full rebuilds with the policy (the first whole, the later
     ones as deltas against routeDb_) equal the oracle's buildRouteDb +
-    applyPolicy after the same prefix and metric changes."""
+    applyPolicy after the same prefix and metric changes, and the policy's
+    invalidated-routes counter accumulates what the reference's full rebuilds
+    count (RibPolicy.cpp:149-150): the device's count of the selected routes,
+    host-path routes, and static routes the delta did not rebuild - one
+    invalidated (every nexthop weighted 0), one shadowed by an advertisement.
+    With tag sets past the device's ids (ORH_POL_HOST) the delta materialises
+    those routes to count them; with 33 statements every rebuild is whole."""
+    from openr_amd.types import RouteDb
     adj, pfx = _c5(3000, _mixed_retag(5))
-    stmts = _mixed_statements(pfx, 5)
-    als_h, ps_h = load_topology(hip, adj, pfx)
+    sp, snh = _static(1)
+    shadow = pfx[7][2].prefix
+    stmts = [RibPolicyStatement("static0", [sp, shadow], None, RibRouteActionWeight(0, {}, {}))]
+    stmts += _mixed_statements(pfx, 5) + (_fillers(27) if variant == "33_statements" else [])
+    ps_h = hip.prefix_state()
+    if variant == "tag_ids_saturated":
+        ps_h._impl.set_tag_set_id_limit(3)
+    als_h, ps_h = load_topology(hip, adj, pfx, ps=ps_h)
     als_o, ps_o = load_topology(oracle, adj, pfx)
     sh = hip.spf_solver("me", True, enable_best_route_selection=True)
     so = oracle.spf_solver("me", True, enable_best_route_selection=True)
+    statics = [(sp, [snh]), (shadow, [snh])]
+    sh.update_static_unicast_routes(statics)
+    so.update_static_unicast_routes(statics)
     ph = hip.rib_policy(stmts, 3600)
     rib = hip.module.DecisionRib()
     rng = random.Random(9)
+    want_inv = 0
     for rnd in range(3):
         rib.rebuild_routes(sh._impl, "me", als_h._impl, ps_h._impl, True, [], ph._impl, wire=False)
         po = oracle.rib_policy(stmts, 3600)
         want = so.build_route_db_with_policy("me", als_o, ps_o, po)
-        from openr_amd.types import RouteDb
+        want_inv += po.invalidated_routes
         got = RouteDb.from_wire(rib.route_db())
         assert got.canonical_full() == want.canonical_full(), rnd
+        assert sp in got.unicastRoutes
+        assert ph.invalidated_routes == want_inv, rnd
         # prefix re-advertisements with new metrics and one adjacency metric change
         for _ in range(200):
             node, area, e = pfx[rng.randrange(len(pfx))]
@@ -176,4 +246,8 @@ def test_decision_rib_rebuild_with_policy(hip, oracle):
             db.adjacencies[0].metric = rng.randint(1, 3)
             als_h[db.area].update_adjacency_database(db)
             als_o[db.area].update_adjacency_database(db)
-    assert rib.delta_rebuilds >= 1
+    assert want_inv >= 3
+    if variant == "33_statements":
+        assert rib.delta_rebuilds == 0
+    else:
+        assert rib.delta_rebuilds >= 1
