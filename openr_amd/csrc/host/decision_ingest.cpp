@@ -2,6 +2,10 @@
 // decision_ingest.h.
 #include "decision_ingest.h"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <arpa/inet.h>
 
 #include <algorithm>
@@ -268,11 +272,23 @@ DecisionRouteUpdate DecisionRib::rebuildRoutes(SpfSolver& solver, const std::str
       routeDb_.update(update);
     } else {
       // buildRouteDb + RibPolicy::applyPolicy (the policy decided on the device)
+      static const bool prof = std::getenv("ORH_ROUTE_PROF") != nullptr;
+      auto t0 = std::chrono::steady_clock::now();
+      auto lap = [&](const char* what) {
+        if (!prof) return;
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "route-prof rib %-20s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count());
+        t0 = t1;
+      };
       DecisionRouteDb db = solver.buildRouteDbWithPolicy(me, als, ps, policy).value_or(DecisionRouteDb{});
+      lap("build + policy");
       update = routeDb_.calculateUpdate(db);
+      lap("calculateUpdate");
       // routeDb_.update(update) leaves routeDb_ equal to db: take db itself
       // (no second copy of every changed route; the old maps free in parallel)
       routeDb_ = std::move(db);
+      lap("routeDb_ replaced");
       ++wholeRebuilds_;
     }
   } else {

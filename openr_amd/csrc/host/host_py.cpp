@@ -3,6 +3,7 @@
 // oracle so that openr_amd.facade can drive either one.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <limits>
 #include <pybind11/stl.h>
 
 #include <algorithm>
@@ -84,6 +85,85 @@ PrefixEntry entryFromWire(const py::tuple& t) {
   return e;
 }
 
+// entryFromWire over the CPython API for the bulk load (pybind's accessors
+// and casts were most of its per-entry cost); false for what it does not
+// take (metric vectors, out-of-range or unexpected values): entryFromWire then
+bool strFast(PyObject* o, std::string& out) {
+  const char* p;
+  Py_ssize_t n;
+  if (PyUnicode_Check(o)) {
+    p = PyUnicode_AsUTF8AndSize(o, &n);
+    if (!p) {
+      PyErr_Clear();
+      return false;
+    }
+  } else if (PyBytes_Check(o)) {
+    p = PyBytes_AS_STRING(o);
+    n = PyBytes_GET_SIZE(o);
+  } else {
+    return false;
+  }
+  out.assign(p, static_cast<size_t>(n));
+  return true;
+}
+
+template <class T>
+bool intFast(PyObject* o, T& out) {
+  if (!PyLong_Check(o)) return false;
+  int overflow = 0;
+  const long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
+  if (overflow || (v == -1 && PyErr_Occurred()) || v < std::numeric_limits<T>::min() ||
+      v > std::numeric_limits<T>::max()) {
+    PyErr_Clear();
+    return false;
+  }
+  out = static_cast<T>(v);
+  return true;
+}
+
+bool entryFromWireFast(PyObject* t, PrefixEntry& e) {
+  if (!PyTuple_Check(t) || PyTuple_GET_SIZE(t) < 10) return false;
+  auto at = [t](Py_ssize_t i) { return PyTuple_GET_ITEM(t, i); };
+  PyObject* a = at(0);
+  if (!PyBytes_Check(a) || PyBytes_GET_SIZE(a) > static_cast<Py_ssize_t>(AddrBytes::kMax)) return false;
+  e.addr.assign(PyBytes_AS_STRING(a), static_cast<size_t>(PyBytes_GET_SIZE(a)));
+  if (!intFast(at(1), e.len) || !intFast(at(2), e.type) || !intFast(at(3), e.forwardingType) ||
+      !intFast(at(4), e.forwardingAlgorithm))
+    return false;
+  if (at(5) != Py_None) {
+    int64_t v;
+    if (!intFast(at(5), v)) return false;
+    e.minNexthop = v;
+  }
+  if (at(6) != Py_None) {
+    int32_t v;
+    if (!intFast(at(6), v)) return false;
+    e.prependLabel = v;
+  }
+  PyObject* m = at(7);
+  if (!PyTuple_Check(m) || PyTuple_GET_SIZE(m) < 3 || !intFast(PyTuple_GET_ITEM(m, 0), e.pathPreference) ||
+      !intFast(PyTuple_GET_ITEM(m, 1), e.sourcePreference) || !intFast(PyTuple_GET_ITEM(m, 2), e.distance))
+    return false;
+  if (at(8) != Py_None) return false;  // metric vector: the pybind path
+  if (at(9) != Py_None) {
+    std::string d;
+    if (!strFast(at(9), d)) return false;
+    e.data = std::move(d);
+  }
+  if (PyTuple_GET_SIZE(t) > 10 && at(10) != Py_None) {
+    PyObject* tags = at(10);
+    if (!PyTuple_Check(tags) && !PyList_Check(tags)) return false;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(tags);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      std::string tag;
+      if (!PyUnicode_Check(PySequence_Fast_GET_ITEM(tags, i)) || !strFast(PySequence_Fast_GET_ITEM(tags, i), tag))
+        return false;
+      e.tags.insert(std::move(tag));
+    }
+  }
+  return true;
+}
+
 py::object entryToWire(const PrefixEntry& e) {
   py::object mv = py::none();
   if (e.mv) {
@@ -136,6 +216,7 @@ py::list nhsToWire(const NextHopSet& s) {
   for (const auto& nh : s) l.append(nhToWire(nh));
   return l;
 }
+py::list nhsToWire(const NextHops& s) { return nhsToWire(s.set()); }
 
 py::tuple unicastToWire(const RibUnicastEntry& e) {
   return py::make_tuple(pyBytes(e.prefix.first), e.prefix.second, nhsToWire(e.nexthops),
@@ -462,6 +543,7 @@ void writeNexthops(DigestWriter& w, const NextHopSet& nhs) {
   w.i32(static_cast<int32_t>(v.size()));
   for (const auto& x : v) w.str(x);
 }
+void writeNexthops(DigestWriter& w, const NextHops& nhs) { writeNexthops(w, nhs.set()); }
 
 void writeEntry(DigestWriter& w, const PrefixEntry& e) {
   w.str(e.addr.str());
@@ -1183,12 +1265,22 @@ PYBIND11_MODULE(_openr_host, m) {
                out.append(py::make_tuple(pyBytes(c.first), c.second));
              return out;
            })
-      .def("update_prefixes",
+      .def("update_prefixes",  // [(node, area, entry wire)]: changed prefixes counted
            [](PrefixState& s, py::list items) {
+             s.reserve(items.size());
              size_t n = 0;
+             std::string node, area;
              for (auto it : items) {
-               auto t = it.cast<py::tuple>();
-               n += s.updatePrefix(str(t[0]), str(t[1]), entryFromWire(t[2].cast<py::tuple>())).size();
+               PyObject* t = it.ptr();
+               PrefixEntry e;
+               if (!(PyTuple_Check(t) && PyTuple_GET_SIZE(t) == 3 && strFast(PyTuple_GET_ITEM(t, 0), node) &&
+                     strFast(PyTuple_GET_ITEM(t, 1), area) && entryFromWireFast(PyTuple_GET_ITEM(t, 2), e))) {
+                 auto tt = it.cast<py::tuple>();
+                 node = str(tt[0]);
+                 area = str(tt[1]);
+                 e = entryFromWire(tt[2].cast<py::tuple>());
+               }
+               n += s.upsertPrefix(node, area, std::move(e));
              }
              return n;
            })

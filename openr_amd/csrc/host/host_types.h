@@ -12,8 +12,11 @@
 #include <array>
 #include <atomic>
 #include <cstdint>
+#include <initializer_list>
 #include <iterator>
+#include <memory>
 #include <type_traits>
+#include <cstdlib>
 #include <cstring>
 #include <optional>
 #include <set>
@@ -204,6 +207,73 @@ struct NextHopHash {
 };
 
 using NextHopSet = std::unordered_set<NextHopThrift, NextHopHash>;
+
+// A route's nexthop set (RibEntry.h's std::unordered_set<NextHopThrift>) with
+// value semantics over one shared, immutable NextHopSet: a copy shares the
+// set (a reference count), a mutation of a shared set copies it first. The
+// routes of a build mostly carry a few dozen distinct sets (C5: 1M routes),
+// so a route takes a count, not a set of nodes, and so does every copy the
+// Decision path makes (calculateUpdate, routeDb_ updates, the RIB's delta).
+// Iteration is the shared set's, i.e. the reference's insertion order.
+class NextHops {
+ public:
+  using value_type = NextHopThrift;
+  using const_iterator = NextHopSet::const_iterator;
+  using iterator = const_iterator;
+  NextHops() = default;
+  NextHops(NextHopSet s)  // NOLINT: a built set becomes a route's
+      : p_(s.empty() ? nullptr : std::make_shared<NextHopSet>(std::move(s))) {}
+  NextHops(std::initializer_list<NextHopThrift> l) : NextHops(NextHopSet(l)) {}
+  const_iterator begin() const { return set().begin(); }
+  const_iterator end() const { return set().end(); }
+  size_t size() const { return p_ ? p_->size() : 0; }
+  bool empty() const { return size() == 0; }
+  size_t count(const NextHopThrift& nh) const { return p_ ? p_->count(nh) : 0; }
+  const NextHopSet& set() const { return p_ ? *p_ : kEmpty(); }
+  template <class... A>
+  std::pair<const_iterator, bool> insert(A&&... a) {
+    auto r = mut().insert(std::forward<A>(a)...);
+    return {r.first, r.second};
+  }
+  template <class It>
+  void insert(It b, It e) {
+    mut().insert(b, e);
+  }
+  template <class... A>
+  std::pair<const_iterator, bool> emplace(A&&... a) {
+    auto r = mut().emplace(std::forward<A>(a)...);
+    return {r.first, r.second};
+  }
+  void clear() { p_.reset(); }
+  // the set for building in place (copied first when shared)
+  NextHopSet& edit() { return mut(); }
+  // the set itself, for rebuilding it (moved out when this route holds the
+  // only reference, else copied); this route is left empty
+  NextHopSet take() {
+    NextHopSet out = !p_ ? NextHopSet{} : p_.use_count() == 1 ? std::move(*p_) : NextHopSet(*p_);
+    p_.reset();
+    return out;
+  }
+  bool sameSet(const NextHops& o) const { return p_ == o.p_; }
+  const void* id() const { return p_.get(); }  // the shared set (null: empty)
+  bool operator==(const NextHops& o) const { return p_ == o.p_ || set() == o.set(); }
+  bool operator!=(const NextHops& o) const { return !(*this == o); }
+
+ private:
+  NextHopSet& mut() {
+    if (!p_)
+      p_ = std::make_shared<NextHopSet>();
+    else if (p_.use_count() > 1)
+      p_ = std::make_shared<NextHopSet>(*p_);
+    return *p_;
+  }
+  static const NextHopSet& kEmpty() {
+    static const NextHopSet e;
+    return e;
+  }
+  std::shared_ptr<NextHopSet> p_;  // never mutated while shared
+};
+
 using Cidr = std::pair<AddrBytes, int32_t>;  // (masked address bytes, length)
 
 struct CidrHash {
@@ -212,10 +282,36 @@ struct CidrHash {
   }
 };
 
+// A shared, immutable PrefixEntry: PrefixState's advertisements and the
+// routes built from them (RibUnicastEntry::bestPrefixEntry) hold one copy, so
+// a route - and every copy Decision makes of it - takes a reference count,
+// not the entry's tag set and strings. Null stands for std::nullopt.
+class PrefixEntryRef {
+ public:
+  PrefixEntryRef() = default;
+  PrefixEntryRef(std::nullopt_t) {}  // NOLINT
+  PrefixEntryRef(PrefixEntry e) : p_(std::make_shared<const PrefixEntry>(std::move(e))) {}  // NOLINT
+  explicit operator bool() const { return p_ != nullptr; }
+  bool has_value() const { return p_ != nullptr; }
+  const PrefixEntry& operator*() const { return *p_; }
+  const PrefixEntry* operator->() const { return p_.get(); }
+  const PrefixEntry& value() const {
+    if (!p_) throw std::bad_optional_access();
+    return *p_;
+  }
+  bool operator==(const PrefixEntryRef& o) const { return p_ == o.p_ || (p_ && o.p_ && *p_ == *o.p_); }
+  bool operator!=(const PrefixEntryRef& o) const { return !(*this == o); }
+  bool operator==(const PrefixEntry& e) const { return p_ && *p_ == e; }
+  bool operator!=(const PrefixEntry& e) const { return !(*this == e); }
+
+ private:
+  std::shared_ptr<const PrefixEntry> p_;
+};
+
 struct RibUnicastEntry {
   Cidr prefix;
-  NextHopSet nexthops;
-  std::optional<PrefixEntry> bestPrefixEntry;
+  NextHops nexthops;
+  PrefixEntryRef bestPrefixEntry;
   std::string bestArea;
   bool doNotInstall{false};
   // RibEntry.h:65-69: bestArea does not take part
@@ -228,7 +324,7 @@ struct RibUnicastEntry {
 
 struct RibMplsEntry {
   int32_t label{0};
-  NextHopSet nexthops;
+  NextHops nexthops;
   bool operator==(const RibMplsEntry& o) const { return label == o.label && nexthops == o.nexthops; }  // RibEntry.h:123-126
   bool operator!=(const RibMplsEntry& o) const { return !(*this == o); }
 };
@@ -422,6 +518,7 @@ struct DecisionRouteDb {
       const auto& mine = unicastRoutes.shard(s);
       const auto& theirs = newDb.unicastRoutes.shard(s);
       auto& out = delta.unicastRoutesToUpdate.shard(s);
+      if (mine.empty()) out.reserve(theirs.size());  // a first build: every route is an update
       for (const auto& [prefix, entry] : theirs) {
         auto it = mine.find(prefix);
         if (it == mine.end() || it->second != entry) out.emplace(prefix, entry);

@@ -1,6 +1,7 @@
 // PrefixState (openr/decision/PrefixState.cpp:17-56) and its device mirror
 // (orh_prefix_set): see spf_solver.h.
 #include <algorithm>
+#include <type_traits>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -29,19 +30,54 @@ PrefixState::~PrefixState() {
 
 std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
                                             const PrefixEntry& e) {
+  return updatePrefix(node, area, PrefixEntry(e));
+}
+
+std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::string& area,
+                                            PrefixEntry&& e) {
   Cidr key{e.addr, e.len};
-  auto [it, inserted] = prefixes_[key].emplace(NodeAndArea{node, area}, e);
-  if (!inserted && it->second == e) return {};
-  if (!inserted) {
-    ksp2Entries_ -= it->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
-    it->second = e;
-  }
-  ksp2Entries_ += e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+  if (!upsertPrefix(node, area, std::move(e))) return {};
+  return {key};
+}
+
+bool PrefixState::upsertPrefix(const std::string& node, const std::string& area, PrefixEntry&& e) {
+  Cidr key{e.addr, e.len};
+  auto& entries = prefixes_[key];
+  auto it = entries.find(NodeAndArea{node, area});
+  if (it != entries.end() && it->second == e) return false;
+  const bool ksp2 = e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
   internName(node);
   internArea(area);
   internTagSet(e.tags);
+  if (it == entries.end()) {
+    entries.emplace(NodeAndArea{node, area}, PrefixEntryRef(std::move(e)));
+  } else {
+    ksp2Entries_ -= it->second->forwardingAlgorithm == kAlgoKsp2EdEcmp;
+    it->second = PrefixEntryRef(std::move(e));
+  }
+  ksp2Entries_ += ksp2;
   touch(key, false);
-  return {key};
+  return true;
+}
+
+void PrefixState::reserve(size_t n) {
+  // grown geometrically: a load fed in chunks rehashes O(log n) times
+  auto grow = [](auto& c, size_t want) {
+    if constexpr (std::is_same_v<std::decay_t<decltype(c)>, std::vector<typename std::decay_t<decltype(c)>::value_type>>) {
+      if (c.capacity() < want) c.reserve(std::max(want, 2 * c.size()));
+    } else {
+      if (want > c.bucket_count() * c.max_load_factor()) c.reserve(std::max(want, 2 * c.size()));
+    }
+  };
+  const size_t want = cidrOf_.size() + n;
+  grow(prefixes_, want);
+  grow(pid_, want);
+  grow(cidrOf_, want);
+  grow(live_, want);
+  grow(isDirty_, want);
+  grow(pidStamp_, want);
+  grow(run_, want);
+  grow(dirty_, dirty_.size() + n);
 }
 
 // distinct PrefixEntry.tags sets get ids (0: no tags) that the device mirror
@@ -50,6 +86,7 @@ std::vector<Cidr> PrefixState::updatePrefix(const std::string& node, const std::
 // so the device records read the table concurrently
 uint32_t PrefixState::internTagSet(const std::set<std::string>& tags) {
   if (tags.empty()) return 0;
+  if (auto it = tagSetIds_.find(tags); it != tagSetIds_.end()) return it->second;
   auto [it, inserted] = tagSetIds_.emplace(tags, 0u);
   if (inserted) {
     tagSets_.push_back(&it->first);
@@ -75,7 +112,7 @@ std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::
   if (it == prefixes_.end()) return {};
   auto e = it->second.find(NodeAndArea{node, area});
   if (e == it->second.end()) return {};
-  ksp2Entries_ -= e->second.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+  ksp2Entries_ -= e->second->forwardingAlgorithm == kAlgoKsp2EdEcmp;
   it->second.erase(e);
   const bool gone = it->second.empty();
   if (gone) prefixes_.erase(it);
@@ -83,16 +120,19 @@ std::vector<Cidr> PrefixState::deletePrefix(const std::string& node, const std::
   return {prefix};
 }
 
+// (looked up first: emplace would build - and free - a node per call)
 uint32_t PrefixState::internName(const std::string& n) {
-  auto [it, inserted] = nameIds_.emplace(n, static_cast<uint32_t>(names_.size()));
-  if (inserted) names_.push_back(n);
-  return it->second;
+  if (auto it = nameIds_.find(n); it != nameIds_.end()) return it->second;
+  nameIds_.emplace(n, static_cast<uint32_t>(names_.size()));
+  names_.push_back(n);
+  return static_cast<uint32_t>(names_.size() - 1);
 }
 
 uint32_t PrefixState::internArea(const std::string& a) {
-  auto [it, inserted] = areaIds_.emplace(a, static_cast<uint32_t>(areas_.size()));
-  if (inserted) areas_.push_back(a);
-  return it->second;
+  if (auto it = areaIds_.find(a); it != areaIds_.end()) return it->second;
+  areaIds_.emplace(a, static_cast<uint32_t>(areas_.size()));
+  areas_.push_back(a);
+  return static_cast<uint32_t>(areas_.size() - 1);
 }
 
 std::optional<uint32_t> PrefixState::nameId(const std::string& n) const {
@@ -112,8 +152,10 @@ std::optional<uint32_t> PrefixState::areaId(const std::string& a) const {
 void PrefixState::touch(const Cidr& prefix, bool erased) {
   uint32_t pid;
   stamp_ = nextGeneration();
-  auto it = pid_.find(prefix);
-  if (it != pid_.end()) {
+  // one lookup: a new prefix's slot is made here and numbered below
+  auto [it, fresh] = erased ? std::make_pair(pid_.find(prefix), false) : pid_.try_emplace(prefix, 0u);
+  if (erased && it == pid_.end()) return;
+  if (!fresh) {
     pid = it->second;
     if (erased) {
       pid_.erase(it);
@@ -127,7 +169,6 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
       }
     }
   } else {
-    if (erased) return;
     if (!freePids_.empty()) {
       pid = freePids_.back();
       freePids_.pop_back();
@@ -140,7 +181,7 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
       pidStamp_.push_back(0);
       run_.emplace_back(0u, 0u);
     }
-    pid_.emplace(prefix, pid);
+    it->second = pid;
     live_[pid] = 1;
   }
   pidStamp_[pid] = stamp_;
@@ -197,7 +238,7 @@ void PrefixState::buildRecords(const std::vector<uint32_t>* ids, std::vector<uin
     const uint32_t pid = ids ? (*ids)[i] : static_cast<uint32_t>(i);
     if (!live_[pid]) return;
     const AdvRef* a = advPool_.data() + run_[pid].first;
-    for (uint32_t k = 0; k < ptr[i + 1] - ptr[i]; ++k) recs[ptr[i] + k] = advRecord(*a[k].key, *a[k].entry);
+    for (uint32_t k = 0; k < ptr[i + 1] - ptr[i]; ++k) recs[ptr[i] + k] = advRecord(*a[k].key, **a[k].entry);
   });
 }
 
@@ -263,7 +304,7 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
       uint32_t k = ptr[pid];
       for (const auto& [na, e] : *ents[pid]) {
         advPool_[k] = AdvRef{&na, &e};
-        recs[k] = advRecord(na, e);
+        recs[k] = advRecord(na, *e);
         ++k;
       }
     });
@@ -319,7 +360,7 @@ orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {
       uint32_t k = ptr[i];
       for (const auto& [na, e] : *ents[i]) {
         advPool_[base + k] = AdvRef{&na, &e};
-        recs[k] = advRecord(na, e);
+        recs[k] = advRecord(na, *e);
         ++k;
       }
     });

@@ -52,6 +52,39 @@ int32_t RibPolicyStatement::weightOf(const std::optional<std::string>& area,
 
 bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidated) const {
   if (!match(route)) return false;  // RibPolicy.cpp:108-161
+  // the outcome depends on the nexthop set and this statement only: the
+  // routes sharing a set (NextHops) share its result, per thread. A memo
+  // entry holds its input set, so that set's address is not reused while
+  // it is a key; statements are named by a process-unique id
+  struct Key {
+    const void* set;
+    uint64_t stmt;
+    bool operator==(const Key& o) const { return set == o.set && stmt == o.stmt; }
+  };
+  struct KeyHash {
+    size_t operator()(const Key& k) const {
+      return std::hash<const void*>()(k.set) ^ (std::hash<uint64_t>()(k.stmt) * 0x9E3779B97F4A7C15ull);
+    }
+  };
+  struct Memo {
+    NextHops in, out;
+    bool kept;
+  };
+  thread_local std::unordered_map<Key, Memo, KeyHash> memo;
+  const bool shared = route.nexthops.id() != nullptr;
+  if (shared) {
+    auto it = memo.find(Key{route.nexthops.id(), id_});
+    if (it != memo.end()) {
+      if (!it->second.kept) {
+        if (invalidated) ++*invalidated;
+        return false;
+      }
+      route.nexthops = it->second.out;
+      return true;
+    }
+    if (memo.size() >= 4096) memo.clear();
+  }
+  const NextHops in = shared ? route.nexthops : NextHops{};
   auto weightOf = [&](const NextHopThrift& nh) { return this->weightOf(nh.area, nh.neighborNodeName); };
   bool any = false;
   for (const auto& nh : route.nexthops) {
@@ -62,6 +95,7 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidat
   }
   if (!any) {  // every nexthop dropped: keep the route as it was
     if (invalidated) ++*invalidated;
+    if (shared) memo.emplace(Key{in.id(), id_}, Memo{in, NextHops{}, false});
     return false;
   }
   // the kept nexthops move into a new set as nodes (no copies of their
@@ -69,15 +103,17 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route, uint64_t* invalidat
   // reference's insertion sequence into newNexthops (RibPolicy.cpp:116-141),
   // so the new set iterates as the reference's does (the weight is part of
   // the hash, NetworkUtil.cpp:57-66)
+  NextHopSet src = route.nexthops.take();  // moved out, or copied when shared
   NextHopSet out;  // grown as the reference's is (no reserve: the bucket count shapes the order)
-  while (!route.nexthops.empty()) {
-    auto node = route.nexthops.extract(route.nexthops.begin());
+  while (!src.empty()) {
+    auto node = src.extract(src.begin());
     const int32_t w = weightOf(node.value());
     if (w <= 0) continue;
     node.value().weight = w;
     out.insert(std::move(node));
   }
   route.nexthops = std::move(out);
+  if (shared) memo.emplace(Key{in.id(), id_}, Memo{in, route.nexthops, true});
   return true;
 }
 

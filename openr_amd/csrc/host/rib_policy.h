@@ -52,6 +52,7 @@ class RibPolicyStatement {
   RibRouteActionWeight action_;
   std::set<Cidr> prefixSet_;
   std::set<std::string> tagSet_;
+  uint64_t id_{nextGeneration()};  // names the statement in the nexthop memo
 };
 
 class RibPolicy {

@@ -310,11 +310,11 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
 
   bool hasBgp = false, hasNonBgp = false, missingMv = false, selfPrepend = true;
   for (const auto& [na, e] : entries) {
-    const bool bgp = e.type == kPrefixTypeBgp;
+    const bool bgp = e->type == kPrefixTypeBgp;
     hasBgp |= bgp;
     hasNonBgp |= !bgp;
-    if (na.first == me) selfPrepend &= e.prependLabel.has_value();
-    if (bgp && !e.mv) missingMv = true;
+    if (na.first == me) selfPrepend &= e->prependLabel.has_value();
+    if (bgp && !e->mv) missingMv = true;
   }
   if (hasBgp && ((hasNonBgp && !enableBestRouteSelection_) || missingMv)) return std::nullopt;
 
@@ -326,8 +326,8 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
   int32_t ft = kFwdSrMpls, fa = kAlgoKsp2EdEcmp;
   for (const auto& [na, e] : entries) {
     if (!best.allNodeAreas.count(na)) continue;
-    ft = std::min(ft, e.forwardingType);
-    fa = std::min(fa, e.forwardingAlgorithm);
+    ft = std::min(ft, e->forwardingType);
+    fa = std::min(fa, e->forwardingAlgorithm);
     if (ft == kFwdIp && fa == kAlgoSpEcmp) break;
   }
   if (kspPlan_) {
@@ -374,8 +374,8 @@ BestRouteSelectionResult SpfSolver::selectBestRoutes(const std::string& me,
                                                std::numeric_limits<int32_t>::min()};
     for (const auto& [na, e] : entries) {
       std::tuple<int32_t, int32_t, int32_t> t{
-          e.pathPreference, e.sourcePreference,
-          static_cast<int32_t>(0u - static_cast<uint32_t>(e.distance))};
+          e->pathPreference, e->sourcePreference,
+          static_cast<int32_t>(0u - static_cast<uint32_t>(e->distance))};
       if (t < best) continue;
       if (t > best) {
         best = t;
@@ -406,11 +406,11 @@ BestRouteSelectionResult SpfSolver::runBestPathSelectionBgp(const PrefixEntries&
   BestRouteSelectionResult r;  // Decision.cpp:864-902
   std::optional<MetricVector> bestVector;
   for (const auto& [na, e] : entries) {
-    const Cmp c = bestVector ? compareMv(*e.mv, *bestVector) : Cmp::kWinner;
+    const Cmp c = bestVector ? compareMv(*e->mv, *bestVector) : Cmp::kWinner;
     if (c == Cmp::kTie || c == Cmp::kError) return r;
     if (c == Cmp::kWinner) r.allNodeAreas.clear();
     if (c == Cmp::kWinner || c == Cmp::kTieWinner) {
-      bestVector = e.mv;
+      bestVector = e->mv;
       r.bestNodeArea = na;
     }
     if (c != Cmp::kLooser) r.allNodeAreas.insert(na);
@@ -530,8 +530,8 @@ NextHopSet SpfSolver::getNextHopsThrift(const std::string& me, const std::set<No
         if (!dst.empty()) {
           std::vector<int32_t> push;
           const auto& dpe = entries->at({dst, area});
-          if (dpe.prependLabel) {
-            push.push_back(*dpe.prependLabel);
+          if (dpe->prependLabel) {
+            push.push_back(*dpe->prependLabel);
             if (!isMplsLabelValid(push.back())) continue;
           }
           if (dst != nbr) {
@@ -558,7 +558,7 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsSpf(
   const std::set<NodeAndArea>* fp = &r.allNodeAreas;
   if (r.hasNode(me) && perDst) {
     for (const auto& [na, e] : entries) {
-      if (na.first == me && e.prependLabel) {
+      if (na.first == me && e->prependLabel) {
         filteredCopy = r.allNodeAreas;
         filteredCopy.erase(na);
         fp = &filteredCopy;
@@ -630,7 +630,7 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsKsp2(
       }
       labels.pop_back();  // PHP: the first hop's label is not pushed
       const auto& pe = entries.at({pls.nodeName(next), area});
-      if (pe.prependLabel) labels.push_front(*pe.prependLabel);
+      if (pe->prependLabel) labels.push_front(*pe->prependLabel);
       const Link& first = pls.link(ap.path.front());
       const uint32_t myId = *pls.nodeId(me);
       std::optional<MplsAction> act;
@@ -652,14 +652,14 @@ std::optional<RibUnicastEntry> SpfSolver::addBestPaths(const std::string& me, co
   std::optional<int64_t> minNh;
   for (const auto& na : r.allNodeAreas) {
     const auto& e = entries.at(na);
-    if (e.minNexthop && (!minNh || *e.minNexthop > *minNh)) minNh = e.minNexthop;
+    if (e->minNexthop && (!minNh || *e->minNexthop > *minNh)) minNh = e->minNexthop;
   }
   if (minNh && *minNh > static_cast<int64_t>(nexthops.size())) return std::nullopt;
   if (r.hasNode(me)) {
     std::optional<int32_t> prepend;
     for (const auto& [na, e] : entries) {
-      if (na.first == me && e.prependLabel) {
-        prepend = e.prependLabel;
+      if (na.first == me && e->prependLabel) {
+        prepend = e->prependLabel;
         break;
       }
     }
@@ -1029,7 +1029,7 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
     uint64_t gen = 0;
     const void* pol = nullptr;  // the DevicePolicy decision the statements index
     uint32_t hits = 0, misses = 0;
-    std::unordered_map<NhKey, NextHopSet, NhKeyHash> sets;
+    std::unordered_map<NhKey, NextHops, NhKeyHash> sets;  // shared with the routes
   };
   thread_local NhCache cache;
   if (cache.gen != selGen_ || cache.pol != &devPol_) {
@@ -1058,11 +1058,15 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
       e.nexthops = it->second;
     } else {
       ++cache.misses;
-      buildSet(e.nexthops);
+      NextHopSet built;
+      buildSet(built);
+      e.nexthops = std::move(built);
       cache.sets.emplace(key, e.nexthops);
     }
   } else {
-    buildSet(e.nexthops);
+    NextHopSet built;
+    buildSet(built);
+    e.nexthops = std::move(built);
   }
   uint32_t cnt = 0;
   const AdvRef* advs = ps.advs(pid, &cnt);
@@ -1216,7 +1220,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     try {
       for (const auto& [prefix, entries] : ps.prefixes()) {
         bool ksp = false;
-        for (const auto& [na, e] : entries) ksp |= e.forwardingAlgorithm == kAlgoKsp2EdEcmp;
+        for (const auto& [na, e] : entries) ksp |= e->forwardingAlgorithm == kAlgoKsp2EdEcmp;
         if (ksp) createRouteForPrefix(me, als, ps, prefix);
       }
     } catch (...) {
@@ -1258,6 +1262,76 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   };
   if (devPolicy) prof.mark("policy (device)");
   bool labelsDone = false;  // node-label routes built by the pipelined path
+  // node-label candidates per area (the candidate entry of every adjacency
+  // database); computed on the pool beside the unicast routes when the
+  // generic pool path runs, else in the node-label section below
+  struct LabelArea {
+    const std::string* area;
+    const LinkState* ls;
+    std::vector<const AdjacencyDatabase*> dbs;
+    const AreaWork* tw = nullptr;
+    const SpfRow* myRow = nullptr;
+    std::vector<std::optional<RibMplsEntry>> cand;
+  };
+  std::vector<LabelArea> labAreas;
+  std::vector<size_t> labOff{0};  // flat candidate index -> area
+  bool labPre = false;
+  auto labelPrepare = [&] {
+    for (const auto& [area, ls] : als) {
+      LabelArea la;
+      la.area = &area;
+      la.ls = &ls;
+      for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) la.dbs.push_back(&adjDb);
+      la.cand.resize(la.dbs.size());
+      // one area with device-selection templates: the route to node v is its
+      // first-hop mask in me's row, each bit's tight links with PHP when the
+      // neighbour is v, else SWAP(label) (getNextHopsThrift, :1278-1287)
+      if (dev && als.size() == 1)
+        for (const auto& w : areaWork_)
+          if (w.ls == &ls && w.words) la.tw = &w;
+      la.myRow = la.tw ? &ls.getSpfRow(me) : nullptr;
+      labOff.push_back(labOff.back() + la.dbs.size());
+      labAreas.push_back(std::move(la));
+    }
+  };
+  auto labelCompute = [&](LabelArea& la, size_t i) {
+    const std::string& area = *la.area;
+    const LinkState& ls = *la.ls;
+    const AdjacencyDatabase& adjDb = *la.dbs[i];
+    const int32_t label = adjDb.nodeLabel;
+    if (label == 0 || !isMplsLabelValid(label)) return;
+    RibMplsEntry entry{label, {}};
+    if (adjDb.thisNodeName == me) {
+      NextHopThrift nh;
+      nh.address.addr = std::string(16, '\0');  // "::"
+      nh.area = area;
+      nh.mplsAction = mpls(kPopAndLookup);
+      entry.nexthops.insert(std::move(nh));
+    } else if (la.tw) {
+      auto v = ls.nodeId(adjDb.thisNodeName);
+      if (!v || !la.myRow->reachable(*v)) return;
+      const int32_t metric = static_cast<int32_t>(la.myRow->metric(*v));
+      const uint32_t* vm = la.myRow->nh.data() + static_cast<size_t>(*v) * la.tw->words;
+      bool any = false;
+      for (uint32_t k = 0; k < la.tw->words; ++k) any |= vm[k] != 0;
+      if (any)  // one area: its words start at 0
+        insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops.edit(),
+                        [&](const NextHopThrift& nh) -> std::optional<MplsAction> {
+                          return *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp) : mpls(kSwap, label);
+                        });
+      if (!any) return;
+    } else {
+      const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};
+      if (als.size() == 1 && ls.nodeId(me)) {
+        if (!fastSpEcmp(me, ls, area, dst, false, label, entry.nexthops.edit())) return;
+      } else {
+        auto nhm = getNextHopsWithMetric(me, dst, false, als);
+        if (nhm.second.empty()) return;
+        entry.nexthops = getNextHopsThrift(me, dst, false, false, nhm.first, nhm.second, label, als, nullptr);
+      }
+    }
+    la.cand[i] = std::move(entry);
+  };
   std::vector<const Cidr*> keys;
   // static unicast routes go to the shard of their prefix id (shard 0 when
   // PrefixState lacks the prefix)
@@ -1330,7 +1404,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           for (uint32_t k = 0; k < tw->words; ++k) any |= vm[k] != 0;
           if (!any) return;
           // the row's words are the only area's: wordOff 0
-          insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops,
+          insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops.edit(),
                           [&](const NextHopThrift& nh) -> std::optional<MplsAction> {
                             return *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp) : mpls(kSwap, lbl);
                           });
@@ -1388,15 +1462,27 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       }
       labelsDone = true;
     } else if (!hasKsp && nOwn >= kParallelMin && pool.size() > 1) {
-      // contiguous pid ranges per worker into per-worker maps, then spliced
+      // contiguous pid ranges per worker into per-worker maps, then spliced;
+      // the node-label candidates (shard 0) are computed in the same pass
       std::vector<RouteMap> parts(pool.size());
-      pool.parallelFor(nOwn, [&](size_t w, size_t b, size_t e) {
+      if (shardRank_ == 0) {
+        labelPrepare();
+        labPre = true;
+      }
+      const size_t nLab = labOff.back();
+      pool.parallelFor(nOwn + nLab, [&](size_t w, size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) {
+          if (i >= nOwn) {
+            const size_t f = i - nOwn;
+            const size_t a = static_cast<size_t>(std::upper_bound(labOff.begin(), labOff.end(), f) - labOff.begin()) - 1;
+            labelCompute(labAreas[a], f - labOff[a]);
+            continue;
+          }
           const uint32_t pid = pidLo + static_cast<uint32_t>(i);
           if (ps.prefixLive(pid)) one(pid, parts[w].shard(RouteMap::shardOf(ps.prefixOf(pid))));
         }
       });
-      prof.mark("unicast (pool)");
+      prof.mark("unicast + labels (pool)");
       mergeParts(db.unicastRoutes, parts, pool);
       prof.mark("unicast merge");
     } else {
@@ -1477,64 +1563,25 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   // worker pool, then the duplicate resolution walks them in the reference's
   // iteration order (Decision.cpp:655-744).
   std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
-  for (const auto& [area, ls] : als) {
-    if (labelsDone || shardRank_ != 0) break;
-    std::vector<const AdjacencyDatabase*> dbs;
-    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) dbs.push_back(&adjDb);
-    std::vector<std::optional<RibMplsEntry>> cand(dbs.size());
-    // one area with device-selection templates: the route to node v is its
-    // first-hop mask in me's row, each bit's tight links with PHP when the
-    // neighbour is v, else SWAP(label) (getNextHopsThrift, :1278-1287)
-    const AreaWork* tw = nullptr;
-    if (dev && als.size() == 1)
-      for (const auto& w : areaWork_)
-        if (w.ls == &ls && w.words) tw = &w;
-    const SpfRow* myRow = tw ? &ls.getSpfRow(me) : nullptr;
-    auto compute = [&, &area = area, &ls = ls](size_t i) {
-      const AdjacencyDatabase& adjDb = *dbs[i];
-      const int32_t label = adjDb.nodeLabel;
-      if (label == 0 || !isMplsLabelValid(label)) return;
-      RibMplsEntry entry{label, {}};
-      if (adjDb.thisNodeName == me) {
-        NextHopThrift nh;
-        nh.address.addr = std::string(16, '\0');  // "::"
-        nh.area = area;
-        nh.mplsAction = mpls(kPopAndLookup);
-        entry.nexthops.insert(std::move(nh));
-      } else if (tw) {
-        auto v = ls.nodeId(adjDb.thisNodeName);
-        if (!v || !myRow->reachable(*v)) return;
-        const int32_t metric = static_cast<int32_t>(myRow->metric(*v));
-        const uint32_t* vm = myRow->nh.data() + static_cast<size_t>(*v) * tw->words;
-        bool any = false;
-        for (uint32_t k = 0; k < tw->words; ++k) any |= vm[k] != 0;
-        if (any)  // one area: its words start at 0
-          insertTemplates(vm, false, metric, nullptr, nullptr, entry.nexthops,
-                          [&](const NextHopThrift& nh) -> std::optional<MplsAction> {
-                            return *nh.neighborNodeName == adjDb.thisNodeName ? mpls(kPhp)
-                                                                              : mpls(kSwap, label);
-                          });
-        if (!any) return;
-      } else {
-        const std::set<NodeAndArea> dst{{adjDb.thisNodeName, area}};
-        if (als.size() == 1 && ls.nodeId(me)) {
-          if (!fastSpEcmp(me, ls, area, dst, false, label, entry.nexthops)) return;
-        } else {
-          auto nhm = getNextHopsWithMetric(me, dst, false, als);
-          if (nhm.second.empty()) return;
-          entry.nexthops = getNextHopsThrift(me, dst, false, false, nhm.first, nhm.second, label,
-                                             als, nullptr);
+  if (!labelsDone && shardRank_ == 0 && !labPre) {
+    labelPrepare();
+    const size_t nLab = labOff.back();
+    if (nLab >= kParallelMin && pool.size() > 1) {
+      pool.parallelFor(nLab, [&](size_t, size_t b, size_t e) {
+        for (size_t f = b; f < e; ++f) {
+          const size_t a = static_cast<size_t>(std::upper_bound(labOff.begin(), labOff.end(), f) - labOff.begin()) - 1;
+          labelCompute(labAreas[a], f - labOff[a]);
         }
-      }
-      cand[i] = std::move(entry);
-    };
-    if (dbs.size() >= kParallelMin && pool.size() > 1) {
-      pool.parallelFor(dbs.size(), [&](size_t, size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) compute(i);
       });
     } else {
-      for (size_t i = 0; i < dbs.size(); ++i) compute(i);
+      for (auto& la : labAreas)
+        for (size_t i = 0; i < la.dbs.size(); ++i) labelCompute(la, i);
     }
+  }
+  for (auto& la : labAreas) {
+    if (labelsDone || shardRank_ != 0) break;
+    const auto& dbs = la.dbs;
+    auto& cand = la.cand;
     // winner per label: (node name, candidate index); entries move once
     std::unordered_map<int32_t, std::pair<const std::string*, size_t>> win;
     win.reserve(dbs.size());

@@ -22,12 +22,12 @@
 
 namespace openr_amd {
 
-using PrefixEntries = std::unordered_map<NodeAndArea, PrefixEntry, StrPairHash>;
+using PrefixEntries = std::unordered_map<NodeAndArea, PrefixEntryRef, StrPairHash>;
 
 // one advertisement as the device mirror numbers it (order within a prefix)
 struct AdvRef {
   const NodeAndArea* key;
-  const PrefixEntry* entry;
+  const PrefixEntryRef* entry;  // shared with the routes built from it
 };
 
 // PrefixState (openr/decision/PrefixState.h:22-70) plus a device mirror of
@@ -45,6 +45,12 @@ class PrefixState {
 
   std::vector<Cidr> updatePrefix(const std::string& node, const std::string& area,
                                  const PrefixEntry& e);
+  // the same, taking the entry (no copy of it)
+  std::vector<Cidr> updatePrefix(const std::string& node, const std::string& area, PrefixEntry&& e);
+  // updatePrefix without the changed-prefix list: whether the prefix changed
+  bool upsertPrefix(const std::string& node, const std::string& area, PrefixEntry&& e);
+  // capacity for n more prefixes (a bulk load: no rehash of the maps)
+  void reserve(size_t n);
   std::vector<Cidr> deletePrefix(const std::string& node, const std::string& area,
                                  const Cidr& prefix);
   const std::unordered_map<Cidr, PrefixEntries, CidrHash>& prefixes() const { return prefixes_; }

@@ -197,7 +197,7 @@ void writeUnicastRoute(Writer& w, const RibUnicastEntry& e) {  // Network.thrift
   w.structBegin();
   w.field(1, kStruct);
   writeIpPrefix(w, e.prefix);
-  writeNextHops(w, 4, e.nexthops);
+  writeNextHops(w, 4, e.nexthops.set());
   const bool bgp = e.bestPrefixEntry && e.bestPrefixEntry->type == kPrefixTypeBgp;
   if (bgp) {
     w.fieldI32(5, kPrefixTypeBgp);
@@ -211,7 +211,7 @@ void writeUnicastRoute(Writer& w, const RibUnicastEntry& e) {  // Network.thrift
 void writeMplsRoute(Writer& w, const RibMplsEntry& e) {  // Network.thrift:99-103
   w.structBegin();
   w.fieldI32(1, e.label);
-  writeNextHops(w, 4, e.nexthops);
+  writeNextHops(w, 4, e.nexthops.set());
   w.structEnd();
 }
 

@@ -399,6 +399,15 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   __shared__ uint32_t s_lo[3], s_hin[3];  // per level: min / ~max id with a new frontier bit
   M* f_cur = reinterpret_cast<M*>(lds);
   M* f_nxt = f_cur + a.ms_pitch;
+  // the ELL columns hold byte offsets into a frontier array (16 bits each:
+  // the planner keeps pitch * sizeof(M) <= 64 KiB), so a gather address is
+  // one add of the array's offset that also picks the half-word (3 VALU ->
+  // 1 per gather, ~3 % of the step: profiles/r05/l_msbfs_offsets_ab.txt); u64
+  // masks (opt-in) store dword offsets, doubled at the read
+  constexpr uint32_t kE = sizeof(M);
+  constexpr uint32_t kC = kE <= 4 ? kE : 4;  // bytes per stored column unit
+  const char* const lbase = reinterpret_cast<const char*>(lds);
+  uint32_t cur_off = 0u, nxt_off = a.ms_pitch * kE;  // f_cur / f_nxt in bytes
   uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
   // arrival log (u16 / u32 masks, kLog): each wave appends its nodes' level
   // events {new bits (hi), slice j << 14 | lane << 8 | level (lo)} to a log
@@ -456,16 +465,32 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   for (int j = 0; j < J; ++j) {
     const uint32_t v = j * B + tid;
 #pragma unroll
-    for (int h = 0; h < KH; ++h) col[j][h] = NZ | (NZ << 16);
+    for (int h = 0; h < KH; ++h) col[j][h] = (NZ * kC) | ((NZ * kC) << 16);
     vis[j] = full;
     if (v < N) {
       const uint2* slots = a.recs + static_cast<size_t>(v) * K;
       uint2 r[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) r[k] = slots[k];
+#ifdef ORH_X_SORT
+      uint32_t c[2 * KH];
+#pragma unroll
+      for (int k = 0; k < 2 * KH; ++k) c[k] = k < K ? ms_col(r[k], NZ) : NZ;
+#pragma unroll
+      for (int x = 0; x < 2 * KH; ++x)
+#pragma unroll
+        for (int y = 0; y + 1 < 2 * KH - x; ++y) {
+          const uint32_t lo = min(c[y], c[y + 1]), hi = max(c[y], c[y + 1]);
+          c[y] = lo;
+          c[y + 1] = hi;
+        }
+#pragma unroll
+      for (int h = 0; h < KH; ++h) col[j][h] = c[2 * h] * kC | (c[2 * h + 1] * kC << 16);
+#else
 #pragma unroll
       for (int h = 0; h < KH; ++h)
-        col[j][h] = ms_col(r[2 * h], NZ) | ((2 * h + 1 < K ? ms_col(r[2 * h + 1], NZ) : NZ) << 16);
+        col[j][h] = ms_col(r[2 * h], NZ) * kC | ((2 * h + 1 < K ? ms_col(r[2 * h + 1], NZ) : NZ) * kC << 16);
+#endif
       if (r[0].x & ORH_REC_ROW_OVL) ovlm |= 1u << j;
       if (r[K - 1].x & ORH_REC_CONT) ovfm |= 1u << j;
     }
@@ -543,8 +568,9 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
         acc[g] = 0u;
 #pragma unroll
         for (int h = 0; h < KH; ++h) {
-          acc[g] |= f_cur[col[j0 + g][h] & 0xFFFFu];
-          if (2 * h + 1 < K) acc[g] |= f_cur[col[j0 + g][h] >> 16];
+          acc[g] |= *reinterpret_cast<const M*>(lbase + cur_off + (col[j0 + g][h] & 0xFFFFu) * (kE / kC));
+          if (2 * h + 1 < K)
+            acc[g] |= *reinterpret_cast<const M*>(lbase + cur_off + (col[j0 + g][h] >> 16) * (kE / kC));
         }
       }
 #pragma unroll
@@ -625,6 +651,9 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     M* t = f_cur;
     f_cur = f_nxt;
     f_nxt = t;
+    const uint32_t to = cur_off;
+    cur_off = nxt_off;
+    nxt_off = to;
   }
   if constexpr (kLog) {
     // the logs -> node-major level blocks, one wave's nodes at a time: the
@@ -2463,7 +2492,8 @@ SpfPlan plan_spf(uint32_t n_nodes, bool uniform, uint64_t path_bound, uint32_t e
     if (j <= 32) {
       for (uint32_t mb = 4; mb >= 2; mb /= 2) {
         const size_t bytes = 2 * static_cast<size_t>(mb) * pitch;
-        if (bytes <= lds_limit) {
+        // (16-bit byte offsets in the kernel's ELL columns)
+        if (bytes <= lds_limit && static_cast<size_t>(mb) * pitch <= 65536) {
           p.variant = SpfVariant::kMsBfs;
           p.mask_bytes = mb;
           p.ms_j = (j + 3) & ~3u;
@@ -2591,7 +2621,8 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
   const size_t bytes64 = 2 * 8 * static_cast<size_t>(plan.ms_pitch);
   const char* e = getenv("ORH_MS_WIDE");
   const bool allow = e && atoi(e) == 1;
-  if (allow && plan.mask_bytes == 4 && n_cu && n_rows > 32ull * n_cu && bytes64 <= lds_limit) {
+  if (allow && plan.mask_bytes == 4 && n_cu && n_rows > 32ull * n_cu && bytes64 <= lds_limit &&
+      4ull * plan.ms_pitch <= 65536) {
     plan.mask_bytes = 8;
     plan.lds_bytes = bytes64;
     plan.ms_width = std::min<uint32_t>(64, (n_rows + n_cu - 1) / n_cu);
