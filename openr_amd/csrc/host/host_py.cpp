@@ -851,6 +851,17 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("prefetch_spf_results", &LinkState::prefetchSpfResults, py::arg("nodes"),
            py::arg("use_link_metric") = true)
       .def("prefetch_kth_paths", &LinkState::prefetchKthPaths)
+      .def("time_prefetch_kth_paths",  // wall seconds of each cold prefetchKthPaths call (memo dropped first)
+           [](const LinkState& ls, const std::vector<std::pair<std::string, std::string>>& pairs, int reps) {
+             std::vector<double> out;
+             for (int r = 0; r < reps; ++r) {
+               ls.dropMemo();
+               const auto t0 = std::chrono::steady_clock::now();
+               ls.prefetchKthPaths(pairs);
+               out.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+             }
+             return out;
+           })
       .def("ksp_stats", [](const LinkState& s) {  // pairs traced on the device / host
         return py::make_tuple(s.kspDevicePairs_, s.kspHostPairs_);
       })

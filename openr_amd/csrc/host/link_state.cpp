@@ -276,13 +276,15 @@ bool LinkState::updateNodeOverloaded(const std::string& n, bool o, Metric up, Me
 }
 
 void LinkState::invalidate(bool topologyChanged) {
-  if (topologyChanged) {
-    spfResults_.clear();
-    spfMaps_.clear();
-    kthPaths_.clear();
-    kthLinkPaths_.clear();
-    countedOnDevice_.clear();
-  }
+  if (topologyChanged) dropMemo();
+}
+
+void LinkState::dropMemo() const {
+  spfResults_.clear();
+  spfMaps_.clear();
+  kthPaths_.clear();
+  kthLinkPaths_.clear();
+  countedOnDevice_.clear();
 }
 
 // ---- mutators -------------------------------------------------------------
@@ -723,8 +725,9 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
     kthPaths_.reserve(kthPaths_.size() + 2 * pairs.size());
     for (const auto& pr : pairs) {
       if (!seen.insert(pr).second) continue;
-      const bool m1 = kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{1})) != 0;
-      const bool m2 = kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{2})) != 0;
+      const bool any = !kthPaths_.empty();  // (a cold batch skips the key copies)
+      const bool m1 = any && kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{1})) != 0;
+      const bool m2 = any && kthPaths_.count(std::make_tuple(pr.first, pr.second, size_t{2})) != 0;
       if (m1 && m2) continue;
       auto s = nodeId(pr.first);
       auto d = nodeId(pr.second);

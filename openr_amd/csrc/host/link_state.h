@@ -250,6 +250,9 @@ class LinkState {
                                   const std::vector<std::vector<uint32_t>>* ignoreSets) const;
   void prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
   void prefetchKthPaths(const std::vector<std::pair<std::string, std::string>>& pairs) const;
+  // drop every memoized SPF row and k-th path set (what a topology change
+  // does): benchmarks repeat a cold prefetch with it
+  void dropMemo() const;
   // the same over host traces of device rows (exact-order graphs, pairs the
   // device trace flags)
   void prefetchKthPathsHost(const std::vector<std::pair<std::string, std::string>>& pairs) const;

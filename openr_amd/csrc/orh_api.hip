@@ -2525,8 +2525,9 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     }
     for (uint32_t x : srcs) ro[x] = -1;
     const uint32_t S = static_cast<uint32_t>(srcs.size());
-    // device layout (u32 words): dist1 [S][N] | dist2 [P][N] | sources [S] |
-    // src | dst | row1 | rowp | ign_ptr [P+1] | ign [P][cap] | need2 | out | visited | stack
+    // device layout (u32 words): the staged request first - src | dst | row1 |
+    // rowp | ign_ptr [P+1] | sources [S] | stop targets - then dist1 [S][N] |
+    // dist2 [P][N] | ign [P][cap] | need2 | out | visited | stack
     // (the traces read distances only: both searches run dist-only)
     const size_t nd1 = static_cast<size_t>(S) * N, nd2 = static_cast<size_t>(P) * N;
     size_t off = 0;
@@ -2535,40 +2536,42 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
       off += (words_ + 63) & ~size_t{63};  // 256-byte aligned pieces
       return o;
     };
-    const size_t o_d1 = take(nd1), o_d2 = take(nd2), o_s1 = take(S);
     const size_t o_src = take(P), o_dst = take(P), o_r1 = take(P), o_rp = take(P), o_ip = take(P + 1);
+    const size_t o_s1 = take(S);
+    // early-stop targets of the searches: the k = 1 row of a source stops once
+    // all its pairs' destinations are final, a k = 2 row once its pair's is
+    const size_t o_sp1 = take(S + 1), o_sn1 = take(P), o_sp2 = take(P + 1);
+    const size_t staged = off;  // words uploaded in one copy
+    const size_t o_d1 = take(nd1), o_d2 = take(nd2);
     const size_t o_ign = take(size_t{P} * kKspIgnCap), o_need = take(P), o_out = take(size_t{P} * kKspOutCap);
     const size_t o_vis = take(size_t{P} * kKspHashCap);
     const size_t o_st = take(size_t{P} * kKspStackCap * (sizeof(orh::KspFrame) / 4));
     const size_t o_ovf = take(size_t{std::max(S, P)} + 1);
-    // early-stop targets of the searches: the k = 1 row of a source stops once
-    // all its pairs' destinations are final, a k = 2 row once its pair's is
-    const size_t o_sp1 = take(S + 1), o_sn1 = take(P), o_sp2 = take(P + 1);
     rc = ensure_bytes(ctx, &ctx->d_ksp, &ctx->d_ksp_cap, off * 4);
     if (rc) return rc;
     uint32_t* D = reinterpret_cast<uint32_t*>(ctx->d_ksp);
-    // staged request: src | dst | row1 | rowp | ign_ptr (fixed stride)
-    std::vector<uint32_t> ip(P + 1);
-    for (uint32_t i = 0; i <= P; ++i) ip[i] = i * kKspIgnCap;
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_src, h_src + c0, P * 4ull, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_dst, h_dst + c0, P * 4ull, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_r1, row1.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_rp, rowp.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_ip, ip.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
-    ORH_HIP(ctx, hipMemcpyAsync(D + o_s1, srcs.data(), S * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    // the staged request is assembled in this chunk's pinned output block
+    // (its copy-out comes later on the same stream) and goes up in one copy
+    uint32_t* H = ctx->h_ksp + size_t{c0} * kKspOutCap;
+    if (staged > size_t{P} * kKspOutCap) return fail(ctx, ORH_E_INVALID, "orh_ksp2_batch: staging block too small");
+    std::memcpy(H + o_src, h_src + c0, P * 4ull);
+    std::memcpy(H + o_dst, h_dst + c0, P * 4ull);
+    std::memcpy(H + o_r1, row1.data(), P * 4ull);
+    std::memcpy(H + o_rp, rowp.data(), P * 4ull);
+    for (uint32_t i = 0; i <= P; ++i) H[o_ip + i] = i * kKspIgnCap;  // fixed-stride ignore lists
+    std::memcpy(H + o_s1, srcs.data(), S * 4ull);
     const char* stop_e = getenv("ORH_KSP_STOP");  // 0: full searches (A/B)
     const bool stop = !(stop_e && stop_e[0] == '0');
-    std::vector<uint32_t> sp1(S + 1, 0), sn1(P), sp2(P + 1);
     if (stop) {
+      uint32_t* sp1 = H + o_sp1;
+      std::fill(sp1, sp1 + S + 1, 0u);
       for (uint32_t i = 0; i < P; ++i) ++sp1[row1[i] + 1];
       for (uint32_t r = 0; r < S; ++r) sp1[r + 1] += sp1[r];
-      std::vector<uint32_t> fill(sp1.begin(), sp1.end() - 1);
-      for (uint32_t i = 0; i < P; ++i) sn1[fill[row1[i]]++] = h_dst[c0 + i];
-      for (uint32_t i = 0; i <= P; ++i) sp2[i] = i;
-      ORH_HIP(ctx, hipMemcpyAsync(D + o_sp1, sp1.data(), (S + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
-      ORH_HIP(ctx, hipMemcpyAsync(D + o_sn1, sn1.data(), P * 4ull, hipMemcpyHostToDevice, ctx->stream));
-      ORH_HIP(ctx, hipMemcpyAsync(D + o_sp2, sp2.data(), (P + 1) * 4ull, hipMemcpyHostToDevice, ctx->stream));
+      std::vector<uint32_t> fill(sp1, sp1 + S);
+      for (uint32_t i = 0; i < P; ++i) H[o_sn1 + fill[row1[i]]++] = h_dst[c0 + i];
+      for (uint32_t i = 0; i <= P; ++i) H[o_sp2 + i] = i;
     }
+    ORH_HIP(ctx, hipMemcpyAsync(D, H, staged * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
     // both searches: the HBM frontier kernel, distances only (u32 labels)
     orh::SpfPlan fp = orh::plan_spf(N, uniform, bound, g->ell_k, ctx->lds_limit, false, orh::SpfMode::kGlobal);
