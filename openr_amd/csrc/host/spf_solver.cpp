@@ -1009,10 +1009,13 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
   };
   // Routes with the same first-hop mask, metric, family and policy statement
   // get the same set from the same insertion sequence: it is built once per
-  // selection and worker thread and then copied. A copy of a libstdc++
-  // unordered_set keeps the bucket count and node order, so it iterates
-  // exactly as the set built in place - the reference's order (a30). C3:
-  // ~2,400 distinct sets for 100k routes.
+  // worker thread and then shared (NextHops), so it iterates exactly as the
+  // set built in place - the reference's order (a30). C3: ~2,400 distinct
+  // sets for 100k routes. A set depends on nothing else but the nexthop
+  // templates and area layout (their digest, prevLayout_ of the selection
+  // that produced the record) and the policy's weights (its generation), so
+  // the cache lives across builds while those stay: a build after a
+  // topology change elsewhere builds no set it had before.
   struct NhKey {  // mask words, metric, family + statement (inline: no allocation)
     uint32_t w[8];
     uint32_t n;
@@ -1026,16 +1029,16 @@ RibUnicastEntry SpfSolver::materialize(uint32_t pid, const PrefixState& ps) cons
     }
   };
   struct NhCache {
-    uint64_t gen = 0;
-    const void* pol = nullptr;  // the DevicePolicy decision the statements index
+    uint64_t layout = 0, polGen = 0;
     uint32_t hits = 0, misses = 0;
     std::unordered_map<NhKey, NextHops, NhKeyHash> sets;  // shared with the routes
   };
   thread_local NhCache cache;
-  if (cache.gen != selGen_ || cache.pol != &devPol_) {
+  const uint64_t polGen = s < ORH_POL_MAX_STMTS && devPol_.policy ? devPol_.policy->generation() : 0;
+  if (cache.layout != prevLayout_ || (s < ORH_POL_MAX_STMTS && cache.polGen != polGen)) {
     cache.sets.clear();
-    cache.gen = selGen_;
-    cache.pol = &devPol_;
+    cache.layout = prevLayout_;
+    cache.polGen = polGen;
     cache.hits = cache.misses = 0;
   }
   // off when the words do not fit the key, or once the sets turn out to be
