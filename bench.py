@@ -299,7 +299,8 @@ def main():
 
 # newest committed PMC summary of this command (tools/profile.sh +
 # tools/pmc_summary.py), per sweep launch
-PMC_PROFILES = [os.path.join(ROOT, "profiles", "r04", "pmc.json"),
+PMC_PROFILES = [os.path.join(ROOT, "profiles", "r05", "pmc.json"),
+                os.path.join(ROOT, "profiles", "r04", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r03", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r02", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r01", "v6_pmc.json")]
