@@ -179,7 +179,9 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
                             hipStream_t s);
 // multi-source plans, once the row count is known: sources per batch, and
 // u64 masks when u32 ones would put more than one batch on a CU
-void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit);
+// alone: no other sweep in flight on the device (lone-sweep plan)
+void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit,
+                  bool alone = false);
 // bytes of node-major level scratch a multi-source plan needs for n_rows rows
 size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows);
 // bytes of the multi-source arrival logs (u16 / u32 masks; 0 otherwise), after

@@ -2588,7 +2588,8 @@ size_t ms_scratch_bytes(const SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows) 
   return static_cast<size_t>((n_rows + w - 1) / w) * n_nodes * (plan.mask_bytes * 8);
 }
 
-void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit) {
+void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_cu, size_t lds_limit,
+                  bool alone) {
   if (plan.variant != SpfVariant::kMsBfs) return;
   plan.ms_width = plan.mask_bytes * 8;
   // ORH_MS_WIDE=1 (opt-in): when u32 masks need more than one batch per CU
@@ -2616,6 +2617,17 @@ void ms_set_width(SpfPlan& plan, uint32_t n_nodes, uint32_t n_rows, uint32_t n_c
       plan.block = 1024;
       plan.ms_j = (j + 3) & ~3u;
       plan.ms_skip = lat && atoi(lat) == 2;
+    } else if (!(lat && atoi(lat) == 0) && !getenv("ORH_MS_BLOCK") && alone && plan.block == 512) {
+      // lone-sweep plan: no other sweep in flight on the device, so the
+      // batches do not share CUs with other streams' kernels and 12 waves
+      // per batch cut the per-level time (one C2 sweep 0.82 -> 0.68 ms of
+      // MS-BFS); under concurrent sweeps 8 waves stay (the 4-lane step
+      // 24.8 vs 26.3 ms at 12, profiles/r04/ai_ms_block_ab.txt)
+      const uint32_t j12 = (n_nodes + 767) / 768;
+      if (j12 <= 32) {
+        plan.block = 768;
+        plan.ms_j = (j12 + 3) & ~3u;
+      }
     }
   }
   const size_t bytes64 = 2 * 8 * static_cast<size_t>(plan.ms_pitch);

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -535,6 +536,19 @@ int orh_device_count(int* out) {
   return ORH_OK;
 }
 
+// every live context, by device: a sweep planned while no other context of
+// its device has a sweep in flight (its end event not reached) takes the
+// lone-sweep plan (orh::ms_set_width)
+static std::mutex g_ctx_mu;
+static std::vector<orh_ctx*> g_ctxs;
+
+static bool device_busy_elsewhere(const orh_ctx* ctx) {
+  std::lock_guard<std::mutex> lock(g_ctx_mu);
+  for (const orh_ctx* o : g_ctxs)
+    if (o != ctx && o->device == ctx->device && hipEventQuery(o->ev1) == hipErrorNotReady) return true;
+  return false;
+}
+
 int orh_create(int device, uint32_t flags, orh_ctx** out) {
   (void)flags;
   if (!out) return ORH_E_INVALID;
@@ -567,6 +581,10 @@ int orh_create(int device, uint32_t flags, orh_ctx** out) {
     ctx->lds_limit = std::max<size_t>(prop.sharedMemPerBlock, 64 * 1024);
     if (prop.multiProcessorCount > 0) ctx->n_cu = static_cast<uint32_t>(prop.multiProcessorCount);
   }
+  {
+    std::lock_guard<std::mutex> lock(g_ctx_mu);
+    g_ctxs.push_back(ctx);
+  }
   *out = ctx;
   return ORH_OK;
 }
@@ -585,6 +603,10 @@ int orh_set_repair_mode(orh_ctx* ctx, int mode) {
 
 int orh_destroy(orh_ctx* ctx) {
   if (!ctx) return ORH_E_INVALID;
+  {
+    std::lock_guard<std::mutex> lock(g_ctx_mu);
+    g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), ctx), g_ctxs.end());
+  }
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   hipFree(ctx->d_req);
@@ -1924,7 +1946,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // when one mask word covers every source and the two-phase scheme would
   // need extra neighbour rows (or the HBM kernel is forced)
   orh::SpfPlan run_plan = plan;
-  orh::ms_set_width(run_plan, N, n_rows, ctx->n_cu, ctx->lds_limit);
+  orh::ms_set_width(run_plan, N, n_rows, ctx->n_cu, ctx->lds_limit,
+                    run_plan.variant == orh::SpfVariant::kMsBfs && !device_busy_elsewhere(ctx));
   // uniform metric, at most ORH_BFS_NH_MAX sources (default: one per CU):
   // one fused BFS + first-hop workgroup per source instead of searching
   // every neighbour row too (ORH_BFS_NH_MAX=0 turns it off)
