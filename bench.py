@@ -188,6 +188,7 @@ def main():
             probe.run()
             kernel_ms.append(probe.last_ms())
             phases.append(probe.phase_ms())
+        probe_info = probe.info()
 
     value = total_units * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -245,6 +246,10 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel_ms": round(kms, 4),
+                     # the sweep ran alone: the lone-sweep plan (12-wave
+                     # batches); the step's overlapping sweeps run 8-wave ones
+                     "plan": {"ms_threads": probe_info.get("ms_threads"),
+                              "batch_sources": probe_info.get("batch_sources")},
                      "phase_ms": [round(statistics.mean(p[0] for p in phases), 4),
                                   round(statistics.mean(p[1] for p in phases), 4)],
                      "algorithmic_bytes_per_source": bytes_per_source,
