@@ -1082,6 +1082,13 @@ PYBIND11_MODULE(_openr_host, m) {
       });
 
   // DecisionRouteDb::calculateUpdate / update (Decision.cpp:108-160)
+  // the bulk ingest's parser against the general one (tests): (whether the
+  // CPython-API path took the entry, the entry as each path reads it)
+  m.def("parse_prefix_entry", [](py::tuple t) {
+    PrefixEntry fast;
+    const bool ok = entryFromWireFast(t.ptr(), fast);
+    return py::make_tuple(ok, ok ? entryToWire(fast) : py::none(), entryToWire(entryFromWire(t)));
+  });
   m.def("host_threads", [] { return WorkerPool::instance().size(); },
         "threads of the host worker pool (the caller included)");
   // ---- thrift Compact wire -----------------------
