@@ -278,6 +278,11 @@ def main():
             ls.update_adjacency_database(db)
             return solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3
 
+        # two untimed topology changes first: the first ones after the initial
+        # build grow one-time buffers (mirror patch staging, set caches) and
+        # measured 3.5-4.4 ms against a steady 2.3-2.7 (tools/c2_build_spread.py)
+        cold()
+        cold()
         st0 = cgroup_cpu_stat()
         cold_ms = [cold() for _ in range(7)]
         st1 = cgroup_cpu_stat()
@@ -286,6 +291,7 @@ def main():
         out["build_route_db_ms"] = round(statistics.median(cold_ms), 3)
         out["build_route_db_warm_ms"] = round(statistics.median(warm_ms), 3)
         out["build_route_db_runs"] = {"cold_ms": spread(cold_ms), "warm_ms": spread(warm_ms),
+                                      "cold_settle": "2 untimed topology-change builds before the 7 timed ones",
                                       "host_pool_threads": hip.module.host_threads(),
                                       "cgroup_throttling": {"cold": throttle_delta(st0, st1),
                                                             "warm": throttle_delta(st1, st2)}}
@@ -369,7 +375,7 @@ def spread(xs):
     """median, min, max and (max - min) / median of repeated timings (ms)."""
     m = statistics.median(xs)
     return {"median": round(m, 3), "min": round(min(xs), 3), "max": round(max(xs), 3),
-            "spread": round((max(xs) - min(xs)) / m, 3) if m else None}
+            "spread": round((max(xs) - min(xs)) / m, 3) if m else None, "ms": [round(x, 3) for x in xs]}
 
 
 def usable_cpus():
