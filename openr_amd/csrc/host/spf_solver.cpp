@@ -1356,6 +1356,96 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     deviceSelected_ = nDev;
     hostSelected_ = nHost;
     using RouteMap = decltype(db.unicastRoutes);
+    // the unicast routes of [pidLo, pidHi) into db, and `extra(k)` for k in
+    // [0, nExtra) (node-label candidates) in the same pool pass. Two passes
+    // (ORH_ROUTE_TWO_PHASE=0, A/B: one pass into per-worker maps, then
+    // spliced): the routes are built over contiguous prefix-id ranges into a
+    // flat slot array (no hashing, no map nodes), each worker listing its
+    // slots per output shard; then each shard's routes move into its map,
+    // shard by shard on the pool - one insertion per route instead of an
+    // insertion and a splice (C5: build 51-54 -> 42-45 ms,
+    // profiles/r05/ze_route_two_phase_ab.txt)
+    auto fillRoutes = [&](size_t nExtra, auto&& extra) {
+      static const bool twoPhase = [] {
+        const char* e = std::getenv("ORH_ROUTE_TWO_PHASE");
+        return !(e && e[0] == '0');
+      }();
+      if (!twoPhase) {
+        std::vector<RouteMap> parts(pool.size());
+        pool.parallelFor(nOwn + nExtra, [&](size_t w, size_t b, size_t e) {
+          for (size_t i = b; i < e; ++i) {
+            if (i >= nOwn) {
+              extra(i - nOwn);
+              continue;
+            }
+            const uint32_t pid = pidLo + static_cast<uint32_t>(i);
+            if (!ps.prefixLive(pid)) continue;
+            if (selStatus_[pid] == ORH_SEL_ROUTE) {
+              RibUnicastEntry r = materialize(pid, ps);
+              Cidr k = r.prefix;
+              parts[w].shard(RouteMap::shardOf(k)).emplace(std::move(k), std::move(r));
+            } else if (selStatus_[pid] == ORH_SEL_HOST) {
+              if (auto r = createRouteForPrefix(me, als, ps, ps.prefixOf(pid))) {
+                hostPolicy(*r);
+                Cidr k = r->prefix;
+                parts[w].shard(RouteMap::shardOf(k)).emplace(std::move(k), std::move(*r));
+              }
+            }
+          }
+        });
+        prof.mark("unicast + labels (pool)");
+        mergeParts(db.unicastRoutes, parts, pool);
+        prof.mark("unicast merge");
+        return;
+      }
+      constexpr size_t kS = RouteMap::kShards;
+      const size_t W = pool.size();
+      RouteSlots& slots = routeSlots_;
+      slots.reserve(nOwn);
+      slots.lists.resize(W * kS);
+      for (auto& l : slots.lists) l.clear();
+      pool.parallelFor(nOwn + nExtra, [&](size_t w, size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) {
+          if (i >= nOwn) {
+            extra(i - nOwn);
+            continue;
+          }
+          const uint32_t pid = pidLo + static_cast<uint32_t>(i);
+          if (!ps.prefixLive(pid)) continue;
+          RibUnicastEntry* slot = slots.at(i);
+          if (selStatus_[pid] == ORH_SEL_ROUTE) {
+            new (slot) RibUnicastEntry(materialize(pid, ps));
+          } else if (selStatus_[pid] == ORH_SEL_HOST) {
+            auto r = createRouteForPrefix(me, als, ps, ps.prefixOf(pid));
+            if (!r) continue;
+            hostPolicy(*r);
+            new (slot) RibUnicastEntry(std::move(*r));
+          } else {
+            continue;
+          }
+          slots.lists[w * kS + RouteMap::shardOf(slot->prefix)].push_back(static_cast<uint32_t>(i));
+        }
+      });
+      prof.mark("unicast + labels (pool)");
+      std::atomic<bool> dup{false};
+      pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
+        for (size_t sh = b; sh < e; ++sh) {
+          size_t n = 0;
+          for (size_t w = 0; w < W; ++w) n += slots.lists[w * kS + sh].size();
+          auto& dst = db.unicastRoutes.shard(sh);
+          dst.reserve(dst.size() + n);
+          for (size_t w = 0; w < W; ++w)
+            for (uint32_t i : slots.lists[w * kS + sh]) {
+              RibUnicastEntry* r = slots.at(i);
+              Cidr k = r->prefix;
+              if (!dst.emplace(std::move(k), std::move(*r)).second) dup = true;
+              r->~RibUnicastEntry();
+            }
+        }
+      });
+      if (dup) throw std::logic_error("duplicate unicast route");
+      prof.mark("unicast merge");
+    };
     auto one = [&](uint32_t pid, RouteMap::Shard& out) {
       if (!ps.prefixLive(pid)) return;
       if (selStatus_[pid] == ORH_SEL_ROUTE) {
@@ -1414,22 +1504,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         }
         cand[i] = std::move(entry);
       };
-      {
-        std::vector<RouteMap> parts(pool.size());
-        pool.parallelFor(nOwn + dbs.size(), [&](size_t w, size_t b, size_t e) {
-          for (size_t i = b; i < e; ++i) {
-            if (i < nOwn) {
-              const uint32_t pid = pidLo + static_cast<uint32_t>(i);
-              if (ps.prefixLive(pid)) one(pid, parts[w].shard(RouteMap::shardOf(ps.prefixOf(pid))));
-            } else {
-              label(i - nOwn);
-            }
-          }
-        });
-        prof.mark("unicast + labels (pool)");
-        mergeParts(db.unicastRoutes, parts, pool);
-        prof.mark("unicast merge");
-      }
+      fillRoutes(dbs.size(), label);
       for (const auto& [prefix, nhs] : staticUnicastRoutes_) {
         if (db.unicastRoutes.count(prefix) || !ownsStatic(prefix)) continue;
         RibUnicastEntry se;
@@ -1465,29 +1540,17 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       }
       labelsDone = true;
     } else if (!hasKsp && nOwn >= kParallelMin && pool.size() > 1) {
-      // contiguous pid ranges per worker into per-worker maps, then spliced;
       // the node-label candidates (shard 0) are computed in the same pass
-      std::vector<RouteMap> parts(pool.size());
       if (shardRank_ == 0) {
         labelPrepare();
         labPre = true;
       }
       const size_t nLab = labOff.back();
-      pool.parallelFor(nOwn + nLab, [&](size_t w, size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) {
-          if (i >= nOwn) {
-            const size_t f = i - nOwn;
-            const size_t a = static_cast<size_t>(std::upper_bound(labOff.begin(), labOff.end(), f) - labOff.begin()) - 1;
-            labelCompute(labAreas[a], f - labOff[a]);
-            continue;
-          }
-          const uint32_t pid = pidLo + static_cast<uint32_t>(i);
-          if (ps.prefixLive(pid)) one(pid, parts[w].shard(RouteMap::shardOf(ps.prefixOf(pid))));
-        }
-      });
-      prof.mark("unicast + labels (pool)");
-      mergeParts(db.unicastRoutes, parts, pool);
-      prof.mark("unicast merge");
+      auto label = [&](size_t f) {
+        const size_t a = static_cast<size_t>(std::upper_bound(labOff.begin(), labOff.end(), f) - labOff.begin()) - 1;
+        labelCompute(labAreas[a], f - labOff[a]);
+      };
+      fillRoutes(nLab, label);
     } else {
       for (uint32_t pid = pidLo; pid < pidHi; ++pid) {
         if (!ps.prefixLive(pid)) continue;

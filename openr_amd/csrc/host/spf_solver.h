@@ -371,6 +371,24 @@ class SpfSolver {
   size_t dDiffCap_{0};
   bool havePrev_{false}, lastDiffed_{false};
   uint64_t selGen_{0}, prevLayout_{0}, staticEpoch_{0};
+  // the route build's flat slot array (two-pass fill, buildRouteDbImpl):
+  // uninitialised storage kept across builds (no page faults per build) and
+  // per-(worker, output shard) slot lists
+  struct RouteSlots {
+    struct Free {
+      void operator()(void* p) const { ::operator delete(p); }
+    };
+    std::unique_ptr<void, Free> mem;
+    size_t cap{0};
+    std::vector<std::vector<uint32_t>> lists;
+    void reserve(size_t n) {
+      if (n <= cap) return;
+      mem.reset(::operator new(n * sizeof(RibUnicastEntry)));
+      cap = n;
+    }
+    RibUnicastEntry* at(size_t i) { return static_cast<RibUnicastEntry*>(mem.get()) + i; }
+  };
+  RouteSlots routeSlots_;
   // inputs of the last MPLS route build (every area's LinkState stamp, me,
   // static routes): a delta rebuild with the same inputs keeps the routes
   std::vector<std::pair<const LinkState*, uint64_t>> mplsInputs(const AreaLinkStates& als) const;
