@@ -1404,6 +1404,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       slots.reserve(nOwn);
       slots.lists.resize(W * kS);
       for (auto& l : slots.lists) l.clear();
+      // a slot is listed right after it is constructed: on an exception the
+      // listed slots are exactly the live ones, destroyed before rethrowing
+      auto dropListed = [&] {
+        for (auto& l : slots.lists) {
+          for (uint32_t i : l) slots.at(i)->~RibUnicastEntry();
+          l.clear();
+        }
+      };
+      try {
       pool.parallelFor(nOwn + nExtra, [&](size_t w, size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) {
           if (i >= nOwn) {
@@ -1426,6 +1435,10 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           slots.lists[w * kS + RouteMap::shardOf(slot->prefix)].push_back(static_cast<uint32_t>(i));
         }
       });
+      } catch (...) {
+        dropListed();
+        throw;
+      }
       prof.mark("unicast + labels (pool)");
       std::atomic<bool> dup{false};
       pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {

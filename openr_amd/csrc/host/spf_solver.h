@@ -372,8 +372,9 @@ class SpfSolver {
   bool havePrev_{false}, lastDiffed_{false};
   uint64_t selGen_{0}, prevLayout_{0}, staticEpoch_{0};
   // the route build's flat slot array (two-pass fill, buildRouteDbImpl):
-  // uninitialised storage kept across builds (no page faults per build) and
-  // per-(worker, output shard) slot lists
+  // uninitialised storage kept across builds (no page faults per build; C5:
+  // 1M slots of ~100 B) and per-(worker, output shard) lists of the slots
+  // holding a constructed route (empty between builds)
   struct RouteSlots {
     struct Free {
       void operator()(void* p) const { ::operator delete(p); }
