@@ -51,7 +51,10 @@ def parse():
     p.add_argument("--scaling", choices=("whatif", "strong", "weak"), default="whatif")
     p.add_argument("--topologies", type=int, default=32,
                    help="what-if variants per step (--scaling whatif)")
-    p.add_argument("--lanes", type=int, default=4,
+    # 2 lanes: 22.9-23.0 ms per step against 23.0-23.1 at 3 and 23.6-23.8 at 4
+    # on the round-5 kernels (profiles/r05/zh_lanes_ab.txt; 4 was best with the
+    # round-3 kernels): two sweeps in flight already fill the CUs
+    p.add_argument("--lanes", type=int, default=2,
                    help="stream lanes per rank: a rank's what-if variants are dealt over this many "
                         "contexts (own HIP stream each) so their sweeps overlap on the GPU")
     p.add_argument("--cpu-sample", type=int, default=256, help="oracle sources per thread config")
