@@ -7,6 +7,6 @@ set -e
 REPS=${REPS:-2}
 for r in $(seq 1 "$REPS"); do
   for V in "$@"; do
-    echo "[$V] step: $(env $V T=32 LANES=4 timeout -k 10 300 python tools/lanes_probe.py) | isolated: $(env $V timeout -k 10 120 python tools/quick_bench.py)"
+    echo "[$V] step: $(env $V T=32 LANES=${LANES:-2} timeout -k 10 300 python tools/lanes_probe.py) | isolated: $(env $V timeout -k 10 120 python tools/quick_bench.py)"
   done
 done
