@@ -65,8 +65,8 @@ def parse():
                    help="rehearsal of the N-rank path on a one-GPU box: every rank drives GPU 0 "
                         "and the ranks sync over gloo (never used for reported numbers)")
     p.add_argument("--no-route-db", action="store_true")
-    p.add_argument("--legs", default="c1,c3,c4,c5",
-                   help="extra BASELINE configs reported under 'legs' (c1,c3,c4,c5; '' for none)")
+    p.add_argument("--legs", default="c1,c2w,c3,c4,c5",
+                   help="extra BASELINE configs reported under 'legs' (c1,c2w,c3,c4,c5; '' for none)")
     return p.parse_args()
 
 
@@ -211,6 +211,17 @@ def main():
             if not np.array_equal(dist_row[ids], np.abs(rr - rr[s_]) + np.abs(cc - cc[s_])):
                 raise SystemExit(f"bench: wrong distances for source {s_}")
 
+    # N ranks: rank r runs block r of the C3 prefix-sharded route build and
+    # of the C4 what-if job / KSP2 batch on its own GPU (bench_legs.run_ranks);
+    # rank 0 reports the max over ranks. Untimed by the step's clock.
+    rank_legs = None
+    if world > 1 and args.legs:
+        import bench_legs
+        mine = bench_legs.run_ranks(args.legs.split(","), hip, rank, world)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        rank_legs = bench_legs.merge_ranks(gathered, world)
+
     if rank != 0:
         barrier()
         return
@@ -279,7 +290,10 @@ def main():
             flips[0] ^= 1  # topology change: memo cleared, mirror patched
             db.adjacencies[0].metric = 1 + flips[0]
             ls.update_adjacency_database(db)
-            return solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3
+            return profiled_build(solver._impl, "1", als._impl, ps._impl)
+
+        def warm():
+            return profiled_build(solver._impl, "1", als._impl, ps._impl)
 
         # two untimed topology changes first: the first ones after the initial
         # build grow one-time buffers (mirror patch staging, set caches) and
@@ -287,14 +301,18 @@ def main():
         cold()
         cold()
         st0 = cgroup_cpu_stat()
-        cold_ms = [cold() for _ in range(7)]
+        cold_runs = [cold() for _ in range(7)]
         st1 = cgroup_cpu_stat()
-        warm_ms = [solver._impl.time_build_route_db("1", als._impl, ps._impl)[0] * 1e3 for _ in range(7)]
+        warm_runs = [warm() for _ in range(7)]
         st2 = cgroup_cpu_stat()
+        cold_ms = [r["ms"] for r in cold_runs]
+        warm_ms = [r["ms"] for r in warm_runs]
         out["build_route_db_ms"] = round(statistics.median(cold_ms), 3)
         out["build_route_db_warm_ms"] = round(statistics.median(warm_ms), 3)
         out["build_route_db_runs"] = {"cold_ms": spread(cold_ms), "warm_ms": spread(warm_ms),
                                       "cold_settle": "2 untimed topology-change builds before the 7 timed ones",
+                                      "phases": {"cold": phase_summary(cold_runs),
+                                                 "warm": phase_summary(warm_runs)},
                                       "host_pool_threads": hip.module.host_threads(),
                                       "cgroup_throttling": {"cold": throttle_delta(st0, st1),
                                                             "warm": throttle_delta(st1, st2)}}
@@ -306,6 +324,8 @@ def main():
     if world == 1 and args.legs:
         import bench_legs
         out["legs"] = bench_legs.run(args.legs.split(","), hip, not args.no_cpu_baseline)
+    elif rank_legs is not None:
+        out["legs"] = rank_legs
 
     print(json.dumps(out), flush=True)
     barrier()
@@ -343,6 +363,37 @@ def pmc_traffic():
     if len(seen) != len(SWEEP_KERNELS):
         return None, None
     return round(total), os.path.relpath(PMC_PROFILE, ROOT) + ": " + " + ".join(seen)
+
+
+def profiled_build(solver_impl, me, als_impl, ps_impl):
+    """One buildRouteDb with its phase times (the phases ORH_ROUTE_PROF
+    prints), minor / major page faults and RSS growth across the call."""
+    sec, n, phases, minflt, majflt, drss = solver_impl.time_build_route_db_phases(me, als_impl, ps_impl)
+    return {"ms": sec * 1e3, "routes": n, "phases": phases, "minflt": minflt, "majflt": majflt,
+            "rss_delta": drss}
+
+
+def phase_summary(runs):
+    """Per phase the median ms over the runs (a phase named twice in one build
+    is summed), the phases' median total, and the median page faults / RSS
+    growth per build."""
+    names, per = [], []
+    for r in runs:
+        d = {}
+        for name, ms in r["phases"]:
+            name = name.strip()
+            if name not in names:
+                names.append(name)
+            d[name] = d.get(name, 0.0) + ms
+        per.append(d)
+    med = {n: round(statistics.median(d.get(n, 0.0) for d in per), 3) for n in names}
+    return {"phases_ms": med,
+            "unaccounted_ms": round(statistics.median(
+                r["ms"] - sum(ms for name, ms in r["phases"] if not name.strip().startswith("select:"))
+                for r in runs), 3),
+            "minor_faults": int(statistics.median(r["minflt"] for r in runs)),
+            "major_faults": int(statistics.median(r["majflt"] for r in runs)),
+            "rss_delta_mb": round(statistics.median(r["rss_delta"] for r in runs) / 2**20, 2)}
 
 
 def cgroup_cpu_quota():

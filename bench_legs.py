@@ -6,6 +6,7 @@ LinkState / SpfSolver with its containers, on a bounded sample of the same
 work, stating the sample.
 
   c1  createGrid(10): buildRouteDb("1") ms (reference BM_DecisionGrid shape)
+  c2w the 100x100 grid with integer metrics 1..64: all-sources SPF sweep
   c3  Clos (~2.5k nodes, full spine mesh): all-sources SPF sweep + 100k-prefix
       buildRouteDb, default and best-route selection
   c4  50k-node WAN: batched single-link what-if SPFs and KSP2 (src, dst) pairs
@@ -32,12 +33,15 @@ def _route_ms(solver, me, als, ps, reps):
 
 
 def _route_runs(solver, me, als, ps, reps):
-    """Every run's ms with their spread, and the cgroup's CFS throttling over
-    them (bench.cgroup_cpu_stat)."""
+    """Every run's ms with their spread, the phase times / page faults of the
+    builds (bench.profiled_build) and the cgroup's CFS throttling over them
+    (bench.cgroup_cpu_stat)."""
     import bench
     st0 = bench.cgroup_cpu_stat()
-    ms = [solver._impl.time_build_route_db(me, als._impl, ps._impl)[0] * 1e3 for _ in range(reps)]
-    return ms, {"ms": bench.spread(ms), "cgroup_throttling": bench.throttle_delta(st0, bench.cgroup_cpu_stat())}
+    runs = [bench.profiled_build(solver._impl, me, als._impl, ps._impl) for _ in range(reps)]
+    ms = [r["ms"] for r in runs]
+    return ms, {"ms": bench.spread(ms), "phases": bench.phase_summary(runs),
+                "cgroup_throttling": bench.throttle_delta(st0, bench.cgroup_cpu_stat())}
 
 
 def _select_roofline(solver, me, als, ps):
@@ -64,6 +68,54 @@ def leg_c1(hip, cpu):
         o = _oracle()
         als_o, ps_o = load_topology(o, adj, pfx)
         out["cpu_build_route_db_ms"] = round(_route_ms(o.spf_solver("1", True), "1", als_o, ps_o, 9), 4)
+    return out
+
+
+def leg_c2w(hip, cpu, reps=10):
+    """C2 with integer metrics (workloads.c2_weighted_grid: the 100x100 grid,
+    a seeded metric in [1, 64] per link): all 10,000 sources swept, dist +
+    first-hop rows written to HBM (runSpf semantics, LinkState.cpp:808-882,
+    getMetricFromNode :851-852). Wall time of back-to-back sweeps, the HIP-event
+    device time of one sweep alone, and its roofline by the same algorithmic
+    bytes per source as C2."""
+    from openr_amd.facade import load_topology
+    from openr_amd.types import K_TESTING_AREA as A
+    from openr_amd.workloads import C2W_MAX_METRIC, c2_weighted_grid
+    adj, pfx = c2_weighted_grid()
+    als, _ = load_topology(hip, adj, pfx)
+    names = [db.thisNodeName for db in adj]
+    sw = als[A]._impl.sweep(names, True)
+    sw.run()
+    sw.sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sw.run()
+    sw.sync()
+    dt = (time.perf_counter() - t0) / reps
+    dev = []
+    for _ in range(5):
+        sw.run()
+        dev.append(sw.last_ms())
+    kms = statistics.median(dev)
+    N, E, W = sw.nodes, sw.edges, sw.words
+    b_src = 4 * (N + 1) + 8 * E + N * (4 + 4 * W)
+    gbs = b_src * len(names) / (kms * 1e-3) / 1e9
+    info = sw.info()
+    out = {"workload": f"C2w {N}-node grid, link metrics uniform in [1, {C2W_MAX_METRIC}] (E={E})",
+           "sweep_spf_sources_per_s": round(len(names) / dt, 1),
+           "sweep_ms": round(dt * 1e3, 3),
+           "kernel_ms": round(kms, 3),
+           "plan": {"variant": info["variant"], "rows": info["rows"]},
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                        "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_source": b_src,
+                        "sources_per_launch": len(names)}}
+    if cpu:
+        o = _oracle()
+        als_o, _ = load_topology(o, adj, pfx)
+        sample = names[::max(1, len(names) // 128)]
+        sec, _ = als_o[A]._impl.time_spf_sources(sample, 1)
+        out["cpu_sweep_spf_sources_per_s"] = round(len(sample) / sec, 2)
+        out["cpu_sample"] = f"{len(sample)} runSpf calls (evenly spaced sources), 1 thread"
     return out
 
 
@@ -115,6 +167,7 @@ def leg_c3(hip, cpu):
         "ShardedRouteBuilder over 8 contexts: max_ms = slowest shard built alone (the per-GPU time on "
         "8 GPUs); merged_ms = all 8 shards concurrently on this one GPU and its host pool, spliced into "
         "one DecisionRouteDb")
+    sb.release_prefix_mirrors(ps._impl)  # the 7 extra contexts' copies of the prefix mirror
     del sb, ras
     if cpu:
         o = _oracle()
@@ -271,7 +324,9 @@ def leg_c5(hip, cpu):
            "load_s": round(load_s, 2),
            "load_note": "adjacency + 1M prefix advertisements ingested from wire records (updateAdjacencyDatabase / "
                         "updatePrefix in order); the generator's Python-to-wire conversion is not timed",
-           "build_route_db_ms": round(_route_ms(solver, "me", als, ps, 3), 2)}
+           "build_route_db_ms": None}
+    c5_ms, out["build_route_db_runs"] = _route_runs(solver, "me", als, ps, 5)
+    out["build_route_db_ms"] = round(statistics.median(c5_ms), 2)
     out.update(_select_roofline(solver, "me", als, ps))
     policy = RibPolicy([RibPolicyStatement("ucmp", None, [C5_TAG], RibRouteActionWeight(
         0, {"A": 1, "B": 2, "C": 3, "D": 4}, {}))], 3600)
@@ -370,7 +425,7 @@ def leg_c5(hip, cpu):
     return out
 
 
-LEGS = {"c1": leg_c1, "c3": leg_c3, "c4": leg_c4, "c5": leg_c5}
+LEGS = {"c1": leg_c1, "c2w": leg_c2w, "c3": leg_c3, "c4": leg_c4, "c5": leg_c5}
 
 
 def run(names, hip, cpu):
@@ -385,4 +440,172 @@ def run(names, hip, cpu):
         except Exception as e:  # a failed leg is reported, not hidden
             out[n] = {"error": f"{type(e).__name__}: {e}"}
         out[n]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# N-rank legs (bench.py --gpus N, N > 1): one process per GPU, rank r runs
+# block r of configs[2] (C3 prefix shard) and configs[3] (C4 what-if + KSP2
+# blocks) on its own device; bench.py reports the max over ranks. The blocks
+# are the library's own cuts: SpfSolver::setPrefixShard (ShardedRouteBuilder),
+# equalWorkCuts of the sources by request / pair count (MultiDeviceWhatIf,
+# MultiDeviceKthPaths). Every block is independent given the topology: no
+# data-path collective.
+# ---------------------------------------------------------------------------
+def c3_rank_state(hip):
+    from openr_amd.facade import load_topology
+    from openr_amd.workloads import c3_fabric
+    adj, pfx = c3_fabric()
+    als, ps = load_topology(hip, adj, pfx)
+    return als, ps
+
+
+def rank_c3(hip, rank, world, state=None, reps=7, digest=False):
+    """Prefix block `rank` of `world` of the C3 100k-prefix buildRouteDb
+    (Decision.cpp:615-792) on this process's device: the shard's SPF, route
+    selection and materialisation (shard 0 adds the MPLS routes)."""
+    als, ps = state or c3_rank_state(hip)
+    me = "2-0-0"
+    solver = hip.spf_solver(me, True)
+    solver._impl.set_prefix_shard(rank, world)
+    solver._impl.time_build_route_db(me, als._impl, ps._impl)  # warm: mirrors, rows, buffers
+    ms, runs = _route_runs(solver, me, als, ps, reps)
+    out = {"build_route_db_shard_ms": round(statistics.median(ms), 3), "runs": runs}
+    if digest:
+        out["digest"] = solver._impl.build_route_db_digest(me, als._impl, ps._impl)
+    return out
+
+
+def c4_rank_state(hip):
+    from openr_amd.facade import load_topology
+    from openr_amd.types import K_TESTING_AREA as A
+    from openr_amd.workloads import C4_KSP2_PAIRS, c4_ksp2_pairs, c4_wan, c4_what_if_job
+    adj, _ = c4_wan()
+    als, _ = load_topology(hip, adj, [])
+    ls = als[A]._impl
+    names = ls.node_names()
+    srcs, idx, sets = c4_what_if_job([lid for lid, _ in ls.link_ids()], names)
+    return als, ls, srcs, idx, sets, c4_ksp2_pairs(names, C4_KSP2_PAIRS)
+
+
+def c4_what_if_block(srcs, idx, sets, rank, world):
+    """Block `rank` of the C4 what-if job cut as MultiDeviceWhatIf cuts it:
+    contiguous source blocks of equal request counts. Returns (the caller's
+    request indices, the block's sources, per request its source index in the
+    block, ignore sets)."""
+    from openr_amd.sharding import weighted_blocks
+    w = [0.0] * len(srcs)
+    for i in idx:
+        w[i] += 1.0
+    lo, hi = weighted_blocks(w, world)[rank]
+    reqs = [i for i, s in enumerate(idx) if lo <= s < hi]
+    return reqs, srcs[lo:hi], [idx[i] - lo for i in reqs], [sets[i] for i in reqs]
+
+
+def c4_ksp2_block(pairs, rank, world):
+    """Block `rank` of the KSP2 pairs cut as MultiDeviceKthPaths cuts it: the
+    pairs of one source together, sources in first-appearance order cut into
+    blocks of equal pair counts. Returns the caller's pair indices."""
+    from openr_amd.sharding import weighted_blocks
+    order, by_src = [], {}
+    for i, (s, _) in enumerate(pairs):
+        if s not in by_src:
+            by_src[s] = []
+            order.append(s)
+        by_src[s].append(i)
+    lo, hi = weighted_blocks([float(len(by_src[s])) for s in order], world)[rank]
+    return [i for s in order[lo:hi] for i in by_src[s]]
+
+
+def rank_c4(hip, rank, world, state=None, reps=3, digest=False):
+    """Block `rank` of `world` of the C4 what-if job (copy-on-write, the
+    bench's mode) and of the 1,024-pair KSP2 batch (prefetchKthPaths, cold)
+    on this process's device."""
+    from openr_amd.workloads import C4_WHATIF_CHUNK
+    als, ls, srcs, idx, sets, pairs = state or c4_rank_state(hip)
+    reqs, bsrcs, bidx, bsets = c4_what_if_block(srcs, idx, sets, rank, world)
+    out = {"what_if_requests": len(reqs), "what_if_sources": len(bsrcs)}
+    if reqs:
+        # the single job's chunking scaled to the block (four chunks of the
+        # block: the two row buffers stay 1/world of the single job's)
+        chunk = min(C4_WHATIF_CHUNK, max(1024, -(-len(reqs) // 4)))
+        job = ls.what_if_batch(bsrcs, bidx, bsets, chunk, share_base=True)
+        if digest:
+            job.set_digests()
+        job.run()
+        job.sync()
+        walls = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            job.run()
+            job.sync()
+            walls.append(time.perf_counter() - t0)
+        out["what_if_block_ms"] = round(statistics.median(walls) * 1e3, 3)
+        if digest:
+            out["what_if_reqs"] = reqs
+            out["what_if_info"] = job.info()
+            out["what_if_digests"] = job.digests()
+        job.release()
+        del job
+    else:
+        out["what_if_block_ms"] = 0.0
+    kp = c4_ksp2_block(pairs, rank, world)
+    out["ksp2_pairs"] = len(kp)
+    if kp:
+        bp = [pairs[i] for i in kp]
+        walls = ls.time_prefetch_kth_paths(bp, reps)
+        out["ksp2_block_ms"] = round(statistics.median(walls) * 1e3, 3)
+        if digest:
+            out["ksp2_idx"] = kp
+            out["ksp2_paths"] = [(ls.get_kth_path_ids(s, d, 1), ls.get_kth_path_ids(s, d, 2)) for s, d in bp]
+    else:
+        out["ksp2_block_ms"] = 0.0
+    return out
+
+
+def run_ranks(names, hip, rank, world):
+    """This rank's block of every N-rank leg (bench.py gathers them)."""
+    out = {}
+    for n in names:
+        n = n.strip()
+        t0 = time.perf_counter()
+        try:
+            if n == "c3":
+                out[n] = rank_c3(hip, rank, world)
+            elif n == "c4":
+                out[n] = rank_c4(hip, rank, world)
+            else:
+                continue
+        except Exception as e:  # a failed leg is reported, not hidden
+            out[n] = {"error": f"{type(e).__name__}: {e}"}
+        out[n]["leg_wall_s"] = round(time.perf_counter() - t0, 1)
+    return out
+
+
+def merge_ranks(per_rank, world):
+    """Rank 0's report of the N-rank legs: per leg the max over ranks (the
+    per-GPU time of an N-GPU node) and every rank's own numbers."""
+    out = {}
+    for leg in sorted({k for r in per_rank for k in r}):
+        rows = [r.get(leg, {}) for r in per_rank]
+        err = [r["error"] for r in rows if "error" in r]
+        if err:
+            out[leg] = {"error": err[0]}
+            continue
+        if leg == "c3":
+            ms = [r["build_route_db_shard_ms"] for r in rows]
+            out[leg] = {"workload": f"C3 100k-prefix buildRouteDb, prefix block r of {world} on GPU r",
+                        "build_route_db_max_ms": max(ms), "build_route_db_ms_by_rank": ms}
+        elif leg == "c4":
+            wi = [r["what_if_block_ms"] for r in rows]
+            kp = [r["ksp2_block_ms"] for r in rows]
+            n_req = sum(r["what_if_requests"] for r in rows)
+            n_kp = sum(r["ksp2_pairs"] for r in rows)
+            out[leg] = {"workload": f"C4 what-if job ({n_req} requests) and KSP2 ({n_kp} pairs), "
+                                    f"source block r of {world} on GPU r",
+                        "what_if_max_ms": max(wi), "what_if_ms_by_rank": wi,
+                        "what_if_spfs_per_s": round(n_req / (max(wi) * 1e-3), 1) if max(wi) else None,
+                        "ksp2_max_ms": max(kp), "ksp2_ms_by_rank": kp,
+                        "ksp2_pairs_per_s": round(n_kp / (max(kp) * 1e-3), 1) if max(kp) else None}
+        out[leg]["leg_wall_s_by_rank"] = [r.get("leg_wall_s") for r in rows]
     return out

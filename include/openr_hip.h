@@ -158,6 +158,8 @@ int orh_set_repair_mode(orh_ctx* ctx, int mode);
 #define ORH_VARIANT_BFS_NH 10   /* BFS with fused first hops, one workgroup per source */
 #define ORH_VARIANT_REPAIR 11   /* ignore-set batch repaired from its sources' plain rows
                                    (batch_sources = distinct sources searched) */
+#define ORH_VARIANT_LDS_NH 12   /* general metrics, {dist, first hops} labels in LDS,
+                                   first hops fused, one workgroup per source */
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */

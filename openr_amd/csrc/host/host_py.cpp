@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <sys/resource.h>
+#include <unistd.h>
 #include <cstring>
 
 #include "parallel.h"
@@ -1004,6 +1006,7 @@ PYBIND11_MODULE(_openr_host, m) {
              for (size_t r = 0; r < b.shards(); ++r) shardMs.push_back(b.lastShardMs(r));
              return py::make_tuple(sec, n, shardMs, b.lastMergeMs());
            })
+      .def("release_prefix_mirrors", &ShardedRouteBuilder::releasePrefixMirrors, py::arg("prefix_state"))
       .def("time_build_shard",  // shard r alone: (seconds, routes)
            [](ShardedRouteBuilder& b, size_t r, const std::string& me, const PrefixState& ps) {
              py::gil_scoped_release nogil;
@@ -1346,6 +1349,32 @@ PYBIND11_MODULE(_openr_host, m) {
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
              const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
              return std::make_pair(sec, n);
+           })
+      .def("time_build_route_db_phases",  // (seconds, routes, [(phase, ms)], minor faults, major faults, RSS delta bytes)
+           [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps) {
+             auto rss = [] {
+               long pages = 0, resident = 0;
+               if (FILE* f = std::fopen("/proc/self/statm", "r")) {
+                 if (std::fscanf(f, "%ld %ld", &pages, &resident) != 2) resident = 0;
+                 std::fclose(f);
+               }
+               return static_cast<int64_t>(resident) * sysconf(_SC_PAGESIZE);
+             };
+             RoutePhaseCapture cap;
+             struct rusage r0{}, r1{};
+             const int64_t m0 = rss();
+             getrusage(RUSAGE_SELF, &r0);
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.buildRouteDb(me, als.m, ps);
+             const double sec =
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             getrusage(RUSAGE_SELF, &r1);
+             const int64_t m1 = rss();
+             const size_t n = db ? db->unicastRoutes.size() + db->mplsRoutes.size() : 0;
+             py::list ph;
+             for (const auto& [name, ms] : cap.phases) ph.append(py::make_tuple(std::string(name), ms));
+             return py::make_tuple(sec, n, ph, static_cast<int64_t>(r1.ru_minflt - r0.ru_minflt),
+                                   static_cast<int64_t>(r1.ru_majflt - r0.ru_majflt), m1 - m0);
            })
       .def("time_build_route_db_with_policy",  // Decision::rebuildRoutes: build + RibPolicy
            [](SpfSolver& s, const std::string& me, const AreaMap& als, const PrefixState& ps,

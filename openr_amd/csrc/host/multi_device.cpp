@@ -462,6 +462,14 @@ ShardedRouteBuilder::ShardedRouteBuilder(const ReplicatedAreaLinkStates& areas, 
   }
 }
 
+size_t ShardedRouteBuilder::releasePrefixMirrors(PrefixState& ps) const {
+  size_t n = 0;
+  orh_ctx* keep = defaultContext();
+  for (size_t r = 0; r < areas_.replicas(); ++r)
+    if (areas_.context(r) != keep && ps.dropDeviceMirror(areas_.context(r))) ++n;
+  return n;
+}
+
 void ShardedRouteBuilder::updateStaticUnicastRoutes(
     const std::vector<std::pair<Cidr, std::vector<NextHopThrift>>>& upd, const std::vector<Cidr>& del) {
   for (auto& s : solvers_) s->updateStaticUnicastRoutes(upd, del);

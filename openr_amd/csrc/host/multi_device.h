@@ -123,7 +123,12 @@ class MultiDeviceWhatIf {
   std::pair<size_t, size_t> sourceBlock(size_t r) const { return {blocks_.at(r).lo, blocks_.at(r).hi}; }
   size_t blockRequests(size_t r) const { return blocks_.at(r).reqs.size(); }
   size_t requests() const { return total_; }
-  double lastMs(size_t r) const { return blocks_.at(r).job->lastMs(); }
+  // device ms of block r's last run; 0 for a block with no requests (no job)
+  // or one released since
+  double lastMs(size_t r) const {
+    const Block& b = blocks_.at(r);
+    return b.job ? b.job->lastMs() : 0.0;
+  }
   void info(uint32_t* out) const;     // [requests()] in the caller's order
   void digests(uint64_t* out) const;  // [requests()] (setDigests(true) before the run)
 
@@ -221,6 +226,9 @@ class ShardedRouteBuilder {
   // wall times of the last buildRouteDb: each shard's build (its thread), the merge
   double lastShardMs(size_t r) const { return shardMs_.at(r); }
   double lastMergeMs() const { return mergeMs_; }
+  // drops ps's device mirrors on the shards' contexts (all but the default
+  // context's); returns how many were freed
+  size_t releasePrefixMirrors(PrefixState& ps) const;
 
  private:
   const ReplicatedAreaLinkStates& areas_;

@@ -191,6 +191,15 @@ void PrefixState::touch(const Cidr& prefix, bool erased) {
   }
   for (auto& m : mirrors_) {  // every device mirror re-uploads it at its next sync
     if (m->full) continue;
+    // a mirror that has not synced for a long time (its context no longer
+    // builds) stops collecting: past half the prefix ids it reloads whole at
+    // its next sync instead, so its dirty list stays bounded
+    if (m->dirty.size() > cidrOf_.size() / 2 + 1024) {
+      m->full = true;
+      std::vector<uint32_t>().swap(m->dirty);
+      std::vector<uint8_t>().swap(m->isDirty);
+      continue;
+    }
     if (m->isDirty.size() <= pid) m->isDirty.resize(cidrOf_.size(), 0);
     if (!m->isDirty[pid]) {
       m->isDirty[pid] = 1;
@@ -240,6 +249,17 @@ void PrefixState::buildRecords(const std::vector<uint32_t>* ids, std::vector<uin
     const AdvRef* a = advPool_.data() + run_[pid].first;
     for (uint32_t k = 0; k < ptr[i + 1] - ptr[i]; ++k) recs[ptr[i] + k] = advRecord(*a[k].key, **a[k].entry);
   });
+}
+
+bool PrefixState::dropDeviceMirror(orh_ctx* ctx) {
+  std::lock_guard<std::mutex> lock(syncMu_);
+  for (auto it = mirrors_.begin(); it != mirrors_.end(); ++it) {
+    if ((*it)->ctx != ctx) continue;
+    if ((*it)->dev) orh_prefix_destroy((*it)->dev);
+    mirrors_.erase(it);
+    return true;
+  }
+  return false;
 }
 
 orh_prefix_set* PrefixState::syncDevice(orh_ctx* ctx) const {

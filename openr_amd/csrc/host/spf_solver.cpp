@@ -25,18 +25,30 @@ namespace {
 // calling thread (the pool's hand-off costs more than it saves)
 constexpr size_t kParallelMin = 2048;
 
-// ORH_ROUTE_PROF=1: phase times of buildRouteDb on stderr
+// the phase sink of this thread's RoutePhaseCapture (null: none)
+thread_local std::vector<std::pair<const char*, double>>* tlPhases = nullptr;
+
+// phase times of buildRouteDb: on stderr with ORH_ROUTE_PROF=1, and into the
+// calling thread's RoutePhaseCapture when one is open
 struct RouteProf {
   bool on = std::getenv("ORH_ROUTE_PROF") != nullptr;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void mark(const char* what) {
-    if (!on) return;
+    if (!on && !tlPhases) return;
     const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "route-prof %-16s %8.3f ms\n", what,
-                 std::chrono::duration<double, std::milli>(now - t).count());
+    const double ms = std::chrono::duration<double, std::milli>(now - t).count();
+    if (tlPhases) tlPhases->emplace_back(what, ms);
+    if (on) std::fprintf(stderr, "route-prof %-16s %8.3f ms\n", what, ms);
     t = now;
   }
 };
+
+}  // namespace
+
+RoutePhaseCapture::RoutePhaseCapture() : prev_(tlPhases) { tlPhases = &phases; }
+RoutePhaseCapture::~RoutePhaseCapture() { tlPhases = prev_; }
+
+namespace {
 
 MplsAction mpls(int32_t code, std::optional<int32_t> swap = std::nullopt,
                 std::optional<std::vector<int32_t>> push = std::nullopt) {
@@ -828,11 +840,21 @@ bool SpfSolver::selectOnDevice(const std::string& me, const AreaLinkStates& als,
     const auto* b = static_cast<const unsigned char*>(p);
     for (size_t i = 0; i < n; ++i) layout = (layout ^ b[i]) * 1099511628211ull;
   };
+  // the insertion sequence too (a set iterates in the order its nexthops went
+  // in): areas in AreaLinkStates order, my links in LinkSet order - a rehash
+  // of my LinkSet can reorder the links with the templates unchanged
+  for (uint32_t a : areaIter_) mix(&a, sizeof a);
   for (const AreaWork& w : areaWork_) {
     mix(&w.words, sizeof w.words);
     mix(&w.wordOff, sizeof w.wordOff);
     const void* ls = w.ls;
     mix(&ls, sizeof ls);
+    const uint32_t nl = static_cast<uint32_t>(w.linkOrder.size());
+    mix(&nl, sizeof nl);
+    for (const auto& [b, j] : w.linkOrder) {
+      mix(&b, sizeof b);
+      mix(&j, sizeof j);
+    }
     for (const auto* tm : {&w.tmpl6, &w.tmpl4}) {
       const uint32_t nb = static_cast<uint32_t>(tm->size());
       mix(&nb, sizeof nb);
@@ -1441,6 +1463,12 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       }
       prof.mark("unicast + labels (pool)");
       std::atomic<bool> dup{false};
+      // per list, the slots already moved out and destroyed (a list is
+      // consumed in order by the one thread that owns its shard): if the
+      // merge throws (bad_alloc in reserve / emplace), exactly the rest are
+      // destroyed before rethrowing
+      std::vector<uint32_t> done(W * kS, 0u);
+      try {
       pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
         for (size_t sh = b; sh < e; ++sh) {
           size_t n = 0;
@@ -1453,9 +1481,19 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
               Cidr k = r->prefix;
               if (!dst.emplace(std::move(k), std::move(*r)).second) dup = true;
               r->~RibUnicastEntry();
+              ++done[w * kS + sh];
             }
         }
       });
+      } catch (...) {
+        for (size_t l = 0; l < slots.lists.size(); ++l) {
+          auto& list = slots.lists[l];
+          for (size_t q = done[l]; q < list.size(); ++q) slots.at(list[q])->~RibUnicastEntry();
+          list.clear();
+        }
+        throw;
+      }
+      for (auto& l : slots.lists) l.clear();
       if (dup) throw std::logic_error("duplicate unicast route");
       prof.mark("unicast merge");
     };

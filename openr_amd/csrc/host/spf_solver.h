@@ -61,7 +61,14 @@ class PrefixState {
   // ---- device mirror (used by SpfSolver) ----
   // brings the mirror on `ctx` up to date (one mirror per context: a route
   // build sharded over devices keeps one per device); returns it
+  // The PrefixState must not be mutated while a build reads it (the Python
+  // bindings release the GIL during builds: the caller serialises updates).
   orh_prefix_set* syncDevice(orh_ctx* ctx) const;
+  // frees the mirror on `ctx` (e.g. once a sharded build's extra device
+  // contexts are gone); false when there is none. A later build there
+  // uploads a fresh one
+  bool dropDeviceMirror(orh_ctx* ctx);
+  size_t deviceMirrors() const { return mirrors_.size(); }
   uint32_t numPrefixIds() const { return static_cast<uint32_t>(cidrOf_.size()); }
   const Cidr& prefixOf(uint32_t pid) const { return cidrOf_[pid]; }
   bool prefixLive(uint32_t pid) const { return live_[pid] != 0; }
@@ -170,6 +177,21 @@ struct BestRouteSelectionResult {
       if (na.first == n) return true;
     return false;
   }
+};
+
+// Collects the phase times (name, ms) of the route builds this thread runs
+// while it is alive (the phases ORH_ROUTE_PROF prints; " select: ..." entries
+// subdivide "select (device)"). For measurement: bench.py reports them.
+class RoutePhaseCapture {
+ public:
+  RoutePhaseCapture();
+  ~RoutePhaseCapture();
+  RoutePhaseCapture(const RoutePhaseCapture&) = delete;
+  RoutePhaseCapture& operator=(const RoutePhaseCapture&) = delete;
+  std::vector<std::pair<const char*, double>> phases;
+
+ private:
+  std::vector<std::pair<const char*, double>>* prev_;
 };
 
 class SpfSolver {

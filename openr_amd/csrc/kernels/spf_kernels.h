@@ -109,8 +109,17 @@ enum class SpfVariant {
   kGlobalNh,  // HBM frontier kernel that also derives the first hops (no phase 2)
   kExact,     // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
   kBfsNh,     // uniform metric, few sources: BFS with the first hops fused (no phase 2)
-  kRepair     // ignore-set batch derived from its sources' plain SPFs (whatif_kernels.hip)
+  kRepair,    // ignore-set batch derived from its sources' plain SPFs (whatif_kernels.hip)
+  kLdsNh      // general metrics, labels {dist, first hops} in LDS, first hops fused (no phase 2)
 };
+// spf_lds_nh_kernel: LDS bytes per search (packed: u32 labels, <= 16
+// distinct neighbours per source; else u64 labels)
+size_t lds_nh_bytes(uint32_t n_nodes, bool packed);
+// one workgroup of `block` threads per row; packed: rows whose distances
+// outgrow 16 bits are listed in a.ovf_rows (n_rows + 1 words) and redone
+// with u64 labels. Writes out_dist / out_nh rows [0, n_rows)
+hipError_t launch_spf_lds_nh(SpfArgs a, uint32_t n_rows, uint32_t ell_k, bool packed, uint32_t block,
+                             hipStream_t s);
 // fused BFS + first hops (spf_bfs_nh_kernel): workgroup size, nodes per
 // thread and LDS bytes for N nodes and `words` first-hop words per node;
 // false when the graph does not fit (N > 32768 or LDS)

@@ -1804,6 +1804,249 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// phase 1c''': general metrics, first hops fused, labels in LDS (kLdsNh)
+// ---------------------------------------------------------------------------
+// The asynchronous delta-stepping of spf_global_nh_async_kernel with its
+// {dist, first-hop mask} labels in LDS instead of HBM: a weighted graph that
+// fits (N = 10,000: 40 KB packed) is searched by one workgroup per source
+// with no global atomics and no second phase - the first hops ride along the
+// search as in runSpf itself (LinkState.cpp:857-873): a smaller candidate
+// replaces a label, an equal one ORs its mask in (and re-queues the node so
+// the new bits reach its successors). The fixpoint is order-independent, so
+// the rows are the HBM kernel's bit for bit.
+// kPacked: a u32 label {dist (16 bits, hi) | mask (16 bits, lo)}, for sources
+// with <= 16 distinct neighbours; a candidate distance >= 0xFFFF cannot be
+// held, so the row is appended to a.ovf_rows and written by the u64 form
+// (launch_spf_lds_nh runs it over that list). Else a u64 label {dist (32) |
+// mask (32)} as in the HBM kernel.
+template <int K, bool kPacked>
+__global__ __launch_bounds__(1024) void spf_lds_nh_kernel(SpfArgs a) {
+  typedef typename std::conditional<kPacked, uint32_t, unsigned long long>::type L;
+  constexpr uint32_t kSh = kPacked ? 16u : 32u;
+  constexpr uint32_t kDInf = kPacked ? 0xFFFFu : 0xFFFFFFFFu;  // the unreached distance
+  constexpr L kInfLabel = static_cast<L>(static_cast<L>(kDInf) << kSh);
+  constexpr L kMaskBits = static_cast<L>((static_cast<L>(1) << kSh) - 1u);
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf;
+  const uint32_t N = a.n_nodes;
+  const uint32_t NB = (N + 31) >> 5;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  if (a.row_list && blockIdx.x >= *a.row_count) return;
+  const uint32_t row = a.row_list ? a.row_list[blockIdx.x] : blockIdx.x;
+  constexpr int G = K <= 4 ? 4 : 2;
+  L* lab = reinterpret_cast<L*>(lds);
+  const uint32_t lab_words = kPacked ? ((N + 1u) & ~1u) : 2u * N;  // keeps near 8-byte aligned
+  uint32_t* near = lds + lab_words;
+  uint32_t* far = near + NB;
+  uint32_t* filt = far + NB;
+  uint32_t FW = 1;
+  while (2 * FW <= min(NB, 256u)) FW *= 2;
+  const uint32_t fshift = 32u - (5u + static_cast<uint32_t>(__builtin_ctz(FW)));
+  Src s(a, row);
+  for (uint32_t i = tid; i < N; i += nthr) lab[i] = kInfLabel;
+  for (uint32_t i = tid; i < 2 * NB; i += nthr) near[i] = 0u;
+  if (s.n_ign)
+    for (uint32_t i = tid; i < FW; i += nthr) filt[i] = 0u;
+  if (tid < 2) s_min[tid] = kInf;
+  if (tid == 0) {
+    s_nign = 0u;
+    s_ovf = 0u;
+  }
+  __syncthreads();
+  if (s.n_ign) {
+    for (uint32_t i = tid; i < s.n_ign; i += nthr) {
+      const uint32_t l = s.ign[i];
+      if (l == 0xFFFFFFFFu) continue;
+      atomicAdd(&s_nign, 1u);
+      const uint32_t h = ign_hash(l, fshift);
+      atomicOr(&filt[h >> 5], 1u << (h & 31u));
+    }
+    __syncthreads();
+    s.n_ign = s_nign;  // sorted: the real entries come first
+    s.filt = filt;
+    s.fshift = fshift;
+  }
+  if (tid == 0) {
+    lab[s.node] = static_cast<L>(0);
+    near[s.node >> 5] = 1u << (s.node & 31u);
+    s_work = 1u;
+  }
+  __syncthreads();
+
+  const uint32_t delta = a.delta;
+  uint32_t T = delta;
+  uint32_t mpar = 0;
+  bool ovf = false;
+  for (;;) {
+    uint32_t far_min = kInf;
+    // merge the candidate {nd, cnh} into u's label (cl: as loaded); re-queue
+    // u if the label changed
+    auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, L cl) {
+      if (kPacked && nd >= kDInf) {  // not representable: the u64 form redoes the row
+        ovf = true;
+        return;
+      }
+      for (;;) {
+        const uint32_t cd = static_cast<uint32_t>(cl >> kSh);
+        if (nd > cd) return;
+        const L nl = nd < cd ? static_cast<L>((static_cast<L>(nd) << kSh) | cnh) : static_cast<L>(cl | cnh);
+        if (nl == cl) return;
+        const L old = atomicCAS(&lab[u], cl, nl);
+        if (old == cl) break;
+        cl = old;
+      }
+      const uint32_t bit = 1u << (u & 31u);
+      if (nd < T) {
+        atomicAdd(&s_work, 1u);  // counted before the bit is visible
+        const uint32_t old = atomicOr(&near[u >> 5], bit);
+        atomicAnd(&far[u >> 5], ~bit);
+        if (old & bit) atomicSub(&s_work, 1u);  // already queued
+      } else {
+        atomicOr(&far[u >> 5], bit);
+        far_min = min(far_min, nd);
+      }
+    };
+    uint32_t wi = tid, bits = 0, wbase = 0;
+    for (;;) {
+      uint32_t vs[G];
+      int c = 0;
+      while (c < G) {
+        while (!bits && wi < NB) {
+          bits = __hip_atomic_load(&near[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (bits) bits = atomicExch(&near[wi], 0u);  // at least the bits seen: only we clear
+          wbase = wi * 32;
+          wi += nthr;
+        }
+        if (!bits) break;
+        vs[c++] = wbase + __builtin_ctz(bits);
+        bits &= bits - 1;
+      }
+      if (!bits && wi >= NB) wi = tid;  // words exhausted: rescan them next time
+      if (__builtin_amdgcn_ballot_w64(c > 0) == 0ull) {
+        const uint32_t pending = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&s_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (pending == 0u) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (c > 0) {
+        // the group's records in flight together, then the labels
+        uint2 rec[G][K];
+        uint32_t lk[G][K];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (g < c) load_recs<K>(a, vs[g], rec[g]);
+#pragma unroll
+          for (int j = 0; j < K; ++j) lk[g][j] = (g < c && s.n_ign) ? a.link[vs[g] * K + j] : 0u;
+        }
+        L lv[G], cl[G][K];
+        bool ok[G][K];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          lv[g] = g < c ? lab[vs[g]] : static_cast<L>(0);
+          const bool transit = g < c && (vs[g] == s.node || !(rec[g][0].x & ORH_REC_ROW_OVL));
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            ok[g][j] = transit && live_link(s, rec[g][j], lk[g][j]);
+            cl[g][j] = ok[g][j] ? lab[rec[g][j].x & ORH_REC_COL_MASK] : static_cast<L>(0);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (g >= c) break;
+          const uint32_t v = vs[g];
+          const uint32_t dv = static_cast<uint32_t>(lv[g] >> kSh);
+          const uint32_t nhv = static_cast<uint32_t>(lv[g] & kMaskBits);
+          const bool from_src = v == s.node;
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (ok[g][j])
+              merge(rec[g][j].x & ORH_REC_COL_MASK, dv + (a.use_link_metric ? rec[g][j].y : 1u),
+                    from_src ? (1u << a.rank_out[v * K + j]) : nhv, cl[g][j]);
+          const uint2 last = rec[g][K - 1];
+          const bool transit = from_src || !(rec[g][0].x & ORH_REC_ROW_OVL);
+          if (transit && (last.x & ORH_REC_CONT)) {
+            const uint32_t start = last.x & ORH_REC_COL_MASK;
+            for (uint32_t q = 0; q < last.y; ++q) {
+              const uint2 r = a.recs[start + q];
+              if (!live(a, s, r, start + q)) continue;
+              const uint32_t u = r.x & ORH_REC_COL_MASK;
+              merge(u, dv + (a.use_link_metric ? r.y : 1u), from_src ? (1u << a.rank_out[start + q]) : nhv,
+                    lab[u]);
+            }
+          }
+        }
+        atomicSub(&s_work, static_cast<uint32_t>(c));
+      }
+    }
+    {
+      const uint32_t fm = wave_min(far_min);
+      if ((tid & 63u) == 0 && fm != kInf) atomicMin(&s_min[mpar], fm);
+    }
+    __syncthreads();  // bucket drained everywhere; far bound folded
+    const uint32_t m = s_min[mpar];
+    if (m == kInf) break;  // far set empty: done
+    T = m + delta;
+    const uint32_t npar = mpar ^ 1u;
+    if (tid == 0) s_min[npar] = kInf;
+    __syncthreads();
+    uint32_t local_min = kInf, promoted = 0;
+    for (uint32_t w2 = tid; w2 < NB; w2 += nthr) {
+      const uint32_t fb = far[w2];
+      uint32_t promote = 0u;
+      for (uint32_t q = fb; q; q &= q - 1) {
+        const uint32_t b = __builtin_ctz(q);
+        const uint32_t d = static_cast<uint32_t>(lab[w2 * 32 + b] >> kSh);
+        if (d < T) promote |= 1u << b;
+        else local_min = min(local_min, d);
+      }
+      if (promote) {
+        far[w2] = fb & ~promote;
+        near[w2] = promote;  // the near set is empty between buckets
+        promoted += __builtin_popcount(promote);
+      }
+    }
+    if (promoted) atomicAdd(&s_work, promoted);
+    const uint32_t wm = wave_min(local_min);
+    if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
+    mpar = npar;
+    __syncthreads();
+  }
+  if (kPacked && ovf) s_ovf = 1u;
+  __syncthreads();
+  if (kPacked && s_ovf) {  // the u64 form writes this row
+    if (tid == 0) {
+      const uint32_t k = atomicAdd(&a.ovf_rows[0], 1u);
+      a.ovf_rows[1 + k] = row;
+    }
+    return;
+  }
+  // labels -> dist row (kInf = unreachable) and first-hop row, coalesced
+  uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
+  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * a.words;
+  for (uint32_t i = tid; i < N; i += nthr) {
+    const L l = lab[i];
+    const uint32_t d = static_cast<uint32_t>(l >> kSh);
+    __builtin_nontemporal_store(d == kDInf ? kInf : d, &od[i]);
+    const uint32_t m = static_cast<uint32_t>(l & kMaskBits);
+    if (a.words == 1) {
+      __builtin_nontemporal_store(m, &on[i]);
+    } else {
+      on[static_cast<size_t>(i) * a.words] = m;
+      for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
+    }
+  }
+}
+
+size_t lds_nh_bytes(uint32_t n_nodes, bool packed) {
+  const size_t nb = (n_nodes + 31) / 32;
+  size_t fw = 1;
+  while (2 * fw <= std::min<size_t>(nb, 256)) fw *= 2;
+  const size_t lab = packed ? ((n_nodes + 1) & ~size_t{1}) : 2 * static_cast<size_t>(n_nodes);
+  return 4 * (lab + 2 * nb + fw);
+}
+
 template <int K>
 __global__ __launch_bounds__(1024) void spf_global_nh_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -2738,6 +2981,31 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
   b.row_list = a.ovf_rows + 1;
   b.row_count = a.ovf_rows;
   return launch_spf(fallback, b, n_rows, s);
+}
+
+hipError_t launch_spf_lds_nh(SpfArgs a, uint32_t n_rows, uint32_t ell_k, bool packed, uint32_t block,
+                             hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  if (packed && !a.ovf_rows) return hipErrorInvalidValue;
+  a.n_rows = n_rows;
+  a.row_list = nullptr;
+  a.row_count = nullptr;
+  hipError_t e = hipSuccess;
+  if (packed) {
+    e = hipMemsetAsync(a.ovf_rows, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const size_t lds = lds_nh_bytes(a.n_nodes, true);
+    e = ell_k == 8 ? launch(spf_lds_nh_kernel<8, true>, a, n_rows, block, lds, s)
+                   : launch(spf_lds_nh_kernel<4, true>, a, n_rows, block, lds, s);
+    if (e != hipSuccess) return e;
+    // rows with a distance past 16 bits: the u64 form over that list
+    // (workgroups past the list's length exit at once)
+    a.row_list = a.ovf_rows + 1;
+    a.row_count = a.ovf_rows;
+  }
+  const size_t lds = lds_nh_bytes(a.n_nodes, false);
+  return ell_k == 8 ? launch(spf_lds_nh_kernel<8, false>, a, n_rows, block, lds, s)
+                    : launch(spf_lds_nh_kernel<4, false>, a, n_rows, block, lds, s);
 }
 
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {

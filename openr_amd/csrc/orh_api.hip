@@ -1966,6 +1966,35 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       n_rows = n_src;
     }
   }
+  // general metrics whose labels fit LDS: one search per source with the
+  // first hops fused (spf_lds_nh_kernel) instead of the two-phase LDS kernels,
+  // which also search every neighbour row and then stream 1 + deg rows per
+  // source. ORH_LDS_NH=0: the two-phase plan (A/B); orh_set_spf_mode(1)
+  // (per-source) keeps it too
+  bool lds_nh_packed = false;
+  {
+    static const bool on = [] {
+      const char* e = getenv("ORH_LDS_NH");
+      return !(e && e[0] == '0');
+    }();
+    if (on && ctx->spf_mode == orh::SpfMode::kAuto && !uniform && max_nbr <= 32 &&
+        (plan.variant == orh::SpfVariant::kDist16 || plan.variant == orh::SpfVariant::kDist32) &&
+        orh::lds_nh_bytes(N, false) <= ctx->lds_limit) {
+      run_plan.variant = orh::SpfVariant::kLdsNh;
+      lds_nh_packed = max_nbr <= 16;
+      n_rows = n_src;
+      // few rows: wide workgroups (latency); many: narrow ones, several per CU
+      static const uint32_t blk_env = [] {
+        const char* e = getenv("ORH_LDS_NH_BLOCK");
+        const int b = e ? atoi(e) : 0;
+        return (b >= 64 && b <= 1024 && b % 64 == 0) ? static_cast<uint32_t>(b) : 0u;
+      }();
+      run_plan.block = blk_env ? blk_env
+                     : n_src <= ctx->n_cu ? 1024u : n_src <= 2 * ctx->n_cu ? 512u : 256u;
+      int rc = ensure_labels(ctx, (static_cast<size_t>(n_src) + 2) / 2 + 1);  // the overflow row list
+      if (rc) return rc;
+    }
+  }
   if (plan.variant == orh::SpfVariant::kGlobal && max_nbr <= 32 &&
       ctx->spf_mode != orh::SpfMode::kGlobalTwoPhase &&
       (ctx->spf_mode == orh::SpfMode::kGlobal || n_rows > n_src)) {
@@ -1978,7 +2007,8 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     if (rc) return rc;
   }
   const bool fused = run_plan.variant == orh::SpfVariant::kGlobalNh ||
-                     run_plan.variant == orh::SpfVariant::kBfsNh;
+                     run_plan.variant == orh::SpfVariant::kBfsNh ||
+                     run_plan.variant == orh::SpfVariant::kLdsNh;
   const size_t n_extra = n_rows - n_src;
   if (n_extra) {
     int rc = ensure_scratch(ctx, n_extra * N);
@@ -2022,6 +2052,18 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.delta = uniform ? w0
                     : std::max<uint32_t>(1u, static_cast<uint32_t>(
                                                  static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
+  if (run_plan.variant == orh::SpfVariant::kLdsNh) {
+    // ORH_LDS_NH_DELTA_PCT: bucket width of the LDS search in % of the mean
+    // live metric. Its relaxations cost LDS latency, not a global atomic, so
+    // wider buckets (fewer bucket barriers) pay: C2w sweep 45.5 / 30.8 / 28.9 /
+    // 29.0 / 31.4 ms at 25 / 100 / 200 / 400 / 800 (profiles/r06/b_c2w_delta_block.txt)
+    static const uint32_t pct = [] {
+      const char* e = getenv("ORH_LDS_NH_DELTA_PCT");
+      const int v = e ? atoi(e) : 200;
+      return v > 0 ? static_cast<uint32_t>(v) : 200u;
+    }();
+    a.delta = std::max<uint32_t>(1u, static_cast<uint32_t>(static_cast<uint64_t>(g->mean_out) * pct / 100u));
+  }
   a.out_dist = d_dist;
   a.scratch = ctx->d_scratch;
   a.labels = ctx->d_labels;
@@ -2064,7 +2106,11 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     hipError_t pre = hipGetLastError();
     if (pre != hipSuccess) { std::string m = "pending HIP error before spf launch (variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + ")"; return hip_fail(ctx, pre, m.c_str()); }
   }
-  hipError_t e = orh::launch_spf(run_plan, a, n_rows, ctx->stream);
+  if (run_plan.variant == orh::SpfVariant::kLdsNh)
+    a.ovf_rows = reinterpret_cast<uint32_t*>(ctx->d_labels);
+  hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
+      ? orh::launch_spf_lds_nh(a, n_rows, g->ell_k, lds_nh_packed, run_plan.block, ctx->stream)
+      : orh::launch_spf(run_plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) { std::string m = "spf kernel launch variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + " lds " + std::to_string(run_plan.lds_bytes) + " block " + std::to_string(run_plan.block) + " j " + std::to_string(run_plan.ms_j); return hip_fail(ctx, e, m.c_str()); }
 #ifdef ORH_DIAG_STAMPS
   {

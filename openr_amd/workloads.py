@@ -56,6 +56,28 @@ def c3_fabric(num_nodes: int = 2500, num_prefixes: int = 100_000, anycast: float
     return adj_dbs, prefixes
 
 
+C2W_SEED, C2W_MAX_METRIC = 2002, 64
+
+
+def c2_weighted_grid(n: int = 100, max_metric: int = C2W_MAX_METRIC, seed: int = C2W_SEED):
+    """C2 with integer metrics (the weighted all-sources leg): the benchmark
+    grid createGrid(n) (topology.bench_grid) with every link given a seeded
+    metric uniform in [1, max_metric], the same in both directions (an IGP
+    cost per link). Returns (adj_dbs, prefixes) like bench_grid."""
+    adj_dbs, prefixes = bench_grid(n, 1)
+    rng = random.Random(seed)
+    metric = {}
+    for db in adj_dbs:
+        a = int(db.thisNodeName)
+        for adj in db.adjacencies:
+            b = int(adj.otherNodeName)
+            key = (min(a, b), max(a, b))
+            if key not in metric:
+                metric[key] = rng.randint(1, max_metric)
+            adj.metric = metric[key]
+    return adj_dbs, prefixes
+
+
 def c4_wan(num_nodes: int = 50_000, seed: int = C4_SEED):
     return wan(num_nodes, seed=seed)
 

@@ -197,3 +197,46 @@ def test_nexthop_list_order(hip, oracle, case):
     assert not bad, f"{len(bad)} of {len(uo) + len(mo)} routes list their nexthops in another order, e.g. {bad[0]}"
     if case != "c5_policy":  # (C5's `me` has one link per area: single-nexthop routes)
         assert sum(len(v) > 1 for v in list(uo.values()) + list(mo.values())) >= 5  # orders that can differ
+
+
+def test_nexthop_list_order_after_linkset_rehash(hip, oracle):
+    """the shared nexthop sets are cached across builds while the
+    templates stay; a non-tight parallel link added to `me` leaves the tight
+    templates as they were but can rehash my LinkSet and so reorder the
+    links getNextHopsThrift inserts (Decision.cpp:1245-1246). After each of
+    several such additions (both ends, so the link is up), every route's
+    nexthop list must still be in the oracle's order."""
+    import copy
+    adj, pfx = c3_fabric(num_prefixes=2000)
+    me = "2-0-0"
+    by_name = {db.thisNodeName: db for db in adj}
+    als_h, ps_h = load_topology(hip, adj, pfx)
+    als_o, ps_o = load_topology(oracle, adj, pfx)
+    sh = hip.spf_solver(me, True)._impl
+    so = oracle.spf_solver(me, True)._impl
+    mine = list(by_name[me].adjacencies)
+    rng = random.Random(808)
+    multi = 0
+    for step in range(5):
+        (uh, mh), (uo, mo) = _lists(sh.build_route_db(me, als_h._impl, ps_h._impl)), \
+            _lists(so.build_route_db(me, als_o._impl, ps_o._impl))
+        assert uh.keys() == uo.keys() and mh.keys() == mo.keys()
+        bad = [k for k in uo if uh[k] != uo[k]] + [k for k in mo if mh[k] != mo[k]]
+        assert not bad, f"step {step}: {len(bad)} routes list their nexthops in another order, e.g. {bad[0]}"
+        multi += sum(len(v) > 1 for v in uo.values())
+        for i in range(12):  # non-tight parallel links me <-> a neighbour
+            a = rng.choice(mine)
+            peer = by_name[a.otherNodeName]
+            back = next(b for b in peer.adjacencies if b.otherNodeName == me)
+            tag = f"-p{step}.{i}"
+            fwd, rev = copy.copy(a), copy.copy(back)
+            fwd.ifName, fwd.otherIfName = a.ifName + tag, a.otherIfName + tag
+            rev.ifName, rev.otherIfName = back.ifName + tag, back.otherIfName + tag
+            fwd.metric = rev.metric = 5 + i
+            by_name[me].adjacencies.append(fwd)
+            peer.adjacencies.append(rev)
+            for als in (als_h, als_o):
+                als[K_TESTING_AREA].update_adjacency_database(peer)
+        for als in (als_h, als_o):
+            als[K_TESTING_AREA].update_adjacency_database(by_name[me])
+    assert multi >= 5

@@ -233,3 +233,49 @@ def test_prefix_sharded_route_build(hip, oracle):
             assert not db.mplsRoutes
     from openr_amd.types import RouteDb
     assert RouteDb(uc, mp_).canonical_full() == full.canonical_full()
+
+
+def test_merge_ranks_reports_max():
+    """bench.py --gpus N: rank 0 reports each N-rank leg's max over ranks."""
+    import bench_legs
+    per = [{"c3": {"build_route_db_shard_ms": 1.0, "leg_wall_s": 1},
+            "c4": {"what_if_block_ms": 3.0, "ksp2_block_ms": 1.0, "what_if_requests": 10, "ksp2_pairs": 4,
+                   "leg_wall_s": 2}},
+           {"c3": {"build_route_db_shard_ms": 2.0, "leg_wall_s": 1},
+            "c4": {"what_if_block_ms": 1.0, "ksp2_block_ms": 2.0, "what_if_requests": 6, "ksp2_pairs": 4,
+                   "leg_wall_s": 2}}]
+    m = bench_legs.merge_ranks(per, 2)
+    assert m["c3"]["build_route_db_max_ms"] == 2.0
+    assert m["c4"]["what_if_max_ms"] == 3.0 and m["c4"]["ksp2_max_ms"] == 2.0
+    assert m["c4"]["what_if_spfs_per_s"] == round(16 / 3e-3, 1)
+    per[1]["c4"] = {"error": "RuntimeError: x", "leg_wall_s": 0}
+    assert "error" in bench_legs.merge_ranks(per, 2)["c4"]
+
+
+def test_rank_blocks_partition_the_c4_job():
+    """The N-rank C4 blocks (bench_legs.c4_what_if_block / c4_ksp2_block)
+    partition the benched requests and pairs, whole sources per block, with
+    balanced request counts - the cuts MultiDeviceWhatIf / MultiDeviceKthPaths
+    make (equalWorkCuts)."""
+    import random
+    import bench_legs
+    from openr_amd.workloads import c4_ksp2_pairs, c4_what_if_job
+    names = [f"w{i}" for i in range(5000)]
+    srcs, idx, sets = c4_what_if_job(list(range(20000)), names, n_links=256, n_srcs=64)
+    pairs = c4_ksp2_pairs(names, 1024)
+    for world in (1, 2, 3, 8):
+        got, kp = [], []
+        for r in range(world):
+            reqs, bs, bi, bsets = bench_legs.c4_what_if_block(srcs, idx, sets, r, world)
+            assert all(bs[bi[k]] == srcs[idx[q]] and bsets[k] == sets[q] for k, q in enumerate(reqs))
+            got += reqs
+            kp.append(bench_legs.c4_ksp2_block(pairs, r, world))
+            assert len(reqs) <= len(idx) // world + len(idx) // len(srcs)
+        assert sorted(got) == list(range(len(idx)))
+        flat = sorted(i for b in kp for i in b)
+        assert flat == list(range(len(pairs)))
+        owner = {}
+        for r, b in enumerate(kp):
+            for i in b:
+                assert owner.setdefault(pairs[i][0], r) == r  # a source's pairs on one rank
+    random.seed(0)
