@@ -160,6 +160,8 @@ int orh_set_repair_mode(orh_ctx* ctx, int mode);
                                    (batch_sources = distinct sources searched) */
 #define ORH_VARIANT_LDS_NH 12   /* general metrics, {dist, first hops} labels in LDS,
                                    first hops fused, one workgroup per source */
+#define ORH_VARIANT_WMS 13      /* general metrics, many sources: 4-source Bellman-Ford
+                                   batches in LDS, then the first-hop phase */
 typedef struct orh_spf_info {
   int32_t variant;     /* ORH_VARIANT_* of the distance phase */
   uint32_t rows;       /* distance rows searched (sources + neighbour rows) */

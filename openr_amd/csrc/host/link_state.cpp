@@ -123,12 +123,48 @@ bool Link::less(const Link& o) const {
 uint64_t LinkState::nextStamp() { return nextGeneration(); }
 
 LinkState::LinkState(const std::string& area, orh_ctx* ctx)
-    : area_(area), stamp_(nextStamp()), ctx_(ctx ? ctx : defaultContext()) {
+    : area_(area), stamp_(nextStamp()), ctx_(ctx ? ctx : defaultContext()),
+      store_(std::make_shared<LinkStateStore>()), ids_(store_->ids), names_(store_->names),
+      links_(store_->links), freeLinks_(store_->freeLinks), nLinks_(store_->nLinks),
+      nodeLinks_(store_->nodeLinks), nodeOverloads_(store_->nodeOverloads),
+      adjacencyDatabases_(store_->adjacencyDatabases) {
   check(ctx_, orh_graph_create(ctx_, &graph_), "orh_graph_create");
+  store_->views.push_back(this);
+}
+
+LinkState::LinkState(LinkState& primary, orh_ctx* ctx)
+    : area_(primary.area_), stamp_(nextStamp()), ctx_(ctx ? ctx : defaultContext()), replica_(true),
+      store_(primary.store_), ids_(store_->ids), names_(store_->names), links_(store_->links),
+      freeLinks_(store_->freeLinks), nLinks_(store_->nLinks), nodeLinks_(store_->nodeLinks),
+      nodeOverloads_(store_->nodeOverloads), adjacencyDatabases_(store_->adjacencyDatabases) {
+  if (primary.replica_) throw std::invalid_argument("LinkState: a replica of a replica");
+  check(ctx_, orh_graph_create(ctx_, &graph_), "orh_graph_create");
+  store_->views.push_back(this);  // structDirty_: the whole store uploads at first use
 }
 
 LinkState::~LinkState() {
+  auto& v = store_->views;
+  v.erase(std::remove(v.begin(), v.end(), this), v.end());
   if (graph_) orh_graph_destroy(graph_);
+}
+
+void LinkState::mutating() const {
+  if (replica_) throw std::logic_error("LinkState: a device replica is updated through its primary");
+}
+void LinkState::markStruct() {
+  for (LinkState* w : store_->views) w->structDirty_ = true;
+}
+void LinkState::markRow(uint32_t v) {
+  for (LinkState* w : store_->views) w->rowsDirty_.insert(v);
+}
+void LinkState::markLink(uint32_t id) {
+  for (LinkState* w : store_->views) w->patchLinks_.insert(id);
+}
+void LinkState::markNode(uint32_t v) {
+  for (LinkState* w : store_->views) w->patchNodes_.insert(v);
+}
+void LinkState::newStamps() {
+  for (LinkState* w : store_->views) w->stamp_ = nextStamp();
 }
 
 uint32_t LinkState::ensureNode(const std::string& n) {
@@ -138,7 +174,7 @@ uint32_t LinkState::ensureNode(const std::string& n) {
   ids_.emplace(n, id);
   names_.push_back(n);
   nodeLinks_.push_back(std::make_unique<LinkSet>(0, LinkIdHash{&links_}));
-  structDirty_ = true;
+  markStruct();
   return id;
 }
 
@@ -148,7 +184,7 @@ std::optional<uint32_t> LinkState::nodeId(const std::string& n) const {
   return it->second;
 }
 
-LinkState::LinkSet& LinkState::setOf(uint32_t v) { return *nodeLinks_[v]; }
+LinkSet& LinkState::setOf(uint32_t v) { return *nodeLinks_[v]; }
 
 size_t LinkState::numNodes() const {
   size_t n = 0;  // nodes with a link set entry (linkMap_ keys)
@@ -224,8 +260,8 @@ uint32_t LinkState::addLink(Link&& l) {  // LinkState.cpp:421-426
   if (!setOf(first).insert(id).second || !setOf(second).insert(id).second)
     throw std::logic_error("LinkState: duplicate link");
   ++nLinks_;
-  rowsDirty_.insert(first);
-  rowsDirty_.insert(second);
+  markRow(first);
+  markRow(second);
   return id;
 }
 
@@ -237,22 +273,22 @@ void LinkState::removeLink(uint32_t id) {  // LinkState.cpp:429-434
   k.alive = false;
   freeLinks_.push_back(id);
   --nLinks_;
-  rowsDirty_.insert(first);
-  rowsDirty_.insert(k.other(first));
+  markRow(first);
+  markRow(k.other(first));
 }
 
 void LinkState::removeNode(uint32_t v) {  // LinkState.cpp:436-455
   std::vector<uint32_t> ids(setOf(v).begin(), setOf(v).end());
   for (uint32_t id : ids) {
     setOf(links_[id].other(v)).erase(id);
-    rowsDirty_.insert(links_[id].other(v));
+    markRow(links_[id].other(v));
     links_[id].alive = false;
     freeLinks_.push_back(id);
     --nLinks_;
   }
   setOf(v).clear();
-  rowsDirty_.insert(v);
-  if (nodeOverloads_.erase(names_[v])) patchNodes_.insert(v);
+  markRow(v);
+  if (nodeOverloads_.erase(names_[v])) markNode(v);
 }
 
 std::vector<uint32_t> LinkState::orderedLinks(uint32_t v) const {
@@ -267,16 +303,17 @@ bool LinkState::updateNodeOverloaded(const std::string& n, bool o, Metric up, Me
   if (it != nodeOverloads_.end()) {
     const bool before = it->second.value();
     const bool changed = it->second.update(o, up, down);
-    if (it->second.value() != before) patchNodes_.insert(*nodeId(n));
+    if (it->second.value() != before) markNode(*nodeId(n));
     return changed;
   }
   nodeOverloads_.emplace(n, Holdable<bool>(o));
-  if (o) patchNodes_.insert(ensureNode(n));
+  if (o) markNode(ensureNode(n));
   return false;  // a new node's overload bit is not a topology change
 }
 
 void LinkState::invalidate(bool topologyChanged) {
-  if (topologyChanged) dropMemo();
+  if (!topologyChanged) return;
+  for (LinkState* w : store_->views) w->dropMemo();
 }
 
 void LinkState::dropMemo() const {
@@ -291,8 +328,9 @@ void LinkState::dropMemo() const {
 LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric up,
                                                    Metric down) {
   // LinkState.cpp:564-719
+  mutating();
   LinkStateChange change;
-  stamp_ = nextStamp();
+  newStamps();
   const std::string& node = db.thisNodeName;
   const uint32_t v = ensureNode(node);
   AdjacencyDatabase prior = std::move(adjacencyDatabases_[node]);
@@ -332,7 +370,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, 
     const Metric nm = nside1 ? nl.metric1.value() : nl.metric2.value();
     if (nm != om.value()) {
       change.topologyChanged |= om.update(nm, up, down);
-      patchLinks_.insert(id);
+      markLink(id);
     }
     auto& oo = side1 ? ol.overload1 : ol.overload2;
     const bool no = nside1 ? nl.overload1.value() : nl.overload2.value();
@@ -340,7 +378,7 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, 
       const bool wasUp = ol.isUp();
       oo.update(no, up, down);
       change.topologyChanged |= wasUp != ol.isUp();
-      patchLinks_.insert(id);
+      markLink(id);
     }
     const int32_t nlab = nside1 ? nl.adjLabel1 : nl.adjLabel2;
     if (nlab != ol.adjLabelFrom(v)) {
@@ -363,8 +401,9 @@ LinkStateChange LinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, 
 }
 
 LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
+  mutating();
   LinkStateChange c;  // LinkState.cpp:721-738
-  stamp_ = nextStamp();
+  newStamps();
   auto it = adjacencyDatabases_.find(node);
   if (it == adjacencyDatabases_.end()) return c;
   removeNode(*nodeId(node));
@@ -375,8 +414,9 @@ LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& node) {
 }
 
 LinkStateChange LinkState::decrementHolds() {  // LinkState.cpp:500-514
+  mutating();
   LinkStateChange c;
-  stamp_ = nextStamp();
+  newStamps();
   for (uint32_t id = 0; id < links_.size(); ++id) {
     Link& l = links_[id];
     if (!l.alive) continue;
@@ -386,13 +426,13 @@ LinkStateChange LinkState::decrementHolds() {  // LinkState.cpp:500-514
     expired |= l.metric2.decrementTtl();
     expired |= l.overload1.decrementTtl();
     expired |= l.overload2.decrementTtl();
-    if (expired) patchLinks_.insert(id);
+    if (expired) markLink(id);
     c.topologyChanged |= expired;
   }
   for (auto& [name, hv] : nodeOverloads_) {
     if (hv.decrementTtl()) {
       c.topologyChanged = true;
-      patchNodes_.insert(*nodeId(name));
+      markNode(*nodeId(name));
     }
   }
   invalidate(c.topologyChanged);

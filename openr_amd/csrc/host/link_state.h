@@ -207,12 +207,42 @@ class NodeSpfResult {
 };
 using SpfResult = std::unordered_map<std::string /* otherNodeName */, NodeSpfResult>;
 
+// The host graph store of one area (node ids, links, per-node link sets,
+// overloads, adjacency databases): owned by one LinkState and shared by its
+// device replicas (LinkState's replica constructor), so a topology held on N
+// devices is stored and updated on the host once (LinkState.cpp:564-719 run
+// once), and every device mirror is patched from the same delta.
+struct LinkIdHash {
+  const std::vector<Link>* links;
+  size_t operator()(uint32_t id) const { return (*links)[id].hash; }
+};
+using LinkSet = std::unordered_set<uint32_t, LinkIdHash>;
+
+struct LinkStateStore {
+  std::unordered_map<std::string, uint32_t> ids;
+  std::vector<std::string> names;
+  std::vector<Link> links;
+  std::vector<uint32_t> freeLinks;
+  size_t nLinks{0};
+  std::vector<std::unique_ptr<LinkSet>> nodeLinks;
+  std::unordered_map<std::string, Holdable<bool>> nodeOverloads;
+  std::unordered_map<std::string, AdjacencyDatabase> adjacencyDatabases;
+  std::vector<LinkState*> views;  // the owner first, then its device replicas
+};
+
 class LinkState {
  public:
   explicit LinkState(const std::string& area, orh_ctx* ctx = nullptr);
+  // a device replica of `primary`: the same host store (nothing copied, no
+  // update applied twice), its own device mirror on `ctx`, its own memo. The
+  // store is mutated through the primary only; every mutation marks the
+  // replicas' mirrors dirty and clears their memos as it does the primary's.
+  // The primary outlives its replicas.
+  LinkState(LinkState& primary, orh_ctx* ctx);
   ~LinkState();
   LinkState(LinkState&&) = delete;
   LinkState(const LinkState&) = delete;
+  bool isReplica() const { return replica_; }
 
   const std::string& getArea() const { return area_; }
 
@@ -292,12 +322,6 @@ class LinkState {
   orh_ctx* context() const { return ctx_; }
 
  private:
-  struct LinkIdHash {
-    const std::vector<Link>* links;
-    size_t operator()(uint32_t id) const { return (*links)[id].hash; }
-  };
-  using LinkSet = std::unordered_set<uint32_t, LinkIdHash>;
-
   uint32_t ensureNode(const std::string& n);
   std::optional<Link> maybeMakeLink(const std::string& node, const Adjacency& adj);
   uint32_t addLink(Link&& l);
@@ -321,20 +345,32 @@ class LinkState {
                                    std::unordered_set<uint32_t>& visited,
                                    const std::unordered_set<uint32_t>* ignore) const;
 
+  // device-mirror bookkeeping of every view of the store (this one and its
+  // replicas): what a mutation must re-upload, and the memos it invalidates
+  void markStruct();
+  void markRow(uint32_t v);
+  void markLink(uint32_t id);
+  void markNode(uint32_t v);
+  void newStamps();
+  void mutating() const;  // throws on a replica
+
   std::string area_;
   uint64_t stamp_;
   static uint64_t nextStamp();
   orh_ctx* ctx_;
   mutable orh_graph* graph_{nullptr};
+  bool replica_{false};
 
-  std::unordered_map<std::string, uint32_t> ids_;
-  std::vector<std::string> names_;
-  std::vector<Link> links_;
-  std::vector<uint32_t> freeLinks_;
-  size_t nLinks_{0};
-  std::vector<std::unique_ptr<LinkSet>> nodeLinks_;
-  std::unordered_map<std::string, Holdable<bool>> nodeOverloads_;
-  std::unordered_map<std::string, AdjacencyDatabase> adjacencyDatabases_;
+  // the host graph store (shared with the replicas) under its old names
+  std::shared_ptr<LinkStateStore> store_;
+  std::unordered_map<std::string, uint32_t>& ids_;
+  std::vector<std::string>& names_;
+  std::vector<Link>& links_;
+  std::vector<uint32_t>& freeLinks_;
+  size_t& nLinks_;
+  std::vector<std::unique_ptr<LinkSet>>& nodeLinks_;
+  std::unordered_map<std::string, Holdable<bool>>& nodeOverloads_;
+  std::unordered_map<std::string, AdjacencyDatabase>& adjacencyDatabases_;
 
   // device mirror bookkeeping
   mutable bool structDirty_{true};                 // node set changed: full orh_graph_load

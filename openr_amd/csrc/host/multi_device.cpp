@@ -88,30 +88,33 @@ orh_ctx* deviceContext(int device, unsigned slot) {
 }
 
 // ---- ReplicatedLinkState -----------------------------------------------------
+// replica 0 owns the host graph store; replicas 1.. are device views of it
+// (LinkState's replica constructor): one host update per mutation, every
+// device mirror marked with the same delta (LinkState.cpp:564-719 once)
 ReplicatedLinkState::ReplicatedLinkState(const std::string& area, const std::vector<int>& devices) {
   if (devices.empty()) throw std::invalid_argument("ReplicatedLinkState: no devices");
   std::map<int, unsigned> seen;
-  for (int d : devices) reps_.push_back(std::make_unique<LinkState>(area, deviceContext(d, seen[d]++)));
+  for (int d : devices) {
+    orh_ctx* ctx = deviceContext(d, seen[d]++);
+    if (reps_.empty()) reps_.push_back(std::make_unique<LinkState>(area, ctx));
+    else reps_.push_back(std::make_unique<LinkState>(*reps_[0], ctx));
+  }
+}
+
+ReplicatedLinkState::~ReplicatedLinkState() {
+  while (reps_.size() > 1) reps_.pop_back();  // the replicas before the store's owner
 }
 
 LinkStateChange ReplicatedLinkState::updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl,
                                                              Metric holdDownTtl) {
-  LinkStateChange c = reps_[0]->updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
-  for (size_t r = 1; r < reps_.size(); ++r) reps_[r]->updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
-  return c;
+  return reps_[0]->updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
 }
 
 LinkStateChange ReplicatedLinkState::deleteAdjacencyDatabase(const std::string& node) {
-  LinkStateChange c = reps_[0]->deleteAdjacencyDatabase(node);
-  for (size_t r = 1; r < reps_.size(); ++r) reps_[r]->deleteAdjacencyDatabase(node);
-  return c;
+  return reps_[0]->deleteAdjacencyDatabase(node);
 }
 
-LinkStateChange ReplicatedLinkState::decrementHolds() {
-  LinkStateChange c = reps_[0]->decrementHolds();
-  for (size_t r = 1; r < reps_.size(); ++r) reps_[r]->decrementHolds();
-  return c;
-}
+LinkStateChange ReplicatedLinkState::decrementHolds() { return reps_[0]->decrementHolds(); }
 
 // ---- MultiDeviceSweep --------------------------------------------------------
 MultiDeviceSweep::MultiDeviceSweep(const ReplicatedLinkState& rls, const std::vector<std::string>& srcs,
@@ -428,25 +431,29 @@ ReplicatedAreaLinkStates::ReplicatedAreaLinkStates(const std::vector<int>& devic
   }
 }
 
+ReplicatedAreaLinkStates::~ReplicatedAreaLinkStates() {
+  while (reps_.size() > 1) reps_.pop_back();  // the replicas before the stores' owners
+}
+
 void ReplicatedAreaLinkStates::addArea(const std::string& area) {
-  for (size_t r = 0; r < reps_.size(); ++r)
+  if (!reps_[0]->count(area))
+    reps_[0]->emplace(std::piecewise_construct, std::forward_as_tuple(area), std::forward_as_tuple(area, ctxs_[0]));
+  LinkState& primary = reps_[0]->at(area);
+  for (size_t r = 1; r < reps_.size(); ++r)
     if (!reps_[r]->count(area))
-      reps_[r]->emplace(std::piecewise_construct, std::forward_as_tuple(area), std::forward_as_tuple(area, ctxs_[r]));
+      reps_[r]->emplace(std::piecewise_construct, std::forward_as_tuple(area),
+                        std::forward_as_tuple(primary, ctxs_[r]));
 }
 
 LinkStateChange ReplicatedAreaLinkStates::updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl,
                                                                   Metric holdDownTtl) {
-  addArea(db.area);
-  LinkStateChange c = reps_[0]->at(db.area).updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
-  for (size_t r = 1; r < reps_.size(); ++r) reps_[r]->at(db.area).updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
-  return c;
+  addArea(db.area);  // one host update: the replicas share replica 0's store
+  return reps_[0]->at(db.area).updateAdjacencyDatabase(db, holdUpTtl, holdDownTtl);
 }
 
 LinkStateChange ReplicatedAreaLinkStates::deleteAdjacencyDatabase(const std::string& area, const std::string& node) {
   addArea(area);
-  LinkStateChange c = reps_[0]->at(area).deleteAdjacencyDatabase(node);
-  for (size_t r = 1; r < reps_.size(); ++r) reps_[r]->at(area).deleteAdjacencyDatabase(node);
-  return c;
+  return reps_[0]->at(area).deleteAdjacencyDatabase(node);
 }
 
 // ---- ShardedRouteBuilder -----------------------------------------------------

@@ -23,13 +23,15 @@ namespace openr_amd {
 // (or, on a one-GPU box, a rehearsal of several devices).
 orh_ctx* deviceContext(int device, unsigned slot = 0);
 
-// One area's LinkState on several devices: every mutation goes to every
-// replica (each mirrors the same graph into its device), and the replicas
-// answer alike; replica 0 is the primary. devices may repeat a device id
-// (a second context on that device).
+// One area's LinkState on several devices: replica 0 (the primary) owns the
+// host graph store, replicas 1.. are device views of it (LinkState's replica
+// constructor): a mutation is applied to the store once and marks every
+// replica's device mirror with the same delta, and the replicas answer alike.
+// devices may repeat a device id (a second context on that device).
 class ReplicatedLinkState {
  public:
   ReplicatedLinkState(const std::string& area, const std::vector<int>& devices);
+  ~ReplicatedLinkState();
   LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl = 0,
                                           Metric holdDownTtl = 0);
   LinkStateChange deleteAdjacencyDatabase(const std::string& node);
@@ -186,6 +188,7 @@ class MultiDeviceKthPaths {
 class ReplicatedAreaLinkStates {
  public:
   explicit ReplicatedAreaLinkStates(const std::vector<int>& devices);
+  ~ReplicatedAreaLinkStates();
   void addArea(const std::string& area);
   // the area is db.area (added on first use)
   LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db, Metric holdUpTtl = 0,

@@ -1468,6 +1468,12 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
       // merge throws (bad_alloc in reserve / emplace), exactly the rest are
       // destroyed before rethrowing
       std::vector<uint32_t> done(W * kS, 0u);
+      // shards claimed one at a time (dynamic chunks): shard sizes vary, and
+      // kS / threads leaves a static split uneven. ORH_MERGE_DYN=0: static (A/B)
+      static const size_t mergeChunks = [] {
+        const char* e = std::getenv("ORH_MERGE_DYN");
+        return (e && e[0] == '0') ? size_t{0} : kS;
+      }();
       try {
       pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
         for (size_t sh = b; sh < e; ++sh) {
@@ -1484,7 +1490,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
               ++done[w * kS + sh];
             }
         }
-      });
+      }, mergeChunks);
       } catch (...) {
         for (size_t l = 0; l < slots.lists.size(); ++l) {
           auto& list = slots.lists[l];
@@ -1574,19 +1580,25 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           if (lbl == 0 || !isMplsLabelValid(lbl) || !cand[i]) continue;
           byLabelShard[MplsRouteMap::shardOf(lbl)].push_back(static_cast<uint32_t>(i));
         }
+        // per shard: candidates sorted by (label, node name), the first of
+        // each label wins - no per-shard map of winners to allocate; shards
+        // claimed one at a time
         pool.parallelFor(MplsRouteMap::kShards, [&](size_t, size_t b, size_t e) {
           for (size_t sh = b; sh < e; ++sh) {
-            std::unordered_map<int32_t, uint32_t> win;
-            win.reserve(byLabelShard[sh].size());
-            for (uint32_t i : byLabelShard[sh]) {
-              auto [it, fresh] = win.emplace(dbs[i]->nodeLabel, i);
-              if (!fresh && dbs[i]->thisNodeName < dbs[it->second]->thisNodeName) it->second = i;
-            }
+            auto& list = byLabelShard[sh];
+            std::sort(list.begin(), list.end(), [&](uint32_t x, uint32_t y) {
+              const int32_t lx = dbs[x]->nodeLabel, ly = dbs[y]->nodeLabel;
+              return lx != ly ? lx < ly : dbs[x]->thisNodeName < dbs[y]->thisNodeName;
+            });
             auto& dst = db.mplsRoutes.shard(sh);
-            dst.reserve(dst.size() + win.size() + 1);
-            for (auto& [lbl, i] : win) dst.emplace(lbl, std::move(*cand[i]));
+            dst.reserve(dst.size() + list.size() + 1);
+            for (size_t q = 0; q < list.size(); ++q) {
+              const uint32_t i = list[q];
+              if (q && dbs[list[q - 1]]->nodeLabel == dbs[i]->nodeLabel) continue;
+              dst.emplace(dbs[i]->nodeLabel, std::move(*cand[i]));
+            }
           }
-        });
+        }, MplsRouteMap::kShards);
         prof.mark("label map");
       }
       labelsDone = true;

@@ -67,6 +67,12 @@ struct SpfArgs {
   // u16 LDS search (launch_spf_lds16): [0] count, then the rows it left to
   // the HBM kernel (a distance that needs 17 bits)
   uint32_t* ovf_rows;
+  // multi-source Bellman-Ford (kWms): per Cuthill-McKee node K in-link slots
+  // {u | w(u -> v) << 16 | overloaded(u) << 31} (u = N: no link), and the
+  // largest u16 label that proves its row fits 16 bits (0xFFFE - max metric)
+  const uint32_t* wms_slots;
+  uint32_t wms_limit;
+  uint32_t recs_k;  // ELL width of `recs` (kernels launched from plans that do not know it)
 };
 
 // phase 2: first-hop masks of the requested rows from the distance rows of
@@ -110,8 +116,17 @@ enum class SpfVariant {
   kExact,     // the reference's Dijkstra order (zero metrics, 64-bit path metrics)
   kBfsNh,     // uniform metric, few sources: BFS with the first hops fused (no phase 2)
   kRepair,    // ignore-set batch derived from its sources' plain SPFs (whatif_kernels.hip)
-  kLdsNh      // general metrics, labels {dist, first hops} in LDS, first hops fused (no phase 2)
+  kLdsNh,     // general metrics, labels {dist, first hops} in LDS, first hops fused (no phase 2)
+  kWms        // general metrics, many sources: 4-source Bellman-Ford in LDS, then phase 2
 };
+// spf_wms_kernel: LDS bytes of one 4-source batch (u16 x 4 per node + 1)
+size_t wms_lds_bytes(uint32_t n_nodes);
+// batches of 4 rows (a.order), 1024 threads each; rows whose labels come too
+// close to 16 bits are listed in a.ovf_rows (n_rows + 1 words) and redone by
+// the u64 spf_lds_nh_kernel (its LDS must fit). Writes dist rows only.
+// wms_k: in-link slots per node of a.wms_slots (4 or 8); a.recs_k: the ELL
+// width of a.recs (for the u64 LDS search of the flagged rows)
+hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, hipStream_t s);
 // spf_lds_nh_kernel: LDS bytes per search (packed: u32 labels, <= 16
 // distinct neighbours per source; else u64 labels)
 size_t lds_nh_bytes(uint32_t n_nodes, bool packed);

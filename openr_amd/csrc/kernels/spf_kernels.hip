@@ -502,6 +502,23 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     if (v < N) vis[j] = f_cur[v];  // level 0: the sources
     if (kLog) log_events(j, v < N ? vis[j] : V(0), 0u);
   }
+  // wave-uniform bit j: some lane of this wave owns, in slice j, a node with
+  // an overflow list / an overloaded node. Both are rare (none on C2), so the
+  // per-node tests below sit behind one scalar test instead of per-lane exec
+  // masks built from bit masks the compiler keeps in spilled SGPR lanes
+  // (ORH_MS_NO_WAVE_UNIFORM, A/B builds: the per-lane tests alone)
+#ifndef ORH_MS_NO_WAVE_UNIFORM
+  uint32_t wovf = 0u, wovl = 0u;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    wovf |= (__builtin_amdgcn_ballot_w64((ovfm >> j) & 1u) != 0u ? 1u : 0u) << j;
+    wovl |= (__builtin_amdgcn_ballot_w64((ovlm >> j) & 1u) != 0u ? 1u : 0u) << j;
+  }
+  wovf = __builtin_amdgcn_readfirstlane(wovf);
+  wovl = __builtin_amdgcn_readfirstlane(wovl);
+#else
+  const uint32_t wovf = ~0u, wovl = ~0u;
+#endif
 
   const uint32_t w0 = a.w0;
 #ifdef ORH_DIAG_STAMPS
@@ -579,7 +596,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
         const uint32_t v = j * B + me;
         V nx = 0u;
         if (vis[j] != full) {  // also every v >= N
-          if ((ovfm >> j) & 1u) {
+          if (((wovf >> j) & 1u) && ((ovfm >> j) & 1u)) {
             const uint2 last = a.recs[static_cast<size_t>(v) * K + K - 1];
             const uint2* ov = a.recs + (last.x & ORH_REC_COL_MASK);
             for (uint32_t q = 0; q < last.y; ++q) {
@@ -618,10 +635,18 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
 #ifdef ORH_DIAG_STAMPS
         t_store += __builtin_amdgcn_s_memtime() - t_s0;
 #endif
-        if (vis[j] != full || nx) {
-          if ((ovlm >> j) & 1u) nx = 0u;  // reached, but no transit through an overloaded node
-          f_nxt[v] = static_cast<M>(nx);
-        }
+        if (((wovl >> j) & 1u) && ((ovlm >> j) & 1u)) nx = 0u;  // reached, but no transit through an overloaded node
+#ifndef ORH_MS_WRITE_ZEROS
+        // only a node with new bits writes its entry: whatever an entry still
+        // holds from an older level (bits that reached it at level L - 2k)
+        // reached every neighbour by level L - 2k + 1, so the pull masks it
+        // with the neighbour's visited bits. Writing the zeros (every open
+        // node, every level) was ~1/3 of the loop's LDS cycles
+        // (ORH_MS_WRITE_ZEROS, A/B builds: the former stores)
+        if (nx) f_nxt[v] = static_cast<M>(nx);
+#else
+        if (vis[j] != full || nx) f_nxt[v] = static_cast<M>(nx);
+#endif
         if constexpr (kSkip) jm |= (__builtin_amdgcn_ballot_w64(nx != 0u) != 0u ? 1u : 0u) << j;
       }
     }
@@ -2022,14 +2047,16 @@ __global__ __launch_bounds__(1024) void spf_lds_nh_kernel(SpfArgs a) {
     }
     return;
   }
-  // labels -> dist row (kInf = unreachable) and first-hop row, coalesced
-  uint32_t* od = a.out_dist + static_cast<size_t>(row) * N;
-  uint32_t* on = a.out_nh + static_cast<size_t>(row) * N * a.words;
+  // labels -> dist row (kInf = unreachable) and first-hop row, coalesced (a
+  // neighbour row of a two-phase plan, row >= n_out: the distances alone)
+  uint32_t* od = dist_row(a.out_dist, a.scratch, a.n_out, N, row);
+  uint32_t* on = row < a.n_out ? a.out_nh + static_cast<size_t>(row) * N * a.words : nullptr;
   for (uint32_t i = tid; i < N; i += nthr) {
     const L l = lab[i];
     const uint32_t d = static_cast<uint32_t>(l >> kSh);
     __builtin_nontemporal_store(d == kDInf ? kInf : d, &od[i]);
     const uint32_t m = static_cast<uint32_t>(l & kMaskBits);
+    if (!on) continue;
     if (a.words == 1) {
       __builtin_nontemporal_store(m, &on[i]);
     } else {
@@ -2037,6 +2064,195 @@ __global__ __launch_bounds__(1024) void spf_lds_nh_kernel(SpfArgs a) {
       for (uint32_t k = 1; k < a.words; ++k) on[static_cast<size_t>(i) * a.words + k] = 0u;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// phase 1d: general metrics, many sources: multi-source Bellman-Ford in LDS
+// ---------------------------------------------------------------------------
+// The weighted counterpart of spf_msbfs_kernel. A workgroup holds the u16
+// distances of 4 sources for every node in LDS (8 bytes per node, two packed
+// u16 pairs) and relaxes them in pull form: per round each thread recomputes
+// its own nodes, d(v) = min(d(v), min over in-links (u, w) of d(u) + w), for
+// the 4 sources at once with packed 16-bit adds (saturating: 0xFFFF stays
+// "unreached") and packed minima. The in-links of a thread's nodes sit in
+// its registers ({u, w(u -> v)} per slot, a_wms layout, Cuthill-McKee ids),
+// so a round touches no global memory. Writes go in place (any value read
+// is a path length, so the fixpoint is the same in any order) and a round
+// without a change anywhere ends the search: the labels are then the
+// shortest distances of runSpf (LinkState.cpp:808-882) for positive metrics.
+// No transit through an overloaded node: a slot whose u is overloaded is dead,
+// except that an overloaded source still reaches its own neighbours (applied
+// once before the rounds). First hops: phase 2 over the u32 rows.
+// A label past 0xFFFF - 1 - max metric could hide a distance that does not fit
+// 16 bits: such a batch lists its rows in a.ovf_rows and the caller redoes
+// them (spf_lds_nh_kernel, u64 labels, fused first hops - phase 2 then
+// recomputes the same first hops).
+constexpr uint32_t kWmsOvl = 0x80000000u;  // slot flag: u is overloaded
+
+// packed u16 pairs: saturating add (v_pk_add_u16 clamp: 0xFFFF stays
+// "unreached") and minimum (v_pk_min_u16)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t pk_add_sat_u16(uint32_t a, uint32_t b) {
+  const u16x2 r = __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ inline uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  const u16x2 r = __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+  return __builtin_bit_cast(uint32_t, r);
+}
+
+// J <= 10 (N <= 10,240): at most 64 VGPRs, so two 1,024-thread batches share
+// a CU (8 waves per SIMD; their LDS, 2 x 80 KB, fits too)
+template <int K, int J>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(J <= 10 ? 8 : 1)))
+void spf_wms_kernel(SpfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr uint32_t S = 4;
+  const uint32_t N = a.n_nodes;
+  const uint32_t tid = threadIdx.x, B = blockDim.x;
+  const uint32_t b0 = blockIdx.x * S;
+  const uint32_t nsrc = min(S, a.n_rows - b0);
+  __shared__ uint32_t s_prog[3], s_ovf;
+  uint2* D = reinterpret_cast<uint2*>(lds);  // [N + 1]; D[N] stays unreached
+  for (uint32_t i = tid; i <= N; i += B) D[i] = make_uint2(~0u, ~0u);
+  if (tid < 3) s_prog[tid] = 0u;
+  if (tid == 0) s_ovf = 0u;
+  __syncthreads();
+  if (tid < nsrc) {  // sources may repeat: clear each lane's half alone
+    const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
+    uint32_t* w = reinterpret_cast<uint32_t*>(D + src) + (tid >> 1);
+    atomicAnd(w, (tid & 1u) ? 0x0000FFFFu : 0xFFFF0000u);
+  }
+  __syncthreads();
+  // the in-link slots of the owned nodes: {u (16 bits) | w (15 bits) << 16 |
+  // kWmsOvl}; an unused slot (no link, link down) reads u = N, the entry that
+  // stays unreached
+  uint32_t slot[J][K];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = j * B + tid;
+#pragma unroll
+    for (int k = 0; k < K; ++k) slot[j][k] = v < N ? a.wms_slots[static_cast<size_t>(v) * K + k] : N;
+  }
+  // an overloaded source reaches its neighbours and no further: a slot whose
+  // u is overloaded contributes w to the lanes where u is the source (label
+  // 0: only a source holds it, and this pass writes nothing below 1), once,
+  // and is dead from then on like every other slot of an overloaded node
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = j * B + tid;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!(slot[j][k] & kWmsOvl)) continue;
+      const uint32_t u = slot[j][k] & 0xFFFFu, w = (slot[j][k] >> 16) & 0x7FFFu;
+      slot[j][k] = N;
+      const uint2 du = D[u];
+      const uint32_t lz[4] = {du.x & 0xFFFFu, du.x >> 16, du.y & 0xFFFFu, du.y >> 16};
+      uint32_t c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = lz[q] == 0u ? w : 0xFFFFu;
+      uint2 d = D[v];  // v < N: a slot of a padding node is never flagged
+      d.x = pk_min_u16(d.x, c[0] | (c[1] << 16));
+      d.y = pk_min_u16(d.y, c[2] | (c[3] << 16));
+      D[v] = d;
+    }
+  }
+  __syncthreads();
+  // activity: a wave's slice j is the 64-node chunk c = v / 64 (Cuthill-McKee
+  // ids). A chunk whose nodes changed in round r sets its bit in chg[r % 3];
+  // in round r + 1 a slice is recomputed only if a chunk within the layout
+  // bandwidth of it (where all its in-links come from) changed in round r -
+  // a node whose in-neighbours all kept their labels since it was last
+  // recomputed cannot change. (A change later in the same round is seen in
+  // the next one.) Three rotating bitmaps: one read, one written, one cleared.
+  // ORH_WMS_NO_SKIP (A/B builds): every slice every round
+  const uint32_t nchunk = (N + 63) / 64, cw = (nchunk + 31) / 32;
+  uint32_t* chg = reinterpret_cast<uint32_t*>(D + N + 1);  // [3][cw]
+  for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
+  const uint32_t bw = a.ms_bw;
+  const uint32_t wave = tid >> 6;
+  __syncthreads();
+  for (uint32_t round = 1;; ++round) {
+    int prog = 0;
+    const uint32_t* prev = chg + ((round + 2u) % 3u) * cw;
+    uint32_t* cur = chg + (round % 3u) * cw;
+    if (tid < cw) chg[((round + 1u) % 3u) * cw + tid] = 0u;  // read in round - 1, written in round + 1
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint32_t v = j * B + tid;
+      const uint32_t c = __builtin_amdgcn_readfirstlane(j * (B >> 6) + wave);  // this slice's chunk
+#ifndef ORH_WMS_NO_SKIP
+      if (round > 1) {
+        const uint32_t lo = c * 64u > bw ? (c * 64u - bw) >> 6 : 0u;
+        const uint32_t hi = min(nchunk - 1u, (c * 64u + 63u + bw) >> 6);
+        bool act = false;
+        for (uint32_t w = lo >> 5; w <= (hi >> 5) && !act; ++w) {
+          uint32_t m = prev[w];
+          if (w == (lo >> 5)) m &= ~0u << (lo & 31u);
+          if (w == (hi >> 5) && (hi & 31u) != 31u) m &= (2u << (hi & 31u)) - 1u;
+          act = m != 0u;
+        }
+        if (!act) continue;
+      }
+#endif
+      if (v >= N) continue;
+      // opaque per round: the addresses and replicated weights are derived
+      // again each time instead of held in J * K more registers
+#pragma unroll
+      for (int k = 0; k < K; ++k) asm volatile("" : "+v"(slot[j][k]));
+      uint2 du[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) du[k] = D[slot[j][k] & 0xFFFFu];
+      const uint2 own = D[v];
+      uint2 acc = own;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        // {w, w}: the high half twice (an unused slot: w = 0 on the unreached entry)
+        const uint32_t wr = __builtin_amdgcn_perm(slot[j][k], slot[j][k], 0x03020302u);
+        acc.x = pk_min_u16(acc.x, pk_add_sat_u16(du[k].x, wr));
+        acc.y = pk_min_u16(acc.y, pk_add_sat_u16(du[k].y, wr));
+      }
+      const bool changed = acc.x != own.x || acc.y != own.y;
+      if (changed) {
+        D[v] = acc;
+        prog = 1;
+      }
+      if (__builtin_amdgcn_ballot_w64(changed) && (tid & 63u) == 0u) atomicOr(&cur[c >> 5], 1u << (c & 31u));
+    }
+    if (prog) s_prog[round % 3u] = 1u;
+    lds_barrier();
+    if (!s_prog[round % 3u]) break;
+    if (tid == 0) s_prog[(round + 2u) % 3u] = 0u;
+  }
+  // rows out in host order (coalesced), a u16 label widened to u32; a label
+  // within max metric of 0xFFFF may stand for a distance that did not fit
+  const uint32_t lim = a.wms_limit;
+  uint32_t* out[S];
+#pragma unroll
+  for (uint32_t k = 0; k < S; ++k)
+    out[k] = k < nsrc ? dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + k]) : nullptr;
+  bool ovf = false;
+  for (uint32_t i = tid; i < N; i += B) {
+    const uint2 d = D[a.dev_of[i]];
+    const uint32_t l[S] = {d.x & 0xFFFFu, d.x >> 16, d.y & 0xFFFFu, d.y >> 16};
+#pragma unroll
+    for (uint32_t k = 0; k < S; ++k) {
+      if (k >= nsrc) break;
+      ovf |= l[k] != 0xFFFFu && l[k] > lim;
+      __builtin_nontemporal_store(l[k] == 0xFFFFu ? kInf : l[k], &out[k][i]);
+    }
+  }
+  if (ovf) s_ovf = 1u;
+  __syncthreads();
+  if (s_ovf && tid < nsrc) {
+    const uint32_t k = atomicAdd(&a.ovf_rows[0], 1u);
+    a.ovf_rows[1 + k] = a.order[b0 + tid];
+  }
+}
+
+size_t wms_lds_bytes(uint32_t n_nodes) {
+  const size_t cw = (static_cast<size_t>(n_nodes) + 63) / 64 / 32 + 1;
+  return (static_cast<size_t>(n_nodes) + 1) * 8 + 3 * cw * 4;  // labels, then the chunk-change bitmaps
 }
 
 size_t lds_nh_bytes(uint32_t n_nodes, bool packed) {
@@ -3006,6 +3222,43 @@ hipError_t launch_spf_lds_nh(SpfArgs a, uint32_t n_rows, uint32_t ell_k, bool pa
   const size_t lds = lds_nh_bytes(a.n_nodes, false);
   return ell_k == 8 ? launch(spf_lds_nh_kernel<8, false>, a, n_rows, block, lds, s)
                     : launch(spf_lds_nh_kernel<4, false>, a, n_rows, block, lds, s);
+}
+
+template <int K>
+static hipError_t launch_wms_k(const SpfArgs& a, uint32_t batches, size_t lds, hipStream_t s) {
+  const uint32_t j = (a.n_nodes + 1023) / 1024;
+  switch (j <= 2 ? 2 : j <= 4 ? 4 : j <= 6 ? 6 : j <= 8 ? 8 : j <= 10 ? 10 : j <= 12 ? 12 : j <= 16 ? 16 : 20) {
+    case 2: return launch(spf_wms_kernel<K, 2>, a, batches, 1024, lds, s);
+    case 4: return launch(spf_wms_kernel<K, 4>, a, batches, 1024, lds, s);
+    case 6: return launch(spf_wms_kernel<K, 6>, a, batches, 1024, lds, s);
+    case 8: return launch(spf_wms_kernel<K, 8>, a, batches, 1024, lds, s);
+    case 10: return launch(spf_wms_kernel<K, 10>, a, batches, 1024, lds, s);
+    case 12: return launch(spf_wms_kernel<K, 12>, a, batches, 1024, lds, s);
+    case 16: return launch(spf_wms_kernel<K, 16>, a, batches, 1024, lds, s);
+    default: return launch(spf_wms_kernel<K, 20>, a, batches, 1024, lds, s);
+  }
+}
+
+hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  if (!a.ovf_rows || !a.wms_slots || a.n_nodes > 20480 || a.n_nodes >= 0xFFFFu) return hipErrorInvalidValue;
+  a.n_rows = n_rows;
+  a.row_list = nullptr;
+  a.row_count = nullptr;
+  hipError_t e = hipMemsetAsync(a.ovf_rows, 0, 4, s);
+  if (e != hipSuccess) return e;
+  const uint32_t batches = (n_rows + 3) / 4;
+  const size_t lds = wms_lds_bytes(a.n_nodes);
+  e = wms_k == 8 ? launch_wms_k<8>(a, batches, lds, s) : launch_wms_k<4>(a, batches, lds, s);
+  if (e != hipSuccess) return e;
+  // rows whose distances may not fit 16 bits: the u64 LDS search over the
+  // list (workgroups past its length exit at once); its first-hop rows are
+  // rewritten, identically, by phase 2
+  a.row_list = a.ovf_rows + 1;
+  a.row_count = a.ovf_rows;
+  const size_t lds64 = lds_nh_bytes(a.n_nodes, false);
+  return a.recs_k == 8 ? launch(spf_lds_nh_kernel<8, false>, a, n_rows, 256, lds64, s)
+                       : launch(spf_lds_nh_kernel<4, false>, a, n_rows, 256, lds64, s);
 }
 
 hipError_t launch_spf(const SpfPlan& plan, SpfArgs a, uint32_t n_rows, hipStream_t s) {

@@ -121,6 +121,12 @@ struct orh_graph {
   uint2* d_ms_recs = nullptr;
   uint32_t* d_ms_dev_of = nullptr;
   uint32_t* d_ms_host_of = nullptr;
+  // multi-source Bellman-Ford (kWms): in-link slots per Cuthill-McKee node,
+  // rebuilt with the multi-source layout; wms_ok: the graph qualifies (every
+  // degree <= 8, metrics < 2^15, N < 20,481); wms_k slots per node (4 or 8)
+  uint32_t* d_wms = nullptr;
+  bool wms_dirty = true, wms_ok = false;
+  uint32_t wms_maxw = 0, wms_k = 4;
   std::vector<int32_t> row_of;  // scratch for orh_spf_run (all -1 between calls)
   // orh_spf_run's staged request on this graph (sources, ignore sets,
   // neighbour rows, batch order), keyed by the request: a repeated sweep
@@ -174,6 +180,9 @@ void free_graph_device(orh_graph* g) {
   g->d_ms_dev_of = nullptr;
   g->d_ms_host_of = nullptr;
   g->ms_dirty = true;
+  (void)hipFree(g->d_wms);
+  g->d_wms = nullptr;
+  g->wms_dirty = true;
   g->d_recs = nullptr;
   g->d_link = nullptr;
   g->d_rank_out = nullptr;
@@ -360,6 +369,50 @@ int sync_ms_layout(orh_graph* g) {
   return ORH_OK;
 }
 
+// kWms in-link slots: per Cuthill-McKee node dv, ell_k slots {u | w(u -> v)
+// << 16 | overloaded(u) << 31}, u the Cuthill-McKee id of the neighbour and
+// w the metric of the link from u's side (LinkState.cpp:851-852: the search
+// relaxes getMetricFromNode(u)); a down link or an unused slot is u = N
+int sync_wms_layout(orh_graph* g) {
+  if (!g->wms_dirty) return ORH_OK;
+  int rc = sync_ms_layout(g);
+  if (rc) return rc;
+  const uint32_t N = g->n_nodes;
+  uint32_t maxdeg = 0;
+  for (uint32_t v = 0; v < N; ++v) maxdeg = std::max(maxdeg, g->row_ptr[v + 1] - g->row_ptr[v]);
+  const uint32_t K = maxdeg <= 4 ? 4u : 8u;  // slots per node (its own width, not the ELL's)
+  g->wms_k = K;
+  g->wms_ok = N > 0 && N <= 20480 && maxdeg <= 8;
+  g->wms_maxw = 0;
+  std::vector<uint32_t> slots;
+  if (g->wms_ok) {
+    slots.assign(static_cast<size_t>(N) * K, N);
+    for (uint32_t dv = 0; dv < N && g->wms_ok; ++dv) {
+      const uint32_t v = g->ms_host_of[dv];
+      uint32_t k = 0;
+      for (uint32_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; ++e, ++k) {
+        if (g->meta[e] & ORH_META_DOWN) continue;
+        const uint32_t w = g->w_in[e], u = g->col[e];
+        if (w == 0 || w > 0x7FFFu) {
+          g->wms_ok = false;
+          break;
+        }
+        g->wms_maxw = std::max(g->wms_maxw, w);
+        slots[static_cast<size_t>(dv) * K + k] = g->ms_dev_of[u] | (w << 16) | (g->overloaded[u] ? 0x80000000u : 0u);
+      }
+    }
+  }
+  if (g->wms_ok) {
+    orh_ctx* ctx = g->ctx;
+    if (!g->d_wms) ORH_HIP(ctx, hipMalloc(&g->d_wms, static_cast<size_t>(N) * 8 * sizeof(uint32_t)));
+    ORH_HIP(ctx, hipMemcpyAsync(g->d_wms, slots.data(), slots.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                ctx->stream));
+    ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // slots is a local
+  }
+  g->wms_dirty = false;
+  return ORH_OK;
+}
+
 uint64_t next_graph_gen() {
   static std::atomic<uint64_t> gen{0};
   return ++gen;
@@ -393,6 +446,7 @@ int upload_records(orh_graph* g, const std::vector<std::pair<uint32_t, uint32_t>
                                         ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
   g->ms_dirty = true;
+  g->wms_dirty = true;
   return ORH_OK;
 }
 
@@ -927,6 +981,7 @@ int orh_graph_apply_delta(orh_graph* g, uint32_t n_rows, const uint32_t* rows, c
     ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));  // staging is a local
   }
   g->ms_dirty = true;
+  g->wms_dirty = true;
   g->gen = next_graph_gen();  // staged requests hold neighbour lists of the old rows
   return ORH_OK;
 }
@@ -1971,13 +2026,50 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   // which also search every neighbour row and then stream 1 + deg rows per
   // source. ORH_LDS_NH=0: the two-phase plan (A/B); orh_set_spf_mode(1)
   // (per-source) keeps it too
+  // many sources, general metrics, a graph whose in-links fit the ELL rows:
+  // 4-source Bellman-Ford batches in LDS (spf_wms_kernel), then the first
+  // hops over the u32 rows (phase 2). ORH_WMS=0 off (A/B); ORH_WMS_MIN: the
+  // fewest requested sources that take it (default 256: below, the fused
+  // per-source search, which needs no neighbour rows, is the better plan)
+  bool wms = false;
+  {
+    static const bool on = [] {
+      const char* e = getenv("ORH_WMS");
+      return !(e && e[0] == '0');
+    }();
+    static const uint32_t wms_min = [] {
+      const char* e = getenv("ORH_WMS_MIN");
+      return e ? static_cast<uint32_t>(atoi(e)) : 256u;
+    }();
+    if (on && ctx->spf_mode == orh::SpfMode::kAuto && !uniform && !has_ign && n_src >= wms_min &&
+        (plan.variant == orh::SpfVariant::kDist16 || plan.variant == orh::SpfVariant::kDist32) &&
+        orh::wms_lds_bytes(N) <= ctx->lds_limit && orh::lds_nh_bytes(N, false) <= ctx->lds_limit) {
+      int rc = sync_wms_layout(g);
+      if (rc) return rc;
+      if (g->wms_ok) {
+        wms = true;
+        run_plan.variant = orh::SpfVariant::kWms;
+        rc = ensure_labels(ctx, (static_cast<size_t>(n_rows) + 2) / 2 + 1);  // the overflow row list
+        if (rc) return rc;
+      }
+    }
+  }
+  // A few sources without ignore sets keep the two-phase LDS plan: a lone
+  // search pays the fused kernel's per-bucket barriers with nothing beside it
+  // (C2's buildRouteDb after a metric change: spf(me) 1.15 ms fused against
+  // ~0.6 two-phase, profiles/r06/e_bench_phases.json); ORH_LDS_NH_MIN (32)
   bool lds_nh_packed = false;
   {
     static const bool on = [] {
       const char* e = getenv("ORH_LDS_NH");
       return !(e && e[0] == '0');
     }();
-    if (on && ctx->spf_mode == orh::SpfMode::kAuto && !uniform && max_nbr <= 32 &&
+    static const uint32_t lds_nh_min = [] {
+      const char* e = getenv("ORH_LDS_NH_MIN");
+      return e ? static_cast<uint32_t>(atoi(e)) : 32u;
+    }();
+    if (on && !wms && (has_ign || n_src >= lds_nh_min) && ctx->spf_mode == orh::SpfMode::kAuto && !uniform &&
+        max_nbr <= 32 &&
         (plan.variant == orh::SpfVariant::kDist16 || plan.variant == orh::SpfVariant::kDist32) &&
         orh::lds_nh_bytes(N, false) <= ctx->lds_limit) {
       run_plan.variant = orh::SpfVariant::kLdsNh;
@@ -2052,7 +2144,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.delta = uniform ? w0
                     : std::max<uint32_t>(1u, static_cast<uint32_t>(
                                                  static_cast<uint64_t>(g->mean_out) * ctx->delta_pct / 100u));
-  if (run_plan.variant == orh::SpfVariant::kLdsNh) {
+  if (run_plan.variant == orh::SpfVariant::kLdsNh || run_plan.variant == orh::SpfVariant::kWms) {
     // ORH_LDS_NH_DELTA_PCT: bucket width of the LDS search in % of the mean
     // live metric. Its relaxations cost LDS latency, not a global atomic, so
     // wider buckets (fewer bucket barriers) pay: C2w sweep 45.5 / 30.8 / 28.9 /
@@ -2106,10 +2198,18 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     hipError_t pre = hipGetLastError();
     if (pre != hipSuccess) { std::string m = "pending HIP error before spf launch (variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + ")"; return hip_fail(ctx, pre, m.c_str()); }
   }
-  if (run_plan.variant == orh::SpfVariant::kLdsNh)
+  if (run_plan.variant == orh::SpfVariant::kLdsNh || run_plan.variant == orh::SpfVariant::kWms)
     a.ovf_rows = reinterpret_cast<uint32_t*>(ctx->d_labels);
+  if (run_plan.variant == orh::SpfVariant::kWms) {
+    a.dev_of = g->d_ms_dev_of;
+    a.wms_slots = g->d_wms;
+    a.wms_limit = 0xFFFEu - g->wms_maxw;
+    a.ms_bw = g->ms_bw_layout;  // the in-links' reach in Cuthill-McKee ids (activity skip)
+    a.recs_k = g->ell_k;
+  }
   hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
       ? orh::launch_spf_lds_nh(a, n_rows, g->ell_k, lds_nh_packed, run_plan.block, ctx->stream)
+      : run_plan.variant == orh::SpfVariant::kWms ? orh::launch_spf_wms(a, n_rows, g->wms_k, ctx->stream)
       : orh::launch_spf(run_plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) { std::string m = "spf kernel launch variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + " lds " + std::to_string(run_plan.lds_bytes) + " block " + std::to_string(run_plan.block) + " j " + std::to_string(run_plan.ms_j); return hip_fail(ctx, e, m.c_str()); }
 #ifdef ORH_DIAG_STAMPS

@@ -89,6 +89,32 @@ def test_multi_device_replicas_follow_mutations(hip):
         assert np.array_equal(dist[i], want), names[i]
 
 
+def test_replicas_share_one_host_store(hip):
+    """Replicas 1.. are device views of replica 0's host graph store: a
+    mutation is applied once, through the primary (a replica refuses one),
+    and reaches every replica - new nodes and links included."""
+    adj, _ = bench_grid(6)
+    rls = _replicated(hip, adj[:30], [0, 0, 0])
+    with pytest.raises(RuntimeError):
+        rls.replica(1).update_adjacency_database(adj[0].to_wire())
+    for db in adj[30:]:
+        rls.update_adjacency_database(db.to_wire())
+    names = [str(i) for i in range(36)]
+    for r in range(3):
+        assert rls.replica(r).node_names() == rls.replica(0).node_names()
+    sw = rls.sweep(names, True)
+    sw.run()
+    sw.sync()
+    dist, _ = sw.gather()
+    order = rls.replica(0).node_names()
+    pos = {v: i for i, v in enumerate(order)}
+    for i, s in enumerate(names):  # unit grid: Manhattan distances, every block
+        r0, c0 = divmod(int(s), 6)
+        want = [abs(r0 - int(v) // 6) + abs(c0 - int(v) % 6) for v in order]
+        assert list(dist[i]) == want, s
+    assert pos
+
+
 def test_multi_device_sweep_clos_weighted(hip):
     """C3 Clos: blocks cut by work (1 + links / 16 per source), so the 288
     spines (84 links each) do not all land in one block."""

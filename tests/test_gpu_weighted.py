@@ -1,10 +1,13 @@
-"""Weighted all-sources sweeps (general integer metrics) on the fused LDS
-search spf_lds_nh_kernel (ORH_VARIANT_LDS_NH): {dist, first-hop mask} labels
-in LDS, the first hops carried through the search (LinkState.cpp:808-882,
-:857-873), one workgroup per source.
+"""Weighted sweeps (general integer metrics), LinkState::runSpf semantics
+(LinkState.cpp:808-882, first hops :857-873), on the two LDS plans:
+  spf_wms_kernel (ORH_VARIANT_WMS, >= 256 sources): 4-source Bellman-Ford
+      batches with u16 labels in LDS, then the first-hop phase over u32 rows
+  spf_lds_nh_kernel (ORH_VARIANT_LDS_NH, fewer sources or ignore sets):
+      {dist, first-hop mask} labels in LDS, first hops fused, one workgroup per
+      source
 
-  C2w 100x100 grid, metrics 1..64      all 10,000 rows vs the fast checker,
-                                       200 of them vs the faithful oracle
+  C2w 100x100 grid, metrics 1..64      all 10,000 rows (WMS) vs the fast
+                                       checker, 200 of them vs the oracle
   packed labels past 16 bits           a ladder at metric 30,000: every row
                                        overflows the u32 label and is redone
                                        with u64 labels
@@ -25,7 +28,7 @@ from openr_amd.types import K_TESTING_AREA
 
 pytestmark = pytest.mark.gpu
 A = K_TESTING_AREA
-LDS_NH = 12  # ORH_VARIANT_LDS_NH
+LDS_NH, WMS = 12, 13  # ORH_VARIANT_LDS_NH, ORH_VARIANT_WMS
 
 
 def _compare_rows(sweep, names, rows, dist_w, nh_w, label):
@@ -57,7 +60,7 @@ def test_c2w_sweep_all_rows_vs_checker(hip, oracle):
     sw.run()
     sw.sync()
     info = sw.info()
-    assert info["variant"] == LDS_NH and info["rows"] == len(names) and info["hop_nodes"] == 0, info
+    assert info["variant"] == WMS and info["rows"] == len(names) and info["hop_nodes"] == 1, info
     als_o, _ = load_topology(oracle, adj, [])
     fc = oracle.module.FastChecker(als_o[A]._impl, order)
     ids = {n: i for i, n in enumerate(order)}
@@ -84,19 +87,22 @@ def _random_weighted(seed, n, extra, max_metric):
                            overload=0.05, link_overload=0.02)
 
 
-def _all_rows_vs_oracle(hip, oracle, dbs, expect_variant=LDS_NH):
+def _all_rows_vs_oracle(hip, oracle, dbs, expect_variant=LDS_NH, repeat=1):
     als_h, _ = load_topology(hip, dbs, [])
     als_o, _ = load_topology(oracle, dbs, [])
     ls = als_h[A]._impl
     order = ls.node_names()
-    names = sorted(db.thisNodeName for db in dbs)
+    names = sorted(db.thisNodeName for db in dbs) * repeat  # repeat: >= 256 rows take the WMS plan
     sw = ls.sweep(names, True)
     sw.run()
     sw.sync()
     info = sw.info()
     assert info["variant"] == expect_variant, info
-    dist_o, nh_o = als_o[A]._impl.spf_tables(names, order, [ls.neighbors(s) for s in names], 16)
-    _compare_rows(sw, names, list(range(len(names))), dist_o, nh_o, "oracle")
+    uniq = sorted(set(names))
+    dist_o, nh_o = als_o[A]._impl.spf_tables(uniq, order, [ls.neighbors(s) for s in uniq], 16)
+    at = {s: k for k, s in enumerate(uniq)}
+    _compare_rows(sw, names, list(range(len(names))), dist_o[[at[s] for s in names]],
+                  nh_o[[at[s] for s in names]], "oracle")
     return info
 
 
@@ -115,6 +121,28 @@ def test_random_weighted_all_rows(hip, oracle, seed):
     rows, packed labels (degree <= 16)."""
     dbs = _random_weighted(seed, n=250, extra=600, max_metric=20)
     _all_rows_vs_oracle(hip, oracle, dbs)
+
+
+@pytest.mark.parametrize("seed", [85, 86])
+def test_random_weighted_wms(hip, oracle, seed):
+    """The same kind of graph (parallel links, overloaded nodes - sources
+    among them - and drained links), every node twice as a source: the WMS
+    batches (repeated sources inside a batch, overloaded sources reaching
+    only their neighbours), all rows vs the oracle."""
+    dbs = _random_weighted(seed, n=250, extra=250, max_metric=30)
+    for db in dbs:  # WMS needs every in-link in the ELL row: cap the degree
+        db.adjacencies = db.adjacencies[:8]
+    info = _all_rows_vs_oracle(hip, oracle, dbs, expect_variant=WMS, repeat=2)
+    assert info["rows"] >= 500
+
+
+def test_wms_overflow_redone(hip, oracle):
+    """Ladder at metric 20,000: distances pass 16 bits within a few rungs, so
+    every WMS batch flags its rows and the u64 LDS search redoes them."""
+    dbs, _ = ladder(130, metric=20_000)
+    for db in dbs[::5]:
+        db.adjacencies[0].metric = 19_999
+    _all_rows_vs_oracle(hip, oracle, dbs, expect_variant=WMS, repeat=2)
 
 
 def test_many_neighbours_u64_labels(hip, oracle):
@@ -149,7 +177,7 @@ def test_many_neighbours_u64_labels(hip, oracle):
 def test_ignore_sets_lds_nh(hip, oracle):
     """Per-source ignore sets through the fused LDS search: runSpf(src, true,
     {links}) for a batch the what-if repair does not take (repair off)."""
-    dbs = _random_weighted(83, n=300, extra=500, max_metric=15)
+    dbs = _random_weighted(83, n=250, extra=500, max_metric=15)
     als_h, _ = load_topology(hip, dbs, [])
     als_o, _ = load_topology(oracle, dbs, [])
     mod = host_module()

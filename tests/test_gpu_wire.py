@@ -233,6 +233,9 @@ def test_nexthop_list_order_after_linkset_rehash(hip, oracle):
             fwd.ifName, fwd.otherIfName = a.ifName + tag, a.otherIfName + tag
             rev.ifName, rev.otherIfName = back.ifName + tag, back.otherIfName + tag
             fwd.metric = rev.metric = 5 + i
+            # no adjacency label: a repeated one is a duplicate MPLS route,
+            # which the reference CHECK-fails on (Decision.h:115-118)
+            fwd.adjLabel = rev.adjLabel = 0
             by_name[me].adjacencies.append(fwd)
             peer.adjacencies.append(rev)
             for als in (als_h, als_o):
