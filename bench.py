@@ -186,12 +186,26 @@ def main():
     probe = next((sw for _, srcs, _, sw in sweeps if sw is not None and len(srcs) == n * n),
                  next((sw for *_, sw in sweeps if sw is not None), None))
     kernel_ms, phases = [], []
+    step_plan = None
     if probe is not None:
         for _ in range(max(3, min(args.steps, 10))):
             probe.run()
             kernel_ms.append(probe.last_ms())
             phases.append(probe.phase_ms())
         probe_info = probe.info()
+        # the same sweep alone on the plan the timed step's overlapping sweeps
+        # run (8-wave batches: ORH_MS_BLOCK=512 turns the lone-sweep plan off)
+        os.environ["ORH_MS_BLOCK"] = "512"
+        try:
+            sp_ms, sp_ph = [], []
+            for _ in range(max(3, min(args.steps, 10))):
+                probe.run()
+                sp_ms.append(probe.last_ms())
+                sp_ph.append(probe.phase_ms())
+            step_plan = (statistics.mean(sp_ms), [round(statistics.mean(p[i] for p in sp_ph), 4) for i in (0, 1)],
+                         probe.info())
+        finally:
+            del os.environ["ORH_MS_BLOCK"]
 
     value = total_units * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -266,6 +280,13 @@ def main():
                               "batch_sources": probe_info.get("batch_sources")},
                      "phase_ms": [round(statistics.mean(p[0] for p in phases), 4),
                                   round(statistics.mean(p[1] for p in phases), 4)],
+                     # the probe above runs the lone-sweep plan (nothing else in
+                     # flight); the step's sweeps run this one
+                     "step_plan_sweep": None if step_plan is None else {
+                         "kernel_ms": round(step_plan[0], 4), "phase_ms": step_plan[1],
+                         "ms_threads": step_plan[2].get("ms_threads"),
+                         "achieved": round(per_launch / (step_plan[0] * 1e-3) / 1e9, 1),
+                         "frac": round(per_launch / (step_plan[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
                      "algorithmic_bytes_per_source": bytes_per_source,
                      "sources_per_launch": srcs_probe,
                      "output_floor": {"bytes": out_bytes,
@@ -333,7 +354,8 @@ def main():
 
 # newest committed PMC summary of this command (tools/profile.sh +
 # tools/pmc_summary.py), per sweep launch
-PMC_PROFILES = [os.path.join(ROOT, "profiles", "r05", "pmc.json"),
+PMC_PROFILES = [os.path.join(ROOT, "profiles", "r06", "pmc.json"),
+                os.path.join(ROOT, "profiles", "r05", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r04", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r03", "pmc.json"),
                 os.path.join(ROOT, "profiles", "r02", "pmc.json"),
@@ -473,6 +495,15 @@ def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
     k = max(args.cpu_sample, 2 * threads)
     sample_mt = [str((i * (n * n)) // k) for i in range(k)]
     secn, _ = ls._impl.time_spf_sources(sample_mt, threads)
+    # the rate per thread count (how the 16 threads scale: allocator
+    # contention vs box noise), on the same evenly spaced sample
+    by_threads = {}
+    for t in sorted({2, 4, 8, threads} - {1}):
+        if t > threads:
+            continue
+        kt = max(args.cpu_sample, 2 * t)
+        st, _ = ls._impl.time_spf_sources([str((i * (n * n)) // kt) for i in range(kt)], t)
+        by_threads[t] = round(kt / st, 2)
     solver = oracle.spf_solver("1", True)
     db = adj_dbs[n * n // 2]
     flips = [0]
@@ -495,6 +526,8 @@ def cpu_baseline(args, adj_dbs, prefixes, n, gpu_value):
                                    f"use: affinity {len(os.sched_getaffinity(0))}, cgroup quota "
                                    f"{cgroup_cpu_quota()}), one deep LinkState copy per thread"},
         "cpu_baseline_per_core": round(vn / threads, 2),
+        "cpu_baseline_by_threads": {"1": round(v1, 2), **{str(t): r for t, r in by_threads.items()},
+                                    "note": "SPF-sources/s by oracle thread count, same box and sample"},
         "cpu_baseline_all_cores_linear": {
             "value": round(vn / threads * (os.cpu_count() or threads), 1),
             "cores": os.cpu_count(),

@@ -15,6 +15,8 @@
 #include <initializer_list>
 #include <iterator>
 #include <memory>
+#include <mutex>
+#include <new>
 #include <type_traits>
 #include <cstdlib>
 #include <cstring>
@@ -329,6 +331,135 @@ struct RibMplsEntry {
   bool operator!=(const RibMplsEntry& o) const { return !(*this == o); }
 };
 
+// Fixed-size block pool for the route maps' nodes. A route build allocates
+// one map node per route (C5: 1M) and the previous database frees as many;
+// through malloc that was most of a build's merge (~250-400 ns a node, much
+// of it the allocator's bins and first-touched pages). Here a block comes off
+// the calling thread's free list (or a chunk it carves), and a free pushes it
+// onto the freeing thread's list; a list past kLocalMax hands a batch to a
+// global stack the others draw from, so blocks that one thread frees and
+// another allocates circulate instead of piling up. Chunks live as long as
+// the process (freed blocks are reused, never returned: the footprint is the
+// peak of the live routes, as with ORH_MALLOC_TUNE's untrimmed arenas).
+// ORH_NODE_POOL=0 (A/B; read once per process): plain operator new / delete
+inline bool nodePoolOn() {
+  static const bool on = [] {
+    const char* e = std::getenv("ORH_NODE_POOL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <size_t Size, size_t Align>
+class FixedPool {
+ public:
+  static void* alloc() {
+    if (!nodePoolOn()) return ::operator new(kBlock, std::align_val_t(kAlign));
+    Local& l = local();
+    if (!l.head) refill(l);
+    Block* b = l.head;
+    l.head = b->next;
+    --l.count;
+    return b;
+  }
+  static void free(void* p) noexcept {
+    if (!nodePoolOn()) {
+      ::operator delete(p, std::align_val_t(kAlign));
+      return;
+    }
+    Local& l = local();
+    Block* b = static_cast<Block*>(p);
+    b->next = l.head;
+    l.head = b;
+    if (++l.count > kLocalMax) spill(l, kLocalMax / 2);
+  }
+
+ private:
+  struct Block {
+    Block* next;
+  };
+  static constexpr size_t kAlign = Align < 16 ? 16 : Align;
+  static constexpr size_t kBlock = ((Size < sizeof(Block) ? sizeof(Block) : Size) + Align - 1) / Align * Align;
+  static constexpr size_t kChunk = (size_t{1} << 20) / kBlock * kBlock;  // ~1 MB of blocks
+  static constexpr size_t kLocalMax = 1u << 16, kBatch = 1u << 12;
+  struct Local {
+    Block* head = nullptr;
+    size_t count = 0;
+    ~Local() { spill(*this, count); }  // a thread's blocks outlive it
+  };
+  struct Global {
+    std::mutex mu;
+    std::vector<std::pair<Block*, size_t>> batches;  // singly linked runs
+  };
+  static Global& global() {
+    static Global* g = new Global;  // never destroyed: maps may outlive static teardown
+    return *g;
+  }
+  static Local& local() {
+    static thread_local Local l;
+    return l;
+  }
+  static void spill(Local& l, size_t n) noexcept {
+    if (!n || !l.head) return;
+    Block* first = l.head;
+    Block* last = first;
+    size_t k = 1;
+    while (k < n && last->next) {
+      last = last->next;
+      ++k;
+    }
+    l.head = last->next;
+    l.count -= k;
+    last->next = nullptr;
+    Global& g = global();
+    std::lock_guard<std::mutex> lock(g.mu);
+    g.batches.emplace_back(first, k);
+  }
+  static void refill(Local& l) {
+    {
+      Global& g = global();
+      std::lock_guard<std::mutex> lock(g.mu);
+      if (!g.batches.empty()) {
+        l.head = g.batches.back().first;
+        l.count = g.batches.back().second;
+        g.batches.pop_back();
+        return;
+      }
+    }
+    char* c = static_cast<char*>(::operator new(kChunk, std::align_val_t(kAlign)));
+    for (size_t off = kChunk; off >= kBlock; off -= kBlock) {
+      Block* b = reinterpret_cast<Block*>(c + off - kBlock);
+      b->next = l.head;
+      l.head = b;
+      ++l.count;
+    }
+  }
+};
+
+// std::allocator for arrays (bucket tables), FixedPool for single nodes
+template <class T>
+struct PoolAlloc {
+  using value_type = T;
+  PoolAlloc() noexcept = default;
+  template <class U>
+  PoolAlloc(const PoolAlloc<U>&) noexcept {}  // NOLINT: rebinding
+  T* allocate(size_t n) {
+    if (n != 1) return std::allocator<T>().allocate(n);
+    return static_cast<T*>(FixedPool<sizeof(T), alignof(T)>::alloc());
+  }
+  void deallocate(T* p, size_t n) noexcept {
+    if (n != 1) {
+      std::allocator<T>().deallocate(p, n);
+      return;
+    }
+    FixedPool<sizeof(T), alignof(T)>::free(p);
+  }
+  template <class U>
+  bool operator==(const PoolAlloc<U>&) const noexcept { return true; }
+  template <class U>
+  bool operator!=(const PoolAlloc<U>&) const noexcept { return false; }
+};
+
 // The route maps of a DecisionRouteDb (Decision.h:78-119: unordered maps keyed
 // by prefix / label) as kShards hash shards, each an std::unordered_map. A
 // route build fills per-worker shard sets and merges them shard by shard on
@@ -339,7 +470,7 @@ template <class K, class V, class H = std::hash<K>>
 class ShardedMap {
  public:
   static constexpr size_t kShards = 64;
-  using Shard = std::unordered_map<K, V, H>;
+  using Shard = std::unordered_map<K, V, H, std::equal_to<K>, PoolAlloc<std::pair<const K, V>>>;
   using value_type = typename Shard::value_type;
   // maps at least this large are freed shard by shard on the worker pool
   static constexpr size_t kParallelFree = 1u << 16;

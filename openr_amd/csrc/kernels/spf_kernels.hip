@@ -502,12 +502,12 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     if (v < N) vis[j] = f_cur[v];  // level 0: the sources
     if (kLog) log_events(j, v < N ? vis[j] : V(0), 0u);
   }
-  // wave-uniform bit j: some lane of this wave owns, in slice j, a node with
-  // an overflow list / an overloaded node. Both are rare (none on C2), so the
-  // per-node tests below sit behind one scalar test instead of per-lane exec
-  // masks built from bit masks the compiler keeps in spilled SGPR lanes
-  // (ORH_MS_NO_WAVE_UNIFORM, A/B builds: the per-lane tests alone)
-#ifndef ORH_MS_NO_WAVE_UNIFORM
+  // ORH_MS_WAVE_UNIFORM (A/B builds): wave-uniform bit j, some lane of this
+  // wave owns, in slice j, a node with an overflow list / an overloaded node,
+  // tested before the per-lane tests. Measured slower: the kernel grew from 89
+  // to 107 VGPRs and the 2-lane step from 23.0 to 26.5 ms
+  // (profiles/r06/g_ms_ab.txt), so the per-lane tests stay alone
+#ifdef ORH_MS_WAVE_UNIFORM
   uint32_t wovf = 0u, wovl = 0u;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
@@ -2101,11 +2101,16 @@ __device__ inline uint32_t pk_min_u16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, r);
 }
 
-// J <= 10 (N <= 10,240): at most 64 VGPRs, so two 1,024-thread batches share
-// a CU (8 waves per SIMD; their LDS, 2 x 80 KB, fits too)
+// ORH_WMS_OCC2 (A/B builds): J <= 10 capped at 64 VGPRs so two 1,024-thread
+// batches share a CU (their LDS, 2 x 80 KB, fits). Measured slower on C2w
+// (profiles/r06/g_c2w_*), so one batch per CU
+#ifdef ORH_WMS_OCC2
+#define ORH_WMS_ATTR __attribute__((amdgpu_waves_per_eu(J <= 10 ? 8 : 1)))
+#else
+#define ORH_WMS_ATTR
+#endif
 template <int K, int J>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(J <= 10 ? 8 : 1)))
-void spf_wms_kernel(SpfArgs a) {
+__global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   constexpr uint32_t S = 4;
   const uint32_t N = a.n_nodes;
