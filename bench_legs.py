@@ -92,10 +92,11 @@ def leg_c2w(hip, cpu, reps=10):
         sw.run()
     sw.sync()
     dt = (time.perf_counter() - t0) / reps
-    dev = []
+    dev, ph = [], []
     for _ in range(5):
         sw.run()
         dev.append(sw.last_ms())
+        ph.append(sw.phase_ms())
     kms = statistics.median(dev)
     N, E, W = sw.nodes, sw.edges, sw.words
     b_src = 4 * (N + 1) + 8 * E + N * (4 + 4 * W)
@@ -105,6 +106,8 @@ def leg_c2w(hip, cpu, reps=10):
            "sweep_spf_sources_per_s": round(len(names) / dt, 1),
            "sweep_ms": round(dt * 1e3, 3),
            "kernel_ms": round(kms, 3),
+           "phase_ms": {"distances": round(statistics.median(p[0] for p in ph), 3),
+                        "first_hops": round(statistics.median(p[1] for p in ph), 3)},
            "plan": {"variant": info["variant"], "rows": info["rows"]},
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
                         "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_source": b_src,

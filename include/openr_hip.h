@@ -172,6 +172,8 @@ typedef struct orh_spf_info {
   uint32_t batch_sources; /* MS-BFS: sources per workgroup (<= mask_bits), else 0 */
   uint32_t ms_threads;    /* MS-BFS: threads per workgroup (1024: the latency plan), else 0 */
   uint32_t ms_skip;       /* MS-BFS: interval skip on (latency plan or ORH_MS_SKIP=1) */
+  uint32_t ms_direct;     /* MS-BFS / WMS: the node layout kept the host order (MS-BFS: rows
+                             written by the search kernel, no finalize pass) */
 } orh_spf_info;
 int orh_last_spf_info(const orh_ctx* ctx, orh_spf_info* out);
 /* device time (HIP events on the context stream) of the last orh_spf_run;

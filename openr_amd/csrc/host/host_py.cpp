@@ -444,6 +444,7 @@ class SpfSweep {
     d["hop_split"] = i.hop_split;
     d["ms_threads"] = i.ms_threads;
     d["ms_skip"] = i.ms_skip;
+    d["ms_direct"] = i.ms_direct;
     return d;
   }
   py::tuple fetch(size_t i) {

@@ -34,6 +34,8 @@ struct SpfArgs {
   uint32_t ms_zero;           // multi-source BFS: index of the always-zero entry
   uint32_t ms_bw;             // multi-source BFS: layout bandwidth for the interval skip (0: no skip)
   uint32_t ms_width;          // multi-source BFS: sources per batch (<= mask bits)
+  uint32_t ms_direct;         // multi-source BFS (u16 / u32 masks, host-order layout): the
+                              // level assembly writes the rows itself (no ms_lvl, no finalize)
   const uint2* recs;       // ELL slots [N * K] then overflow records
   const uint32_t* link;    // per record: link id (ignore sets)
   const uint32_t* srcs;    // [n_rows]

@@ -408,7 +408,7 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
   constexpr uint32_t kC = kE <= 4 ? kE : 4;  // bytes per stored column unit
   const char* const lbase = reinterpret_cast<const char*>(lds);
   uint32_t cur_off = 0u, nxt_off = a.ms_pitch * kE;  // f_cur / f_nxt in bytes
-  uint8_t* lvl = a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
+  uint8_t* lvl = a.ms_direct ? nullptr : a.ms_lvl + static_cast<size_t>(blockIdx.x) * N * kS;  // [N][kS]
   // arrival log (u16 / u32 masks, kLog): each wave appends its nodes' level
   // events {new bits (hi), slice j << 14 | lane << 8 | level (lo)} to a log
   // of its own - one scalar count, one coalesced store per (j, level) with
@@ -687,6 +687,8 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
     // events into them (loads in flight eight at a time) and writes the
     // blocks out whole, 16 bytes a thread
     if (lane == 0) s_wcnt[wave] = wcnt;
+    __shared__ uint32_t s_row[kS];
+    if (tid < S) s_row[tid] = a.order[b0 + tid];
     __syncthreads();
     // node blocks padded to kS + 4 bytes: consecutive blocks start 9 (kS =
     // 32) or 5 (kS = 16) banks apart, so the scattered byte writes of a wave
@@ -711,12 +713,51 @@ __global__ __launch_bounds__(1024) void spf_msbfs_kernel(SpfArgs a) {
         }
       }
       __syncthreads();
-      for (uint32_t i = tid; i < J * 64u * kQ; i += B) {
-        const uint32_t node = i / kQ, q = i % kQ;  // node = j * 64 + lane
-        const uint32_t v = (node >> 6) * B + w * 64u + (node & 63u);
-        const uint32_t* src = lds + node * (kP / 4u) + q * 4u;
-        if (v < N)
-          reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS)[q] = make_uint4(src[0], src[1], src[2], src[3]);
+      if (a.ms_direct) {
+        // host-order layout: the wave's slice j is the host ids j * B + w * 64
+        // + [0, 64), so each source's row gets 64 consecutive levels - the
+        // u8 level row and the u32 distance row written here, coalesced (a
+        // thread: 4 nodes of one source; 16 threads: one 64-node run). The
+        // padding [N, lvl_pitch) of the level rows is "unreached" (no event
+        // lands there). Deep levels (marker 254) were written during the search
+        const uint32_t P = a.lvl_pitch, w0 = a.w0, nq = J * 16u;
+        for (uint32_t i = tid; i < S * nq; i += B) {
+          const uint32_t b = i / nq, jq = i % nq;
+          const uint32_t j = jq >> 4, n0 = j * 64u + (jq & 15u) * 4u;
+          const uint32_t v0 = j * B + w * 64u + (jq & 15u) * 4u;
+          if (v0 >= P) continue;
+          const uint8_t* nb = blk + n0 * kP + b;
+          const uint32_t l[4] = {nb[0], nb[kP], nb[2 * kP], nb[3 * kP]};
+          const uint32_t r = s_row[b];
+          *reinterpret_cast<uint32_t*>(a.lvl_rows + static_cast<size_t>(r) * P + v0) =
+              l[0] | (l[1] << 8) | (l[2] << 16) | (l[3] << 24);
+          if (r >= a.n_out || v0 >= N) continue;  // a neighbour row is read through its level row
+          uint32_t d[4];
+          bool deep = false;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            d[k] = l[k] == kLvlNone ? kInf : l[k] * w0;
+            deep |= l[k] == kLvlDirect;
+          }
+          uint32_t* od = a.out_dist + static_cast<size_t>(r) * N + v0;
+          if (!deep && v0 + 4u <= N && (reinterpret_cast<uintptr_t>(od) & 15u) == 0u) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 q = {d[0], d[1], d[2], d[3]};
+            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(od));
+          } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+              if (v0 + k < N && l[k] != kLvlDirect) __builtin_nontemporal_store(d[k], od + k);
+          }
+        }
+      } else {
+        for (uint32_t i = tid; i < J * 64u * kQ; i += B) {
+          const uint32_t node = i / kQ, q = i % kQ;  // node = j * 64 + lane
+          const uint32_t v = (node >> 6) * B + w * 64u + (node & 63u);
+          const uint32_t* src = lds + node * (kP / 4u) + q * 4u;
+          if (v < N)
+            reinterpret_cast<uint4*>(lvl + static_cast<size_t>(v) * kS)[q] = make_uint4(src[0], src[1], src[2], src[3]);
+        }
       }
       __syncthreads();
     }
@@ -2087,6 +2128,13 @@ __global__ __launch_bounds__(1024) void spf_lds_nh_kernel(SpfArgs a) {
 // 16 bits: such a batch lists its rows in a.ovf_rows and the caller redoes
 // them (spf_lds_nh_kernel, u64 labels, fused first hops - phase 2 then
 // recomputes the same first hops).
+template <int J, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < J) {
+    f(std::integral_constant<int, I>{});
+    static_for<J, I + 1>(f);
+  }
+}
 constexpr uint32_t kWmsOvl = 0x80000000u;  // slot flag: u is overloaded
 
 // packed u16 pairs: saturating add (v_pk_add_u16 clamp: 0xFFFF stays
@@ -2170,7 +2218,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   // a node whose in-neighbours all kept their labels since it was last
   // recomputed cannot change. (A change later in the same round is seen in
   // the next one.) Three rotating bitmaps: one read, one written, one cleared.
-  // ORH_WMS_NO_SKIP (A/B builds): every slice every round
+  // a.ms_bw = 0: every slice every round (ORH_WMS_SKIP, orh_spf_run)
   const uint32_t nchunk = (N + 63) / 64, cw = (nchunk + 31) / 32;
   uint32_t* chg = reinterpret_cast<uint32_t*>(D + N + 1);  // [3][cw]
   for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
@@ -2182,12 +2230,11 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
     const uint32_t* prev = chg + ((round + 2u) % 3u) * cw;
     uint32_t* cur = chg + (round % 3u) * cw;
     if (tid < cw) chg[((round + 1u) % 3u) * cw + tid] = 0u;  // read in round - 1, written in round + 1
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
+    auto relax = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
       const uint32_t v = j * B + tid;
       const uint32_t c = __builtin_amdgcn_readfirstlane(j * (B >> 6) + wave);  // this slice's chunk
-#ifndef ORH_WMS_NO_SKIP
-      if (round > 1) {
+      if (round > 1 && bw) {
         const uint32_t lo = c * 64u > bw ? (c * 64u - bw) >> 6 : 0u;
         const uint32_t hi = min(nchunk - 1u, (c * 64u + 63u + bw) >> 6);
         bool act = false;
@@ -2197,10 +2244,9 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
           if (w == (hi >> 5) && (hi & 31u) != 31u) m &= (2u << (hi & 31u)) - 1u;
           act = m != 0u;
         }
-        if (!act) continue;
+        if (!act) return;
       }
-#endif
-      if (v >= N) continue;
+      if (v >= N) return;
       // opaque per round: the addresses and replicated weights are derived
       // again each time instead of held in J * K more registers
 #pragma unroll
@@ -2223,7 +2269,10 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
         prog = 1;
       }
       if (__builtin_amdgcn_ballot_w64(changed) && (tid & 63u) == 0u) atomicOr(&cur[c >> 5], 1u << (c & 31u));
-    }
+    };
+    // (walking the slices backwards in odd rounds, for paths against the
+    // slice order, measured no faster: profiles/r06/h_c2w_variants.txt)
+    static_for<J>(relax);
     if (prog) s_prog[round % 3u] = 1u;
     lds_barrier();
     if (!s_prog[round % 3u]) break;

@@ -115,6 +115,7 @@ struct orh_graph {
   // compact region and a wave's 64 nodes progress together). Rebuilt lazily
   // after attribute patches. Rows in HBM are always indexed by host id.
   std::vector<uint32_t> ms_dev_of, ms_host_of;  // host -> CM id, CM id -> host
+  bool ms_identity = false;  // the layout kept the host order (order_nodes)
   bool ms_dirty = true;
   uint32_t ms_bw = 0;  // CM bandwidth over live records when the interval skip is on, else 0
   uint32_t ms_bw_layout = 1;  // the same bandwidth whatever the opt-in (latency-plan skip)
@@ -256,6 +257,28 @@ void order_nodes(orh_graph* g) {
       }
     }
   }
+  // The host order itself when its bandwidth is within 5/4 of the
+  // Cuthill-McKee order's (a grid numbered row by row: bandwidth n either
+  // way). Its slices are runs of host ids, so the multi-source BFS writes the
+  // u32 distance rows straight from its level assembly (no ms_finalize pass)
+  // and a wave's gathers read neighbours at the same offsets (v +- 1, v +- n)
+  // instead of across anti-diagonal boundaries. ORH_MS_ORDER=cm / host forces
+  // one order (A/B)
+  auto bandwidth = [&](const uint32_t* id) {
+    uint32_t bw = 0;
+    for (uint32_t v = 0; v < N; ++v)
+      for (uint32_t k = g->dn_ptr[v]; k < g->dn_ptr[v + 1]; ++k) {
+        const uint32_t a = id ? id[v] : v, b = id ? id[g->dn[k]] : g->dn[k];
+        bw = std::max(bw, a > b ? a - b : b - a);
+      }
+    return bw;
+  };
+  const char* fe = getenv("ORH_MS_ORDER");  // read per layout (tests set it per graph)
+  const int force = !fe ? 0 : strcmp(fe, "cm") == 0 ? 1 : strcmp(fe, "host") == 0 ? 2 : 0;
+  g->ms_identity = force == 2 || (force == 0 && static_cast<uint64_t>(bandwidth(nullptr)) * 4 <=
+                                                    static_cast<uint64_t>(bandwidth(dev_of.data())) * 5);
+  if (g->ms_identity)
+    for (uint32_t v = 0; v < N; ++v) dev_of[v] = host_of[v] = v;
 }
 
 uint2 device_record(const orh_graph* g, uint32_t v, uint32_t e, const uint32_t* dev_of = nullptr) {
@@ -2119,7 +2142,13 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     // latency plan alone (ORH_MS_LATENCY=2)
     a.ms_bw = g->ms_bw ? g->ms_bw : run_plan.ms_skip ? g->ms_bw_layout : 0u;
     a.ms_width = run_plan.ms_width;
-    const size_t scratch = (orh::ms_scratch_bytes(run_plan, N, n_rows) + 255) & ~size_t{255};
+    // host-order layout, u16 / u32 masks: the rows come out of the search
+    // kernel itself (ORH_MS_DIRECT=0: through ms_lvl and ms_finalize, A/B)
+    const char* de = getenv("ORH_MS_DIRECT");  // read per run (tests flip it)
+    const bool direct_on = !(de && de[0] == '0');
+    a.ms_direct = direct_on && g->ms_identity && run_plan.mask_bytes <= 4 ? 1u : 0u;
+    const size_t scratch =
+        a.ms_direct ? 0 : (orh::ms_scratch_bytes(run_plan, N, n_rows) + 255) & ~size_t{255};
     const size_t log_bytes = orh::ms_log_bytes(run_plan, n_rows);
     rc = ensure_ms_lvl(ctx, scratch + log_bytes);
     if (rc) return rc;
@@ -2204,7 +2233,13 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     a.dev_of = g->d_ms_dev_of;
     a.wms_slots = g->d_wms;
     a.wms_limit = 0xFFFEu - g->wms_maxw;
-    a.ms_bw = g->ms_bw_layout;  // the in-links' reach in Cuthill-McKee ids (activity skip)
+    // the in-links' reach in layout ids: the activity skip (ORH_WMS_SKIP=0:
+    // every slice every round)
+    static const bool skip = [] {
+      const char* e = getenv("ORH_WMS_SKIP");
+      return !(e && e[0] == '0');
+    }();
+    a.ms_bw = skip ? g->ms_bw_layout : 0u;
     a.recs_k = g->ell_k;
   }
   hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
@@ -2262,14 +2297,18 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   info.batch_sources = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.ms_width : 0;
   info.ms_threads = run_plan.variant == orh::SpfVariant::kMsBfs ? run_plan.block : 0;
   info.ms_skip = run_plan.variant == orh::SpfVariant::kMsBfs && a.ms_bw ? 1u : 0u;
+  info.ms_direct = run_plan.variant == orh::SpfVariant::kMsBfs ? a.ms_direct
+                 : run_plan.variant == orh::SpfVariant::kWms && g->ms_identity ? 1u : 0u;
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
 #ifdef ORH_EXP_MSBFS_ONLY  // timing experiment only (tools/diag_build.sh): no phase 2
     ctx->last_info = info;
     ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     return ORH_OK;
 #endif
-    e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
+    if (!a.ms_direct) {
+      e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
+      if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
+    }
     e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
   } else if (!fused) {

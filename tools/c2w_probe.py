@@ -43,12 +43,14 @@ def main():
         sw.sync()
     wall = (time.perf_counter() - t0) / (args.reps * len(sweeps))
     sw = sweeps[0][1]
-    dev = []
+    dev, ph = [], []
     for _ in range(5):
         sw.run()
         dev.append(sw.last_ms())
+        ph.append(sw.phase_ms())
     out = {"nodes": sw.nodes, "edges": sw.edges, "sources": len(names), "lanes": args.lanes,
            "wall_ms_per_sweep": round(wall * 1e3, 4), "device_ms": round(statistics.median(dev), 4),
+           "phase_ms": [round(statistics.median(p[i] for p in ph), 4) for i in (0, 1)],
            "spf_sources_per_s": round(len(names) / wall, 1), "info": sw.info(),
            "env": {k: v for k, v in os.environ.items() if k.startswith("ORH_")}}
     print(json.dumps(out), flush=True)
