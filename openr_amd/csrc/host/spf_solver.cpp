@@ -1365,18 +1365,41 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     auto pid = ps.pidOf(prefix);
     return pid ? ownsPid(*pid, ps.numPrefixIds()) : shardRank_ == 0;
   };
+  uint64_t devPolOnDevice = 0, devPolUpdated = 0;
   if (dev) {
     const uint32_t n = ps.numPrefixIds();
     // a prefix shard materialises its own block of prefix ids [pidLo, pidHi)
     const auto [pidLo, pidHi] = shardRange(n);
     const uint32_t nOwn = pidHi - pidLo;
-    uint64_t nHost = 0, nDev = 0;
-    for (uint32_t pid = pidLo; pid < pidHi; ++pid) {
-      if (!ps.prefixLive(pid)) continue;
-      if (selStatus_[pid] == ORH_SEL_HOST) ++nHost; else ++nDev;
+    // the selection counts (and the device policy's, read after the build)
+    // in one pass over the pool: C5's 1M ids were two sequential passes
+    {
+      const size_t W = pool.size();
+      std::vector<std::array<uint64_t, 4>> cnt(W, std::array<uint64_t, 4>{});
+      auto countRange = [&](size_t w, size_t b, size_t e) {
+        uint64_t h = 0, d = 0, od = 0, up = 0;
+        for (size_t i = b; i < e; ++i) {
+          const uint32_t pid = pidLo + static_cast<uint32_t>(i);
+          if (!ps.prefixLive(pid)) continue;
+          const uint8_t st = selStatus_[pid];
+          if (st == ORH_SEL_HOST) ++h; else ++d;
+          if (devPolicy && st == ORH_SEL_ROUTE && devPol_.stmt[pid] != ORH_POL_HOST) {
+            ++od;
+            up += devPol_.stmt[pid] < ORH_POL_MAX_STMTS;
+          }
+        }
+        cnt[w] = {h, d, od, up};
+      };
+      if (nOwn >= kParallelMin && W > 1) pool.parallelFor(nOwn, countRange);
+      else countRange(0, 0, nOwn);
+      uint64_t s[4] = {0, 0, 0, 0};
+      for (const auto& c : cnt)
+        for (int k = 0; k < 4; ++k) s[k] += c[k];
+      hostSelected_ = s[0];
+      deviceSelected_ = s[1];
+      devPolOnDevice = s[2];
+      devPolUpdated = s[3];
     }
-    deviceSelected_ = nDev;
-    hostSelected_ = nHost;
     using RouteMap = decltype(db.unicastRoutes);
     // the unicast routes of [pidLo, pidHi) into db, and `extra(k)` for k in
     // [0, nExtra) (node-label candidates) in the same pool pass. Two passes
@@ -1663,12 +1686,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
   if (policyActive) {
     uint64_t updated = 0, onDevice = 0;
     if (devPolicy) {
-      const auto [pidLo, pidHi] = shardRange(ps.numPrefixIds());
-      for (uint32_t pid = pidLo; pid < pidHi; ++pid)
-        if (ps.prefixLive(pid) && selStatus_[pid] == ORH_SEL_ROUTE && devPol_.stmt[pid] != ORH_POL_HOST) {
-          ++onDevice;
-          updated += devPol_.stmt[pid] < ORH_POL_MAX_STMTS;
-        }
+      onDevice = devPolOnDevice;  // counted with the selection (devPolicy implies dev)
+      updated = devPolUpdated;
       updated += devPol_.hostUpdated;
       policy->addInvalidated(devPol_.deviceInvalidated + devPol_.hostInvalidated);
     } else {  // RibPolicy::applyPolicy over the whole database on the host

@@ -1607,7 +1607,25 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
 constexpr uint32_t kSpillSlots = 2048, kSpillProbe = 64;
 constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
 
-template <int K>
+// kOwn: a thread that lowers a node below the bucket bound keeps it (up to G
+// per expansion) and expands it itself in its next group instead of
+// publishing its near bit for the word's owner to find: a relaxation chain
+// inside a bucket then advances one group round trip per hop, with no
+// discovery pass in between. A kept node still counts in s_work (counted
+// when kept, uncounted after its expansion) and clears its far bit, so the
+// bucket's termination and the promotion pass see it as if queued; a node
+// kept by one thread and queued or kept by another is expanded twice, which
+// the order-independent fixpoint absorbs. ORH_LDS16_OWN=1 (A/B): measured
+// slower on the C4 batch (k = 1 searches 3.0 -> 3.8 ms, k = 2 4.0 -> 4.8 ms;
+// a longer s_sleep or 512 threads did not help either,
+// profiles/r06/j_ksp2_ab.txt), so the owner-scan form is the default.
+#ifndef ORH_LDS16_SLEEP
+#define ORH_LDS16_SLEEP 1
+#endif
+#ifndef ORH_LDS16_G
+#define ORH_LDS16_G 4
+#endif
+template <int K, bool kOwn>
 __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf, s_inf, s_stop;
@@ -1616,7 +1634,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
   const uint32_t row = blockIdx.x;
   if (a.row_mask && !a.row_mask[row]) return;
-  constexpr int G = K <= 4 ? 4 : 2;
+  constexpr int G = K <= 4 ? ORH_LDS16_G : 2;  // nodes a thread expands together
   const uint32_t DWp = ((N + 1) / 2 + 3) & ~3u;
   uint32_t stop_lo = 0, stop_hi = 0;  // this row's target nodes (early stop)
   if (a.stop_ptr) {
@@ -1692,6 +1710,8 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   uint32_t mpar = 0;
   uint32_t stop_m = 0;  // > 0: stopped with every node at distance <= stop_m final
   bool ovf = false;
+  uint32_t keep[G];  // kOwn: nodes this thread lowered below T, expanded next
+  int nkeep = 0;
   for (;;) {
     uint32_t far_min = kInf;
     // lower u to nd, starting from the word w as read; queue it if lowered
@@ -1727,6 +1747,16 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
       const uint32_t bit = 1u << (u & 31u);
       if (nd < T) {
         atomicAdd(&s_work, 1u);  // counted before the bit is visible
+        if constexpr (kOwn) {
+          if (nkeep < G) {  // static slots (no dynamic register indexing)
+#pragma unroll
+            for (int q = 0; q < G; ++q)
+              if (q == nkeep) keep[q] = u;
+            ++nkeep;
+            atomicAnd(&far[u >> 5], ~bit);
+            return;
+          }
+        }
         const uint32_t old = atomicOr(&near[u >> 5], bit);
         atomicAnd(&far[u >> 5], ~bit);
         if (old & bit) atomicSub(&s_work, 1u);  // already queued
@@ -1739,6 +1769,12 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     for (;;) {
       uint32_t vs[G];
       int c = 0;
+      if constexpr (kOwn) {  // kept nodes first (merge fills keep[] anew below)
+#pragma unroll
+        for (int q = 0; q < G; ++q) vs[q] = keep[q];
+        c = nkeep;
+        nkeep = 0;
+      }
       while (c < G) {
         while (!bits && wi < NB) {
           bits = __hip_atomic_load(&near[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1755,7 +1791,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
         const uint32_t pending = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&s_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (pending == 0u) break;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(ORH_LDS16_SLEEP);
         continue;
       }
       if (c > 0) {
@@ -3242,8 +3278,18 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
     const int b = v ? atoi(v) : 1024;
     return (b >= 64 && b <= 1024 && b % 64 == 0) ? static_cast<uint32_t>(b) : 1024u;
   }();
-  e = ell_k == 8 ? launch(spf_lds16_kernel<8>, a, n_rows, block, lds, s)
-                 : launch(spf_lds16_kernel<4>, a, n_rows, block, lds, s);
+  // ORH_LDS16_OWN: a thread expands the nodes it lowered below the bucket
+  // bound itself (kOwn) instead of publishing them for the word's owner
+  static const bool own = [] {
+    const char* v = getenv("ORH_LDS16_OWN");
+    return v && atoi(v) != 0;
+  }();
+  if (own)
+    e = ell_k == 8 ? launch(spf_lds16_kernel<8, true>, a, n_rows, block, lds, s)
+                   : launch(spf_lds16_kernel<4, true>, a, n_rows, block, lds, s);
+  else
+    e = ell_k == 8 ? launch(spf_lds16_kernel<8, false>, a, n_rows, block, lds, s)
+                   : launch(spf_lds16_kernel<4, false>, a, n_rows, block, lds, s);
   if (e != hipSuccess) return e;
   // rows the u16 search could not finish: the HBM kernel over that list
   // (workgroups past the list's length exit at once)

@@ -257,26 +257,17 @@ void order_nodes(orh_graph* g) {
       }
     }
   }
-  // The host order itself when its bandwidth is within 5/4 of the
-  // Cuthill-McKee order's (a grid numbered row by row: bandwidth n either
-  // way). Its slices are runs of host ids, so the multi-source BFS writes the
-  // u32 distance rows straight from its level assembly (no ms_finalize pass)
-  // and a wave's gathers read neighbours at the same offsets (v +- 1, v +- n)
-  // instead of across anti-diagonal boundaries. ORH_MS_ORDER=cm / host forces
-  // one order (A/B)
-  auto bandwidth = [&](const uint32_t* id) {
-    uint32_t bw = 0;
-    for (uint32_t v = 0; v < N; ++v)
-      for (uint32_t k = g->dn_ptr[v]; k < g->dn_ptr[v + 1]; ++k) {
-        const uint32_t a = id ? id[v] : v, b = id ? id[g->dn[k]] : g->dn[k];
-        bw = std::max(bw, a > b ? a - b : b - a);
-      }
-    return bw;
-  };
+  // ORH_MS_ORDER=host (A/B): the host order itself. Its slices are runs of
+  // host ids, so the multi-source BFS writes the u32 distance rows straight
+  // from its level assembly (no ms_finalize pass) and a wave's gathers read
+  // neighbours at the same offsets (v +- 1, v +- n on a grid numbered row by
+  // row) instead of across anti-diagonal boundaries. Measured slower on the
+  // C2 grid, so Cuthill-McKee stays the default: the 32-sweep step 24.2-24.6
+  // ms against 22.9, one sweep 1.10 against 0.93 ms (the host-order BFS 0.75
+  // against 0.64 ms, the direct rows another 0.13 ms in it for 0.06 ms of
+  // phase 2; profiles/r06/j_ms_ab.txt). ORH_MS_ORDER=cm forces the default
   const char* fe = getenv("ORH_MS_ORDER");  // read per layout (tests set it per graph)
-  const int force = !fe ? 0 : strcmp(fe, "cm") == 0 ? 1 : strcmp(fe, "host") == 0 ? 2 : 0;
-  g->ms_identity = force == 2 || (force == 0 && static_cast<uint64_t>(bandwidth(nullptr)) * 4 <=
-                                                    static_cast<uint64_t>(bandwidth(dev_of.data())) * 5);
+  g->ms_identity = fe && strcmp(fe, "host") == 0;
   if (g->ms_identity)
     for (uint32_t v = 0; v < N; ++v) dev_of[v] = host_of[v] = v;
 }

@@ -113,7 +113,7 @@ def test_c2_sweep_all_sources_exact(hip, oracle, variant):
     sweep.sync()
     info = sweep.info()
     assert info["variant"] == MSBFS and info["hop_nodes"] == 8, info
-    assert info["ms_direct"] == 1, info  # host-order layout: rows written by the search kernel
+    assert info["ms_direct"] == 0, info  # Cuthill-McKee layout: rows through ms_finalize_kernel, as benched
     order = ls_h._impl.node_names()
     W = sweep.words
     for lo in range(0, n * n, 1000):
@@ -128,13 +128,15 @@ def test_c2_sweep_all_sources_exact(hip, oracle, variant):
         gc.collect()
 
 
-@pytest.mark.parametrize("env", [{"ORH_MS_WIDE": "1"}, {"ORH_MS_SKIP": "1"}, {"ORH_MS_ORDER": "cm"},
-                                 {"ORH_MS_DIRECT": "0"}, {"ORH_MS_SKIP": "1", "ORH_MS_ORDER": "cm"}])
+@pytest.mark.parametrize("env", [{"ORH_MS_WIDE": "1"}, {"ORH_MS_SKIP": "1"}, {"ORH_MS_ORDER": "host"},
+                                 {"ORH_MS_ORDER": "host", "ORH_MS_DIRECT": "0"},
+                                 {"ORH_MS_SKIP": "1", "ORH_MS_ORDER": "host"}])
 def test_c2_sweep_opt_in_variants(hip, oracle, monkeypatch, env):
     """The opt-in MS-BFS variants on the same sweep, 64 sources compared in
-    full: u64 masks (250 batches of 40 sources), the interval skip, the
-    Cuthill-McKee layout (ms_lvl scratch + ms_finalize_kernel) and the host
-    layout through ms_finalize_kernel."""
+    full: u64 masks (250 batches of 40 sources), the interval skip, the host
+    layout with its rows written by the search kernel and through
+    ms_finalize_kernel (the default is the Cuthill-McKee layout: ms_lvl scratch
+    + ms_finalize_kernel)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 100
@@ -148,19 +150,18 @@ def test_c2_sweep_opt_in_variants(hip, oracle, monkeypatch, env):
     wide = "ORH_MS_WIDE" in env
     assert info["variant"] == MSBFS and info["mask_bits"] == (64 if wide else 32), info
     assert info["batch_sources"] == (40 if wide else 32), info
-    direct = not wide and "ORH_MS_ORDER" not in env and "ORH_MS_DIRECT" not in env
+    direct = not wide and env.get("ORH_MS_ORDER") == "host" and "ORH_MS_DIRECT" not in env
     assert info["ms_direct"] == (1 if direct else 0), info
 
 
-@pytest.mark.parametrize("order", ["auto", "cm"])
+@pytest.mark.parametrize("order", ["host", "cm"])
 @pytest.mark.parametrize("length,metric,hop_nodes", [(4100, 3, 8), (300, 1, 4)])
 def test_ladder_deep_levels(hip, oracle, monkeypatch, length, metric, hop_nodes, order):
     """BFS depth beyond the u8 level encoding (levels >= 254 are written to
     the distance rows directly and read back through them), with the rows
-    written by the search kernel (the ladder's host order) and through
-    ms_finalize_kernel (Cuthill-McKee layout)."""
-    if order != "auto":
-        monkeypatch.setenv("ORH_MS_ORDER", order)
+    written by the search kernel (ORH_MS_ORDER=host) and through
+    ms_finalize_kernel (Cuthill-McKee layout, the default)."""
+    monkeypatch.setenv("ORH_MS_ORDER", order)
     adj_dbs, _ = ladder(length, metric)
     als_h, _ = load_topology(hip, adj_dbs, [])
     als_o, _ = load_topology(oracle, adj_dbs, [])
@@ -171,7 +172,7 @@ def test_ladder_deep_levels(hip, oracle, monkeypatch, length, metric, hop_nodes,
     info = _sweep_tables(als_h[A], als_o[A], names, check)
     assert info["variant"] == MSBFS, info
     assert info["hop_nodes"] == hop_nodes, info
-    assert info["ms_direct"] == (1 if order == "auto" else 0), info  # rungs in host order: bandwidth 2
+    assert info["ms_direct"] == (1 if order == "host" else 0), info
 
 
 def test_u16_mask_msbfs_150x150(hip, oracle):
