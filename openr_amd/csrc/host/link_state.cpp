@@ -798,6 +798,28 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
       // spf_runs the reference's way: one per source not yet memoized
       // (getSpfResult), one per pair with k = 1 paths (runSpf ignoring them)
       std::unordered_set<std::string> srcCounted;
+      // the pairs' path blocks -> vectors on the pool; the memo inserts below
+      // stay on this thread
+      std::vector<std::pair<std::vector<Path>, std::vector<Path>>> parsed(dev.size());
+      auto parseRange = [&](size_t, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+          const uint32_t* b = blocks + i * static_cast<size_t>(bw);
+          if (b[0] != 0) continue;
+          auto parse = [&](size_t w, std::vector<Path>& out) {
+            const uint32_t n = b[w++];
+            out.reserve(n);
+            for (uint32_t k = 0; k < n; ++k) {
+              const uint32_t len = b[w++];
+              out.emplace_back(b + w, b + w + len);
+              w += len;
+            }
+          };
+          parse(2, parsed[i].first);
+          parse(b[1], parsed[i].second);
+        }
+      };
+      if (dev.size() >= 64) WorkerPool::instance().parallelFor(dev.size(), parseRange);
+      else parseRange(0, 0, dev.size());
       for (size_t i = 0; i < dev.size(); ++i) {
         const uint32_t* b = blocks + i * static_cast<size_t>(bw);
         if (b[0] != 0) {
@@ -805,17 +827,8 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
           continue;
         }
         ++kspDevicePairs_;
-        auto parse = [&](size_t w, std::vector<Path>& out) {
-          const uint32_t n = b[w++];
-          for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t len = b[w++];
-            out.emplace_back(b + w, b + w + len);
-            w += len;
-          }
-        };
-        std::vector<Path> k1, k2;
-        parse(2, k1);
-        parse(b[1], k2);
+        std::vector<Path>& k1 = parsed[i].first;
+        std::vector<Path>& k2 = parsed[i].second;
         const std::string& src = dev[i]->first;
         if (!spfResults_.count({src, true}) && !countedOnDevice_.count(src) && srcCounted.insert(src).second) {
           ++spfRuns_;

@@ -1607,25 +1607,41 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
 constexpr uint32_t kSpillSlots = 2048, kSpillProbe = 64;
 constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
 
-// kOwn: a thread that lowers a node below the bucket bound keeps it (up to G
-// per expansion) and expands it itself in its next group instead of
-// publishing its near bit for the word's owner to find: a relaxation chain
-// inside a bucket then advances one group round trip per hop, with no
-// discovery pass in between. A kept node still counts in s_work (counted
-// when kept, uncounted after its expansion) and clears its far bit, so the
-// bucket's termination and the promotion pass see it as if queued; a node
-// kept by one thread and queued or kept by another is expanded twice, which
-// the order-independent fixpoint absorbs. ORH_LDS16_OWN=1 (A/B): measured
-// slower on the C4 batch (k = 1 searches 3.0 -> 3.8 ms, k = 2 4.0 -> 4.8 ms;
-// a longer s_sleep or 512 threads did not help either,
-// profiles/r06/j_ksp2_ab.txt), so the owner-scan form is the default.
+// The bucket's work count s_work is one LDS word every thread updates: per
+// lane, an add per push and a subtract per duplicate and per expanded group
+// serialise on that one address. Here a wave reserves, before its group's
+// merges, every push the group could make (its nodes' records) with one
+// atomic, counts locally the pushes that queued a new node, and returns the
+// rest together with its expanded nodes with one more (wave sums over DPP).
+// The count still never undercounts: the reservation precedes the wave's
+// near-bit updates in its LDS order, and the release follows them.
+// A/B of the round-6 search knobs on the C4 batch (profiles/r06/j_ksp2_ab.txt,
+// k_ksp2_ab.txt): a thread expanding the nodes it lowered itself instead of
+// publishing them (3.0 -> 3.8 ms), a longer s_sleep (no change), 512 threads
+// (3.0 -> 4.2 ms), 2 or 8 nodes per group instead of 4 (no change).
 #ifndef ORH_LDS16_SLEEP
 #define ORH_LDS16_SLEEP 1
 #endif
 #ifndef ORH_LDS16_G
 #define ORH_LDS16_G 4
 #endif
-template <int K, bool kOwn>
+// wave-wide sum (every lane active), the DPP pattern of wave_min
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#define ORH_DPP_ADD(ctrl, rmask) \
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, rmask, 0xF, false))
+  ORH_DPP_ADD(0x111, 0xF);  // row_shr:1
+  ORH_DPP_ADD(0x112, 0xF);  // row_shr:2
+  ORH_DPP_ADD(0x114, 0xF);  // row_shr:4
+  ORH_DPP_ADD(0x118, 0xF);  // row_shr:8  -> lane 15 of each row holds the row sum
+  ORH_DPP_ADD(0x142, 0xA);  // row_bcast:15 into rows 1, 3
+  ORH_DPP_ADD(0x143, 0xC);  // row_bcast:31 into rows 2, 3 -> lane 63 holds the sum
+#undef ORH_DPP_ADD
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+#ifndef ORH_LDS16_WAVE_COUNT
+#define ORH_LDS16_WAVE_COUNT 1
+#endif
+template <int K>
 __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_work, s_min[2], s_nign, s_ovf, s_inf, s_stop;
@@ -1710,10 +1726,10 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   uint32_t mpar = 0;
   uint32_t stop_m = 0;  // > 0: stopped with every node at distance <= stop_m final
   bool ovf = false;
-  uint32_t keep[G];  // kOwn: nodes this thread lowered below T, expanded next
-  int nkeep = 0;
+  const bool lane0 = (tid & 63u) == 0u;
   for (;;) {
     uint32_t far_min = kInf;
+    uint32_t newq = 0;  // pushes of the current group that queued a node
     // lower u to nd, starting from the word w as read; queue it if lowered
     auto merge = [&](uint32_t u, uint32_t nd, uint32_t w) {
       const uint32_t sh = (u & 1u) * 16u;
@@ -1746,20 +1762,11 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
       }
       const uint32_t bit = 1u << (u & 31u);
       if (nd < T) {
-        atomicAdd(&s_work, 1u);  // counted before the bit is visible
-        if constexpr (kOwn) {
-          if (nkeep < G) {  // static slots (no dynamic register indexing)
-#pragma unroll
-            for (int q = 0; q < G; ++q)
-              if (q == nkeep) keep[q] = u;
-            ++nkeep;
-            atomicAnd(&far[u >> 5], ~bit);
-            return;
-          }
-        }
+        if (!ORH_LDS16_WAVE_COUNT) atomicAdd(&s_work, 1u);  // counted before the bit is visible
         const uint32_t old = atomicOr(&near[u >> 5], bit);
         atomicAnd(&far[u >> 5], ~bit);
-        if (old & bit) atomicSub(&s_work, 1u);  // already queued
+        if (ORH_LDS16_WAVE_COUNT) newq += (old & bit) ? 0u : 1u;  // reserved by the wave
+        else if (old & bit) atomicSub(&s_work, 1u);  // already queued
       } else {
         atomicOr(&far[u >> 5], bit);
         far_min = min(far_min, nd);
@@ -1769,12 +1776,6 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     for (;;) {
       uint32_t vs[G];
       int c = 0;
-      if constexpr (kOwn) {  // kept nodes first (merge fills keep[] anew below)
-#pragma unroll
-        for (int q = 0; q < G; ++q) vs[q] = keep[q];
-        c = nkeep;
-        nkeep = 0;
-      }
       while (c < G) {
         while (!bits && wi < NB) {
           bits = __hip_atomic_load(&near[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1794,16 +1795,27 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
         __builtin_amdgcn_s_sleep(ORH_LDS16_SLEEP);
         continue;
       }
+      // the group's records in flight together, then the neighbours' words
+      uint2 rec[G][K];
+      uint32_t lk[G][K];  // link ids (ignore sets), loaded with the records
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (g < c) load_recs<K>(a, vs[g], rec[g]);
+#pragma unroll
+        for (int j = 0; j < K; ++j) lk[g][j] = (g < c && s.n_ign) ? a.link[vs[g] * K + j] : 0u;
+      }
+      // every push the group can make (its records, continuation lists
+      // included), reserved in s_work by the wave before any of its merges
+      uint32_t bound = 0;
+      if (ORH_LDS16_WAVE_COUNT) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (g < c) bound += K + ((rec[g][K - 1].x & ORH_REC_CONT) ? rec[g][K - 1].y : 0u);
+        const uint32_t r = wave_sum(bound);
+        if (lane0 && r) atomicAdd(&s_work, r);
+      }
+      newq = 0;
       if (c > 0) {
-        // the group's records in flight together, then the neighbours' words
-        uint2 rec[G][K];
-        uint32_t lk[G][K];  // link ids (ignore sets), loaded with the records
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          if (g < c) load_recs<K>(a, vs[g], rec[g]);
-#pragma unroll
-          for (int j = 0; j < K; ++j) lk[g][j] = (g < c && s.n_ign) ? a.link[vs[g] * K + j] : 0u;
-        }
         uint32_t dv[G], nw[G][K];
         bool ok[G][K];
 #pragma unroll
@@ -1835,7 +1847,12 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
             }
           }
         }
-        atomicSub(&s_work, static_cast<uint32_t>(c));
+        if (!ORH_LDS16_WAVE_COUNT) atomicSub(&s_work, static_cast<uint32_t>(c));
+      }
+      if (ORH_LDS16_WAVE_COUNT) {
+        // the unused reservation and the expanded nodes, after the merges
+        const uint32_t back = wave_sum(c > 0 ? bound - newq + static_cast<uint32_t>(c) : 0u);
+        if (lane0 && back) atomicSub(&s_work, back);
       }
     }
     {
@@ -1878,7 +1895,12 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
         promoted += __builtin_popcount(promote);
       }
     }
-    if (promoted) atomicAdd(&s_work, promoted);
+    if (ORH_LDS16_WAVE_COUNT) {
+      const uint32_t pr = wave_sum(promoted);
+      if (lane0 && pr) atomicAdd(&s_work, pr);
+    } else if (promoted) {
+      atomicAdd(&s_work, promoted);
+    }
     const uint32_t wm = wave_min(local_min);
     if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
     mpar = npar;
@@ -3278,18 +3300,8 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
     const int b = v ? atoi(v) : 1024;
     return (b >= 64 && b <= 1024 && b % 64 == 0) ? static_cast<uint32_t>(b) : 1024u;
   }();
-  // ORH_LDS16_OWN: a thread expands the nodes it lowered below the bucket
-  // bound itself (kOwn) instead of publishing them for the word's owner
-  static const bool own = [] {
-    const char* v = getenv("ORH_LDS16_OWN");
-    return v && atoi(v) != 0;
-  }();
-  if (own)
-    e = ell_k == 8 ? launch(spf_lds16_kernel<8, true>, a, n_rows, block, lds, s)
-                   : launch(spf_lds16_kernel<4, true>, a, n_rows, block, lds, s);
-  else
-    e = ell_k == 8 ? launch(spf_lds16_kernel<8, false>, a, n_rows, block, lds, s)
-                   : launch(spf_lds16_kernel<4, false>, a, n_rows, block, lds, s);
+  e = ell_k == 8 ? launch(spf_lds16_kernel<8>, a, n_rows, block, lds, s)
+                 : launch(spf_lds16_kernel<4>, a, n_rows, block, lds, s);
   if (e != hipSuccess) return e;
   // rows the u16 search could not finish: the HBM kernel over that list
   // (workgroups past the list's length exit at once)
