@@ -95,7 +95,17 @@ typedef struct orh_spf_request {
   const uint32_t* h_ignore_ptr;
   const uint32_t* h_ignore_links;
   int32_t use_link_metric; /* 0: hop count (useLinkMetric = false) */
+  /* ORH_SPF_* flags; zero-initialise the request (0 = the default run) */
+  uint32_t flags;
 } orh_spf_request;
+
+/* orh_spf_request.flags: a multi-source sweep's second phase (level rows ->
+ * distance rows, first hops) runs on the context's second stream, so the
+ * context stream takes the next sweep's search at once. The rows are complete
+ * for work issued on the context after the next orh_sync / orh_memcpy_* /
+ * orh_row_digest / SPF, KSP2, what-if or route call (each joins the deferred
+ * work first); other readers wait for orh_sync. */
+#define ORH_SPF_DEFER_HOPS 1u
 
 typedef struct orh_counters {
   uint64_t spf_runs;      /* fb303 decision.spf_runs equivalent */

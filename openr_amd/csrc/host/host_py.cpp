@@ -411,6 +411,10 @@ class SpfSweep {
     req.h_srcs = srcs_.data();
     req.n_src = static_cast<uint32_t>(srcs_.size());
     req.use_link_metric = useLinkMetric_ ? 1 : 0;
+    // a multi-source sweep's second phase on the context's second stream:
+    // the next sweep on this context starts its search at once (sync(),
+    // fetch() and copy_to() join it)
+    req.flags = ORH_SPF_DEFER_HOPS;
     if (!ignPtr_.empty()) {
       req.h_ignore_ptr = ignPtr_.data();
       req.h_ignore_links = ignLinks_.empty() ? ignPtr_.data() : ignLinks_.data();

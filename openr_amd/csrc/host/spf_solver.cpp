@@ -1504,14 +1504,25 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           for (size_t w = 0; w < W; ++w) n += slots.lists[w * kS + sh].size();
           auto& dst = db.unicastRoutes.shard(sh);
           dst.reserve(dst.size() + n);
-          for (size_t w = 0; w < W; ++w)
-            for (uint32_t i : slots.lists[w * kS + sh]) {
+          for (size_t w = 0; w < W; ++w) {
+            const auto& list = slots.lists[w * kS + sh];
+            for (size_t q = 0; q < list.size(); ++q) {
+              // a shard's slots are ~1/64 of the slot array apart: the
+              // slots a few routes ahead are fetched while this one inserts
+              constexpr size_t kAhead = 6;
+              if (q + kAhead < list.size()) {
+                const char* ahead = reinterpret_cast<const char*>(slots.at(list[q + kAhead]));
+                __builtin_prefetch(ahead);
+                __builtin_prefetch(ahead + 64);
+              }
+              const uint32_t i = list[q];
               RibUnicastEntry* r = slots.at(i);
               Cidr k = r->prefix;
               if (!dst.emplace(std::move(k), std::move(*r)).second) dup = true;
               r->~RibUnicastEntry();
               ++done[w * kS + sh];
             }
+          }
         }
       }, mergeChunks);
       } catch (...) {

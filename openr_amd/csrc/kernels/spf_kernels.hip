@@ -91,6 +91,20 @@ __device__ inline uint32_t wave_min(uint32_t v) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
 
+// wave-wide sum (every lane active), the DPP pattern of wave_min
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#define ORH_DPP_ADD(ctrl, rmask) \
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, rmask, 0xF, false))
+  ORH_DPP_ADD(0x111, 0xF);  // row_shr:1
+  ORH_DPP_ADD(0x112, 0xF);  // row_shr:2
+  ORH_DPP_ADD(0x114, 0xF);  // row_shr:4
+  ORH_DPP_ADD(0x118, 0xF);  // row_shr:8  -> lane 15 of each row holds the row sum
+  ORH_DPP_ADD(0x142, 0xA);  // row_bcast:15 into rows 1, 3
+  ORH_DPP_ADD(0x143, 0xC);  // row_bcast:31 into rows 2, 3 -> lane 63 holds the sum
+#undef ORH_DPP_ADD
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
 struct Src {
   uint32_t node;
   const uint32_t* ign;
@@ -1350,9 +1364,17 @@ __device__ inline uint32_t lab_dist(uint32_t l) { return l; }
 __device__ inline uint32_t lab_nh(unsigned long long l) { return static_cast<uint32_t>(l); }
 __device__ inline uint32_t lab_nh(uint32_t) { return 0u; }
 
-template <int K, int G, typename L, typename Merge>
+struct NoPre {
+  __device__ void operator()(uint32_t) const {}
+};
+// pre(bound): called once the group's records are in, before any merge, with
+// the most pushes the group can make (its records, continuation lists
+// included); a caller that passes one calls expand_group from every lane
+// (c = 0 included), so pre runs with the whole wave active
+template <int K, int G, typename L, typename Merge, typename Pre = NoPre>
 __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* lab,
-                                             const uint32_t (&vs)[G], int c, Merge& merge) {
+                                             const uint32_t (&vs)[G], int c, Merge& merge,
+                                             Pre&& pre = Pre{}) {
   constexpr bool kNh = sizeof(L) == 8;
   uint2 rec[G][K];
   L lv[G];
@@ -1364,6 +1386,13 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* 
 #pragma unroll
     for (int j = 0; j < K; ++j) lk[g][j] = s.n_ign ? a.link[vs[g] * K + j] : 0u;
     lv[g] = __hip_atomic_load(&lab[vs[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  {
+    uint32_t bound = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (g < c) bound += K + ((rec[g][K - 1].x & ORH_REC_CONT) ? rec[g][K - 1].y : 0u);
+    pre(bound);
   }
   L cl[G][K];
   bool ok[G][K];
@@ -1419,6 +1448,10 @@ __device__ __forceinline__ void expand_group(const SpfArgs& a, const Src& s, L* 
 // result is the synchronous kernel's bit for bit; what goes away is the
 // per-round barrier that held every wave to the slowest one (the C4 WAN runs
 // about a hundred near rounds per search).
+// ORH_ASYNC_WAVE_COUNT=0 (A/B builds): per-lane updates of the work count
+#ifndef ORH_ASYNC_WAVE_COUNT
+#define ORH_ASYNC_WAVE_COUNT 1
+#endif
 template <int K, bool kNh>
 __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   typedef typename std::conditional<kNh, unsigned long long, uint32_t>::type L;
@@ -1478,6 +1511,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
   uint32_t mpar = 0;
   for (;;) {
     uint32_t far_min = kInf;
+    uint32_t newq = 0;  // pushes of the current group that queued a node
     auto merge = [&](uint32_t u, uint32_t nd, uint32_t cnh, L cl) {
       if constexpr (kNh) {
         for (;;) {
@@ -1498,10 +1532,11 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
       }
       const uint32_t bit = 1u << (u & 31u);
       if (nd < T) {
-        atomicAdd(&s_work, 1u);  // counted before the bit is visible
+        if (!ORH_ASYNC_WAVE_COUNT) atomicAdd(&s_work, 1u);  // counted before the bit is visible
         const uint32_t old = atomicOr(&near[u >> 5], bit);
         atomicAnd(&far[u >> 5], ~bit);
-        if (old & bit) atomicSub(&s_work, 1u);  // already queued
+        if (ORH_ASYNC_WAVE_COUNT) newq += (old & bit) ? 0u : 1u;  // reserved by the wave
+        else if (old & bit) atomicSub(&s_work, 1u);  // already queued
       } else {
         atomicOr(&far[u >> 5], bit);
         far_min = min(far_min, nd);
@@ -1531,7 +1566,20 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
-      if (c > 0) {
+      if (ORH_ASYNC_WAVE_COUNT) {
+        // the work count per wave, as in spf_lds16_kernel: the group's
+        // possible pushes reserved before its merges, the unused ones and
+        // the expanded nodes returned after them
+        uint32_t bound = 0;
+        newq = 0;
+        expand_group<K, G, L>(a, s, lab, vs, c, merge, [&](uint32_t b) {
+          bound = b;
+          const uint32_t r = wave_sum(b);
+          if ((tid & 63u) == 0u && r) atomicAdd(&s_work, r);
+        });
+        const uint32_t back = wave_sum(c > 0 ? bound - newq + static_cast<uint32_t>(c) : 0u);
+        if ((tid & 63u) == 0u && back) atomicSub(&s_work, back);
+      } else if (c > 0) {
         expand_group<K, G, L>(a, s, lab, vs, c, merge);
         atomicSub(&s_work, static_cast<uint32_t>(c));
       }
@@ -1562,7 +1610,12 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
         promoted += __builtin_popcount(promote);
       }
     }
-    if (promoted) atomicAdd(&s_work, promoted);
+    if (ORH_ASYNC_WAVE_COUNT) {
+      const uint32_t pr = wave_sum(promoted);
+      if ((tid & 63u) == 0u && pr) atomicAdd(&s_work, pr);
+    } else if (promoted) {
+      atomicAdd(&s_work, promoted);
+    }
     const uint32_t wm = wave_min(local_min);
     if ((tid & 63u) == 0 && wm != kInf) atomicMin(&s_min[npar], wm);
     mpar = npar;
@@ -1625,19 +1678,6 @@ constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
 #ifndef ORH_LDS16_G
 #define ORH_LDS16_G 4
 #endif
-// wave-wide sum (every lane active), the DPP pattern of wave_min
-__device__ inline uint32_t wave_sum(uint32_t v) {
-#define ORH_DPP_ADD(ctrl, rmask) \
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, rmask, 0xF, false))
-  ORH_DPP_ADD(0x111, 0xF);  // row_shr:1
-  ORH_DPP_ADD(0x112, 0xF);  // row_shr:2
-  ORH_DPP_ADD(0x114, 0xF);  // row_shr:4
-  ORH_DPP_ADD(0x118, 0xF);  // row_shr:8  -> lane 15 of each row holds the row sum
-  ORH_DPP_ADD(0x142, 0xA);  // row_bcast:15 into rows 1, 3
-  ORH_DPP_ADD(0x143, 0xC);  // row_bcast:31 into rows 2, 3 -> lane 63 holds the sum
-#undef ORH_DPP_ADD
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
-}
 #ifndef ORH_LDS16_WAVE_COUNT
 #define ORH_LDS16_WAVE_COUNT 1
 #endif

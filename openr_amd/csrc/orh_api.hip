@@ -52,6 +52,15 @@ struct orh_ctx {
   // multi-source BFS: node-major level bytes
   uint8_t* d_ms_lvl = nullptr;
   size_t d_ms_lvl_cap = 0;
+  // deferred second phase (ORH_SPF_DEFER_HOPS): finalize + first hops of a
+  // sweep on stream2 while the context stream takes the next sweep's search.
+  // The level bytes alternate between two halves of d_ms_lvl; a search into
+  // half b first waits for the phase 2 still reading it (ev_p2[b])
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_ms2 = nullptr;                // end of the search phase 2 follows
+  hipEvent_t ev_p2[2] = {nullptr, nullptr};   // end of the phase 2 reading half b
+  bool p2_pending[2] = {false, false};        // ev_p2[b] not yet joined
+  uint32_t p2_half = 0;                       // half of the next deferred sweep
   // orh_spf_batch's device rows (reused: a hipMalloc/hipFree pair per call
   // costs more than a single-source SPF)
   uint32_t* d_batch = nullptr;
@@ -530,8 +539,26 @@ int ensure_graph_req(orh_graph* g, size_t words) {
   return ORH_OK;
 }
 
+// deferred second phases: the context stream waits for them (device side)
+void join_deferred(orh_ctx* ctx) {
+  for (int b = 0; b < 2; ++b)
+    if (ctx->p2_pending[b]) {
+      hipStreamWaitEvent(ctx->stream, ctx->ev_p2[b], 0);
+      ctx->p2_pending[b] = false;
+    }
+}
+
+// ... or the host waits for them (before a buffer they read is freed or
+// rewritten outside the context stream's order)
+void drain_deferred(orh_ctx* ctx) {
+  if (!ctx->stream2) return;
+  hipStreamSynchronize(ctx->stream2);
+  ctx->p2_pending[0] = ctx->p2_pending[1] = false;
+}
+
 int ensure_lvl_rows(orh_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->d_lvl_rows_cap) return ORH_OK;
+  drain_deferred(ctx);
   hipFree(ctx->d_lvl_rows);
   ctx->d_lvl_rows = nullptr;
   ctx->d_lvl_rows_cap = 0;
@@ -552,6 +579,7 @@ int ensure_labels(orh_ctx* ctx, size_t n) {
 
 int ensure_scratch(orh_ctx* ctx, size_t words) {
   if (words <= ctx->d_scratch_cap) return ORH_OK;
+  drain_deferred(ctx);
   hipFree(ctx->d_scratch);
   ctx->d_scratch = nullptr;
   ctx->d_scratch_cap = 0;
@@ -584,6 +612,7 @@ bool staged_key_matches(const std::vector<uint32_t>& stored, const std::vector<u
 
 int ensure_ms_lvl(orh_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->d_ms_lvl_cap) return ORH_OK;
+  drain_deferred(ctx);
   hipFree(ctx->d_ms_lvl);
   ctx->d_ms_lvl = nullptr;
   ctx->d_ms_lvl_cap = 0;
@@ -676,6 +705,7 @@ int orh_destroy(orh_ctx* ctx) {
     g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), ctx), g_ctxs.end());
   }
   hipSetDevice(ctx->device);
+  drain_deferred(ctx);
   hipStreamSynchronize(ctx->stream);
   hipFree(ctx->d_req);
   hipFree(ctx->d_scratch);
@@ -693,6 +723,12 @@ int orh_destroy(orh_ctx* ctx) {
   hipEventDestroy(ctx->ev0);
   hipEventDestroy(ctx->evm);
   hipEventDestroy(ctx->ev1);
+  if (ctx->stream2) {
+    hipEventDestroy(ctx->ev_ms2);
+    hipEventDestroy(ctx->ev_p2[0]);
+    hipEventDestroy(ctx->ev_p2[1]);
+    hipStreamDestroy(ctx->stream2);
+  }
   hipStreamDestroy(ctx->stream);
   delete ctx;
   return ORH_OK;
@@ -702,6 +738,7 @@ const char* orh_last_error(const orh_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int orh_sync(orh_ctx* ctx) {
   if (!ctx) return ORH_E_INVALID;
+  join_deferred(ctx);
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
 }
@@ -735,6 +772,7 @@ int orh_device_free(orh_ctx* ctx, void* d_ptr) {
 int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes) {
   if (!ctx || (!h_dst && bytes) || (!d_src && bytes)) return ORH_E_INVALID;
   if (!bytes) return ORH_OK;
+  join_deferred(ctx);
   ORH_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
@@ -743,6 +781,7 @@ int orh_memcpy_d2h(orh_ctx* ctx, void* h_dst, const void* d_src, size_t bytes) {
 int orh_memcpy_h2d(orh_ctx* ctx, void* d_dst, const void* h_src, size_t bytes) {
   if (!ctx || (!d_dst && bytes) || (!h_src && bytes)) return ORH_E_INVALID;
   if (!bytes) return ORH_OK;
+  join_deferred(ctx);
   ORH_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
@@ -750,6 +789,7 @@ int orh_memcpy_h2d(orh_ctx* ctx, void* d_dst, const void* h_src, size_t bytes) {
 
 int orh_memcpy_d2d(orh_ctx* ctx, void* d_dst, const void* d_src, size_t bytes) {
   if (!ctx || (!d_dst && bytes) || (!d_src && bytes)) return ORH_E_INVALID;
+  join_deferred(ctx);
   ORH_HIP(ctx, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
   ORH_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return ORH_OK;
@@ -759,6 +799,7 @@ int orh_row_digest(orh_ctx* ctx, const uint32_t* d_dist, const uint32_t* d_nh, u
                    uint32_t n_rows, uint64_t* d_out) {
   if (!ctx || words == 0 || (n_rows && (!d_dist || !d_nh || !d_out))) return ORH_E_INVALID;
   if (n_rows == 0) return ORH_OK;
+  join_deferred(ctx);
   ORH_HIP(ctx, hipSetDevice(ctx->device));
   ORH_HIP(ctx, orh::launch_row_digest(d_dist, d_nh, words, n, n_rows, d_out, ctx->stream));
   return ORH_OK;
@@ -776,6 +817,7 @@ int orh_graph_create(orh_ctx* ctx, orh_graph** out) {
 int orh_graph_destroy(orh_graph* g) {
   if (!g) return ORH_E_INVALID;
   hipSetDevice(g->ctx->device);
+  drain_deferred(g->ctx);
   hipStreamSynchronize(g->ctx->stream);
   free_graph_device(g);
   g->ctx->req_key.clear();  // the staged request may describe this graph
@@ -786,6 +828,7 @@ int orh_graph_destroy(orh_graph* g) {
 int orh_graph_load(orh_graph* g, const orh_csr* c) {
   if (!g || !c) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  drain_deferred(ctx);  // the deferred phase 2 reads the graph
   if (!c->row_ptr || (c->n_edges && (!c->col || !c->w_out || !c->w_in || !c->meta)) ||
       (c->n_nodes && !c->node_overloaded))
     return fail(ctx, ORH_E_INVALID, "orh_graph_load: null array");
@@ -880,6 +923,7 @@ int orh_graph_patch_edges(orh_graph* g, uint32_t n, const uint32_t* idx, const u
                           const uint32_t* w_in, const uint32_t* meta) {
   if (!g || (n && (!idx || !w_out || !w_in || !meta))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  drain_deferred(ctx);  // the deferred phase 2 reads the graph
   if (!g->d_recs && n) return fail(ctx, ORH_E_STATE, "orh_graph_patch_edges: no graph loaded");
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = idx[i];
@@ -912,6 +956,7 @@ int orh_graph_apply_delta(orh_graph* g, uint32_t n_rows, const uint32_t* rows, c
                           const uint32_t* meta, uint32_t n_links) {
   if (!g || (n_rows && (!rows || !ptr))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  drain_deferred(ctx);  // the deferred phase 2 reads the graph
   if (!g->d_recs) return fail(ctx, ORH_E_STATE, "orh_graph_apply_delta: no graph loaded");
   const uint32_t N = g->n_nodes;
   if (n_rows && ptr[0] != 0) return fail(ctx, ORH_E_INVALID, "orh_graph_apply_delta: ptr[0] != 0");
@@ -1003,6 +1048,7 @@ int orh_graph_apply_delta(orh_graph* g, uint32_t n_rows, const uint32_t* rows, c
 int orh_graph_patch_nodes(orh_graph* g, uint32_t n, const uint32_t* idx, const uint8_t* ovl) {
   if (!g || (n && (!idx || !ovl))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  drain_deferred(ctx);  // the deferred phase 2 reads the graph
   if (!g->d_recs && n) return fail(ctx, ORH_E_STATE, "orh_graph_patch_nodes: no graph loaded");
   for (uint32_t i = 0; i < n; ++i)
     if (idx[i] >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_graph_patch_nodes: bad node");
@@ -1746,6 +1792,7 @@ int orh_whatif_create(orh_graph* g, const uint32_t* h_srcs, uint32_t n_srcs, int
   if (!g || !out || (n_srcs && !h_srcs)) return g ? fail(g->ctx, ORH_E_INVALID, "orh_whatif_create: null argument")
                                                   : ORH_E_INVALID;
   *out = nullptr;
+  join_deferred(g->ctx);
   return whatif_create(g, h_srcs, n_srcs, use_link_metric, out);
 }
 
@@ -1753,6 +1800,7 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
                    const uint32_t* h_ignore_links, uint32_t* d_dist, uint32_t* d_nh, uint32_t* d_info) {
   if (!job) return ORH_E_INVALID;
   orh_ctx* ctx = job->g->ctx;
+  join_deferred(ctx);
   if (n_req == 0) return ORH_OK;
   if (!h_src_idx || !h_ignore_ptr || (h_ignore_ptr[n_req] && !h_ignore_links) || !d_dist || !d_nh)
     return fail(ctx, ORH_E_INVALID, "orh_whatif_run: null argument");
@@ -1988,6 +2036,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       });
       staging.insert(staging.end(), order.begin(), order.end());
     }
+    drain_deferred(ctx);  // a deferred phase 2 may still read the staged request
     int rc = ensure_graph_req(g, staging.size());
     if (rc) return rc;
     ORH_HIP(ctx, hipMemcpyAsync(g->d_req, staging.data(), staging.size() * 4,
@@ -2126,6 +2175,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   a.n_out = n_src;
   a.recs = g->d_recs;
   a.link = g->d_link;
+  bool defer = false;  // this sweep's phase 2 goes to stream2
   if (run_plan.variant == orh::SpfVariant::kMsBfs) {
     int rc = sync_ms_layout(g);
     if (rc) return rc;
@@ -2141,13 +2191,25 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     const size_t scratch =
         a.ms_direct ? 0 : (orh::ms_scratch_bytes(run_plan, N, n_rows) + 255) & ~size_t{255};
     const size_t log_bytes = orh::ms_log_bytes(run_plan, n_rows);
-    rc = ensure_ms_lvl(ctx, scratch + log_bytes);
+    // ORH_SPF_DEFER_HOPS: the level bytes in half p2_half of two. Off unless
+    // ORH_MS_DEFER=1: the 32-sweep C2 step measured 23.1-23.2 ms deferred
+    // against 23.05 (2 lanes; 36.2 ms at 1 lane), i.e. the GPU is already
+    // busy while a sweep's phase 2 runs - the searches and the phase-2
+    // streams share the CUs, so starting the next search earlier only
+    // reorders the same work (profiles/r06/n_defer_ab.txt)
+    static const bool defer_on = [] {
+      const char* e = getenv("ORH_MS_DEFER");
+      return e && e[0] == '1';
+    }();
+    defer = defer_on && (req->flags & ORH_SPF_DEFER_HOPS) && !a.ms_direct && n_extra == 0;
+    const size_t halves = defer ? 2 : 1;
+    rc = ensure_ms_lvl(ctx, halves * scratch + log_bytes);
     if (rc) return rc;
-    a.ms_log = log_bytes ? reinterpret_cast<uint64_t*>(ctx->d_ms_lvl + scratch) : nullptr;
+    a.ms_log = log_bytes ? reinterpret_cast<uint64_t*>(ctx->d_ms_lvl + halves * scratch) : nullptr;
     a.recs = g->d_ms_recs;
     a.dev_of = g->d_ms_dev_of;
     a.host_of = g->d_ms_host_of;
-    a.ms_lvl = ctx->d_ms_lvl;
+    a.ms_lvl = ctx->d_ms_lvl + (defer ? ctx->p2_half * scratch : 0);
     a.lvl_pitch = (N + 15u) & ~15u;
     rc = ensure_lvl_rows(ctx, static_cast<size_t>(n_rows) * a.lvl_pitch);
     if (rc) return rc;
@@ -2206,6 +2268,13 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   h.lvl_pitch = a.lvl_pitch;
   h.w0 = w0;
 
+  if (!defer) {
+    join_deferred(ctx);  // earlier deferred sweeps share the scratch
+  } else if (ctx->p2_pending[ctx->p2_half]) {
+    // the search rewrites the half the phase 2 two sweeps back reads
+    ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_p2[ctx->p2_half], 0));
+    ctx->p2_pending[ctx->p2_half] = false;
+  }
   ORH_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
 #ifdef ORH_DIAG_STAMPS
   static uint64_t* d_diag = nullptr;
@@ -2296,12 +2365,37 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     ORH_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     return ORH_OK;
 #endif
+    hipStream_t s2 = ctx->stream;
+    if (defer) {
+      // phase 2 on stream2 after this search; the context stream is free for
+      // the next sweep's search
+      if (!ctx->stream2) {
+        ORH_HIP(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_ms2, hipEventDisableTiming));
+        ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_p2[0], hipEventDisableTiming));
+        ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_p2[1], hipEventDisableTiming));
+      }
+      ORH_HIP(ctx, hipEventRecord(ctx->ev_ms2, ctx->stream));
+      ORH_HIP(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_ms2, 0));
+      s2 = ctx->stream2;
+    }
     if (!a.ms_direct) {
-      e = orh::launch_ms_finalize(run_plan, a, n_rows, ctx->stream);
+      e = orh::launch_ms_finalize(run_plan, a, n_rows, s2);
       if (e != hipSuccess) return hip_fail(ctx, e, "multi-source finalize launch");
     }
-    e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);
+    e = orh::launch_first_hop(h, max_nbr, s2, &info.hop_nodes, &info.hop_split);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
+    if (defer) {
+      ORH_HIP(ctx, hipEventRecord(ctx->ev_p2[ctx->p2_half], s2));
+      ctx->p2_pending[ctx->p2_half] = true;
+      ctx->p2_half ^= 1u;
+      ctx->last_info = info;
+      ORH_HIP(ctx, hipEventRecord(ctx->ev1, s2));
+      ctx->counters.spf_runs += n_src;
+      ctx->counters.spf_launches += 1;
+      ctx->counters.last_kernel_ms = -1.0;
+      return ORH_OK;
+    }
   } else if (!fused) {
     e = orh::launch_first_hop(h, max_nbr, ctx->stream, &info.hop_nodes, &info.hop_split);
     if (e != hipSuccess) return hip_fail(ctx, e, "first-hop kernel launch");
@@ -2334,6 +2428,7 @@ int orh_spf_batch(orh_graph* g, const orh_spf_request* req, uint32_t words, uint
   uint32_t* d_nh = ctx->d_batch + nd;
   int rc = orh_spf_run(g, req, words, d_dist, d_nh);
   if (rc == ORH_OK) {
+    join_deferred(ctx);
     hipError_t e = hipMemcpyAsync(h_dist, d_dist, nd * 4, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(h_nh, d_nh, nd * words * 4, hipMemcpyDeviceToHost, ctx->stream);
@@ -2375,6 +2470,7 @@ int orh_spf_batch_pinned(orh_graph* g, const orh_spf_request* req, uint32_t word
   }
   int rc = orh_spf_run(g, req, words, ctx->d_batch, ctx->d_batch + nd);
   if (rc != ORH_OK) return rc;
+  join_deferred(ctx);
   hipError_t e = hipMemcpyAsync(ctx->h_pinned, ctx->d_batch, nd * (1 + words) * 4, hipMemcpyDeviceToHost,
                                 ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -2394,6 +2490,7 @@ int orh_spf_run_exact(orh_graph* g, const orh_spf_request* req, uint32_t words, 
   if (!g || !req || (req->n_src && (!req->h_srcs || !d_dist || !d_nh)))
     return g ? fail(g->ctx, ORH_E_INVALID, "orh_spf_run_exact: null argument") : ORH_E_INVALID;
   if (req->n_src == 0) return ORH_OK;
+  join_deferred(g->ctx);
   if (!g->d_recs || g->n_nodes == 0)
     return fail(g->ctx, ORH_E_STATE, "orh_spf_run_exact: no graph loaded");
   return run_exact(g, req, words, nullptr, d_dist, d_nh, d_rank);
@@ -2403,6 +2500,7 @@ int orh_spf_batch_exact(orh_graph* g, const orh_spf_request* req, uint32_t words
                         uint32_t* h_nh, uint32_t* h_rank) {
   if (!g || !req) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  join_deferred(ctx);
   if (req->n_src == 0) return ORH_OK;
   if (!h_dist || !h_nh) return fail(ctx, ORH_E_INVALID, "orh_spf_batch_exact: null output");
   const size_t nd = static_cast<size_t>(req->n_src) * g->n_nodes;
@@ -2592,6 +2690,7 @@ int orh_ksp2(orh_graph* g, uint32_t src, const uint32_t* dsts, uint32_t n_dst, u
              size_t cap, size_t* n_words) {
   if (!g || !n_words || (n_dst && !dsts) || (cap && !out)) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  join_deferred(ctx);
   if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_ksp2: no graph loaded");
   if (src >= g->n_nodes) return fail(ctx, ORH_E_INVALID, "orh_ksp2: source out of range");
   for (uint32_t i = 0; i < n_dst; ++i)
@@ -2665,6 +2764,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
                    const uint32_t** out_blocks, uint32_t* block_words) {
   if (!g || !out_blocks || !block_words || (n_pairs && (!h_src || !h_dst))) return ORH_E_INVALID;
   orh_ctx* ctx = g->ctx;
+  join_deferred(ctx);
   if (!g->d_recs || g->n_nodes == 0) return fail(ctx, ORH_E_STATE, "orh_ksp2_batch: no graph loaded");
   if (g->has_zero || wide_metrics(g))
     return fail(ctx, ORH_E_UNSUPPORTED, "orh_ksp2_batch: zero / 64-bit path metrics need the exact kernel's order");
@@ -3114,6 +3214,7 @@ int orh_route_select_range(orh_prefix_set* ps, uint32_t me_name, uint32_t flags,
                            const orh_select_out* out) {
   if (!ps || !out || (n_areas && !areas)) return ORH_E_INVALID;
   orh_ctx* ctx = ps->ctx;
+  join_deferred(ctx);
   if (pid_lo > pid_hi || pid_hi > ps->hdr.size())
     return fail(ctx, ORH_E_INVALID, "orh_route_select_range: range beyond the prefix set");
   const uint32_t n_prefix = pid_hi;
