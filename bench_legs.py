@@ -520,6 +520,9 @@ def c4_ksp2_block(pairs, rank, world):
     return [i for s in order[lo:hi] for i in by_src[s]]
 
 
+SEARCH_LARGE_BLOCKS = 4  # MultiDeviceWhatIf::kSearchLargeBlocks
+
+
 def rank_c4(hip, rank, world, state=None, reps=3, digest=False):
     """Block `rank` of `world` of the C4 what-if job (copy-on-write, the
     bench's mode) and of the 1,024-pair KSP2 batch (prefetchKthPaths, cold)
@@ -532,7 +535,10 @@ def rank_c4(hip, rank, world, state=None, reps=3, digest=False):
         # the single job's chunking scaled to the block (four chunks of the
         # block: the two row buffers stay 1/world of the single job's)
         chunk = min(C4_WHATIF_CHUNK, max(1024, -(-len(reqs) // 4)))
-        job = ls.what_if_batch(bsrcs, bidx, bsets, chunk, share_base=True)
+        # a 4-way or wider split: the block searches its largest repairs in
+        # full (MultiDeviceWhatIf's rule, ORH_WHATIF_SEARCH_LARGE)
+        job = ls.what_if_batch(bsrcs, bidx, bsets, chunk, share_base=True,
+                               search_large=world >= SEARCH_LARGE_BLOCKS)
         if digest:
             job.set_digests()
         job.run()

@@ -828,11 +828,11 @@ PYBIND11_MODULE(_openr_host, m) {
       .def("what_if_batch",  // a what-if job over `srcs`: request i = (srcs[src_idx[i]], ignore[i])
            [](const LinkState& s, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
               const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric,
-              bool shareBase) {
-             return new WhatIfBatch(s, srcs, srcIdx, ignore, chunk, useLinkMetric, shareBase);
+              bool shareBase, bool searchLarge) {
+             return new WhatIfBatch(s, srcs, srcIdx, ignore, chunk, useLinkMetric, shareBase, searchLarge);
            },
            py::arg("srcs"), py::arg("src_idx"), py::arg("ignore"), py::arg("chunk") = 4096,
-           py::arg("use_link_metric") = true, py::arg("share_base") = false,
+           py::arg("use_link_metric") = true, py::arg("share_base") = false, py::arg("search_large") = false,
            py::return_value_policy::take_ownership, py::keep_alive<0, 1>())
       .def("run_spf_batch",
            [](const LinkState& s, const std::vector<std::string>& srcs,

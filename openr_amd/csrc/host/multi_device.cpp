@@ -277,7 +277,11 @@ MultiDeviceWhatIf::MultiDeviceWhatIf(const ReplicatedLinkState& rls, const std::
       bi.push_back(static_cast<uint32_t>(srcIdx[i] - b.lo));
       bg.push_back(ignore[i]);
     }
-    b.job = std::make_unique<WhatIfBatch>(rls.replica(r), bs, bi, bg, chunk, useLinkMetric, shareBase);
+    // blocks of a 4-way or wider split are short jobs: their largest repairs
+    // are searched in full (ORH_WHATIF_SEARCH_LARGE; rehearsal at 8 blocks:
+    // the slowest block 7.1 -> 5.2 ms, profiles/r06/r_whatif_full_ab.txt)
+    b.job = std::make_unique<WhatIfBatch>(rls.replica(r), bs, bi, bg, chunk, useLinkMetric, shareBase,
+                                          world >= kSearchLargeBlocks);
   }
 }
 

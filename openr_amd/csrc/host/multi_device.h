@@ -108,6 +108,8 @@ std::vector<size_t> equalWorkCuts(const std::vector<double>& w, size_t world);
 // affected count, row digests) come back in the caller's request order.
 class MultiDeviceWhatIf {
  public:
+  // blocks per job from which each block searches its largest repairs in full
+  static constexpr size_t kSearchLargeBlocks = 4;
   MultiDeviceWhatIf(const ReplicatedLinkState& rls, const std::vector<std::string>& srcs,
                     const std::vector<uint32_t>& srcIdx, const std::vector<std::vector<uint32_t>>& ignore,
                     uint32_t chunk, bool useLinkMetric = true, bool shareBase = false);

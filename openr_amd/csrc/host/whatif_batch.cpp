@@ -18,8 +18,8 @@ void check(orh_ctx* ctx, int rc, const char* what) {
 
 WhatIfBatch::WhatIfBatch(const LinkState& ls, const std::vector<std::string>& srcs,
                          const std::vector<uint32_t>& srcIdx, const std::vector<std::vector<uint32_t>>& ignore,
-                         uint32_t chunk, bool useLinkMetric, bool shareBase)
-    : ls_(ls), useLinkMetric_(useLinkMetric), shareBase_(shareBase) {
+                         uint32_t chunk, bool useLinkMetric, bool shareBase, bool searchLarge)
+    : ls_(ls), useLinkMetric_(useLinkMetric), shareBase_(shareBase), searchLarge_(searchLarge) {
   if (srcIdx.size() != ignore.size()) throw std::invalid_argument("WhatIfBatch: one ignore set per request");
   if (chunk == 0) throw std::invalid_argument("WhatIfBatch: chunk must be positive");
   for (const auto& s : srcs) {
@@ -117,7 +117,8 @@ void WhatIfBatch::run() {
     check(ctx_, orh_whatif_create(graph_, srcs_.data(), static_cast<uint32_t>(srcs_.size()), useLinkMetric_ ? 1 : 0,
                                   &job_),
           "orh_whatif_create");
-    if (shareBase_) check(ctx_, orh_whatif_set_flags(job_, ORH_WHATIF_SHARE_BASE), "orh_whatif_set_flags");
+    const uint32_t fl = (shareBase_ ? ORH_WHATIF_SHARE_BASE : 0u) | (searchLarge_ ? ORH_WHATIF_SEARCH_LARGE : 0u);
+    if (fl) check(ctx_, orh_whatif_set_flags(job_, fl), "orh_whatif_set_flags");
   } else {
     check(ctx_, orh_whatif_refresh(job_), "orh_whatif_refresh");
   }

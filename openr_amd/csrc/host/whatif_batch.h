@@ -21,10 +21,12 @@ class WhatIfBatch {
  public:
   // request i = (srcs[srcIdx[i]], ignore[i]) with ignore sets of LinkState link
   // ids; chunk = requests per orh_whatif_run. shareBase: ORH_WHATIF_SHARE_BASE
-  // (a request whose source row stands references the job's base row)
+  // (a request whose source row stands references the job's base row);
+  // searchLarge: ORH_WHATIF_SEARCH_LARGE (the largest repairs searched in
+  // full: for a device's block of a split job)
   WhatIfBatch(const LinkState& ls, const std::vector<std::string>& srcs, const std::vector<uint32_t>& srcIdx,
               const std::vector<std::vector<uint32_t>>& ignore, uint32_t chunk, bool useLinkMetric = true,
-              bool shareBase = false);
+              bool shareBase = false, bool searchLarge = false);
   ~WhatIfBatch();
   WhatIfBatch(const WhatIfBatch&) = delete;
   WhatIfBatch& operator=(const WhatIfBatch&) = delete;
@@ -65,6 +67,7 @@ class WhatIfBatch {
   const LinkState& ls_;
   bool useLinkMetric_;
   bool shareBase_;
+  bool searchLarge_;
   bool digests_{false};
   std::vector<uint32_t> srcs_, srcIdx_;
   std::vector<Chunk> chunks_;

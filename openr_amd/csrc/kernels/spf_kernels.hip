@@ -1658,6 +1658,7 @@ __global__ __launch_bounds__(1024) void spf_global_nh_async_kernel(SpfArgs a) {
 // with, and a node whose distance needed the table stays unreached), so such
 // a row is queued in ovf_rows for the HBM kernel (launch_spf_lds16).
 constexpr uint32_t kSpillSlots = 2048, kSpillProbe = 64;
+constexpr uint32_t kIgnLds = 1024;  // ignore sets up to this size are searched in LDS
 constexpr uint32_t kD16Spill = 0xFFFEu, kD16None = 0xFFFFu;
 
 // The bucket's work count s_work is one LDS word every thread updates: per
@@ -1732,6 +1733,19 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
     s.n_ign = s_nign;  // sorted: the real entries come first
     s.filt = filt;
     s.fshift = fshift;
+    // the set itself into LDS too: a filter hit (every relaxation of an
+    // ignored link - KSP2's k = 2 searches start on the k = 1 path) then
+    // binary-searches LDS instead of a chain of dependent global loads
+#ifndef ORH_LDS16_IGN_GLOBAL  // (A/B builds: the set stays in global memory)
+    if (s.n_ign <= kIgnLds) {
+#else
+    if (false) {
+#endif
+      uint32_t* ign_lds = sp_key + 2 * kSpillSlots;
+      for (uint32_t i = tid; i < s.n_ign; i += nthr) ign_lds[i] = s.ign[i];
+      __syncthreads();
+      s.ign = ign_lds;
+    }
   }
   if (tid == 0) {
     dist[s.node >> 1] &= ~(0xFFFFu << ((s.node & 1u) * 16u));
@@ -3323,7 +3337,7 @@ size_t lds16_bytes(uint32_t n_nodes) {
   const size_t nb = (n_nodes + 31) / 32;
   size_t fw = 1;
   while (2 * fw <= std::min<size_t>(nb, 256)) fw *= 2;
-  return 4 * ((((n_nodes + 1) / 2 + 3) & ~size_t{3}) + 2 * nb + fw + 2 * kSpillSlots);
+  return 4 * ((((n_nodes + 1) / 2 + 3) & ~size_t{3}) + 2 * nb + fw + 2 * kSpillSlots + kIgnLds);
 }
 
 hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows, uint32_t ell_k,

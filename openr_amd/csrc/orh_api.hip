@@ -1466,7 +1466,10 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
     const char* e = getenv("ORH_WHATIF_T3_SPLIT");
     return !(e && atoi(e) == 0);
   }();
-  const bool split = n_slots && full_env == 0 && t3_split;
+  // full searches for the slot tier's queue: ORH_WHATIF_FULL=n (A/B), or the
+  // job's ORH_WHATIF_SEARCH_LARGE (16 per run)
+  const uint32_t full_n = full_env ? full_env : (job->flags & ORH_WHATIF_SEARCH_LARGE) ? 16u : 0u;
+  const bool split = n_slots && full_n == 0 && t3_split;
   if (split) {
     // run slot c's own slot memory, grown only with its stream idle
     if (n_slots * slot_bytes > job->t3_slots_cap[c]) {
@@ -1527,7 +1530,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   // (profiles/r03/r_c4_full_search_ab.txt): the slots stay the default
   if (n_slots) {
     const size_t by_mem = (size_t{1} << 30) / (static_cast<size_t>(N) * 8);
-    ra.full_cap = static_cast<uint32_t>(std::min<size_t>({full_env, by_mem, n_req}));
+    ra.full_cap = static_cast<uint32_t>(std::min<size_t>({full_n, by_mem, n_req}));
     if (ra.full_cap) {
       const size_t need = static_cast<size_t>(ra.full_cap) * N * 8;
       if (need > job->full_lab_cap) {
@@ -1836,7 +1839,8 @@ int orh_whatif_elapsed_ms(orh_whatif* job, double* ms_out) {
 
 int orh_whatif_set_flags(orh_whatif* job, uint32_t flags) {
   if (!job) return ORH_E_INVALID;
-  if (flags & ~ORH_WHATIF_SHARE_BASE) return fail(job->g->ctx, ORH_E_INVALID, "orh_whatif_set_flags: unknown flag");
+  if (flags & ~(ORH_WHATIF_SHARE_BASE | ORH_WHATIF_SEARCH_LARGE))
+    return fail(job->g->ctx, ORH_E_INVALID, "orh_whatif_set_flags: unknown flag");
   job->flags = flags;
   return ORH_OK;
 }

@@ -113,3 +113,20 @@ def row_digest(dist, nh):
         for k in range(nh.shape[1]):
             h = _fmix64(h ^ (nh[:, k] + np.uint64(k) * np.uint64(_K)))
         return int(np.sum(h, dtype=np.uint64))
+
+
+def assert_tiers_match(info, info1, search_large):
+    """Per-request what-if info (ORH_WHATIF_TIER | affected << 3) of a split
+    job against the single job's: equal, except that with
+    ORH_WHATIF_SEARCH_LARGE (a 4-way or wider split) some slot-tier (3)
+    requests are searched in full (tier 4, no affected count). The rows
+    themselves are compared by digest by the caller."""
+    import numpy as np
+    info = np.asarray(info, dtype=np.uint64)
+    info1 = np.asarray(info1, dtype=np.uint64)
+    full = (info & 7) == 4
+    if not search_large:
+        assert np.array_equal(info, info1)
+        return
+    assert np.all((info1[full] & 7) == 3), "a request searched in full was not a slot-tier repair"
+    assert np.array_equal(info[~full], info1[~full])

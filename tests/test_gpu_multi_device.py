@@ -185,7 +185,8 @@ def _c4(hip):
 def test_multi_device_what_if_c4_union(hip, replicas):
     """The benched C4 what-if job (262,144 runSpf(src, true, {link})) split
     over `replicas` device contexts by source block: every request's tier,
-    affected count and row digest (dist + first hops of all 50,000 nodes,
+    affected count (slot-tier requests of a 4-way split may be searched in
+    full instead) and row digest (dist + first hops of all 50,000 nodes,
     orh_row_digest) equal the single-context job's. The split runs
     copy-on-write (the bench's mode) against the dense single job, so the
     shared base rows are pinned too. Blocks run one at a time and release
@@ -212,7 +213,11 @@ def test_multi_device_what_if_c4_union(hip, replicas):
         md.run_block(r)
         md.sync()
         md.release(r)
-    assert np.array_equal(md.info(), info1)
+    # 4 blocks search their largest repairs in full (ORH_WHATIF_SEARCH_LARGE)
+    from helpers import assert_tiers_match
+    assert_tiers_match(md.info(), info1, replicas >= 4)
+    if replicas >= 4:
+        assert np.any((np.asarray(md.info()) & 7) == 4)
     dig = md.digests()
     bad = np.nonzero(dig != dig1)[0]
     assert len(bad) == 0, f"{len(bad)} requests differ, first {bad[:5]}"
