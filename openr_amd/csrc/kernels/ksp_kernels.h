@@ -50,4 +50,12 @@ struct KspArgs {
 
 hipError_t launch_ksp_trace(const KspArgs& a, uint32_t ell_k, hipStream_t s);
 
+// order[0 .. P) = the pairs by descending k = 1 distance of their destination
+// (dist1[row1[i] * N + dst[i]]; pairs with need2[i] == 0 last): the k = 2
+// searches that reach farthest start first, so the batch's last wave of
+// searches is its shortest (P <= 4096, one workgroup)
+hipError_t launch_ksp_order(const uint32_t* dist1, const uint32_t* row1, const uint32_t* dst,
+                            const uint32_t* need2, uint32_t n_nodes, uint32_t n_pairs, uint32_t* order,
+                            hipStream_t s);
+
 }  // namespace orh

@@ -415,6 +415,41 @@ __global__ __launch_bounds__(kWaveWaves * 64) void ksp_trace_wave_kernel(KspArgs
 
 }  // namespace
 
+namespace {
+constexpr uint32_t kOrderMax = 4096;
+
+// rank of pair i = pairs with a larger key, or an equal key and a smaller
+// index (a stable descending order); keys in LDS, P^2 / 1024 compares a thread
+__global__ __launch_bounds__(1024) void ksp_order_kernel(const uint32_t* dist1, const uint32_t* row1,
+                                                         const uint32_t* dst, const uint32_t* need2, uint32_t N,
+                                                         uint32_t P, uint32_t* order) {
+  __shared__ uint32_t key[kOrderMax];
+  for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+    const uint32_t d = need2[i] ? dist1[static_cast<size_t>(row1[i]) * N + dst[i]] : 0u;
+    key[i] = need2[i] ? (d == 0xFFFFFFFFu ? 0xFFFFFFFEu : d) + 1u : 0u;  // searching pairs above the rest
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+    const uint32_t k = key[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < P; ++j) {
+      const uint32_t x = key[j];  // the same j for the whole wave: an LDS broadcast
+      r += (x > k || (x == k && j < i)) ? 1u : 0u;
+    }
+    order[r] = i;
+  }
+}
+}  // namespace
+
+hipError_t launch_ksp_order(const uint32_t* dist1, const uint32_t* row1, const uint32_t* dst,
+                            const uint32_t* need2, uint32_t n_nodes, uint32_t n_pairs, uint32_t* order,
+                            hipStream_t s) {
+  if (n_pairs == 0) return hipSuccess;
+  if (n_pairs > kOrderMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ksp_order_kernel, dim3(1), dim3(1024), 0, s, dist1, row1, dst, need2, n_nodes, n_pairs, order);
+  return hipGetLastError();
+}
+
 hipError_t launch_ksp_trace(const KspArgs& a, uint32_t ell_k, hipStream_t s) {
   if (a.n_pairs == 0) return hipSuccess;
   if ((a.hash_cap & (a.hash_cap - 1)) != 0 || a.out_cap < 4 || a.stack_cap < 2) return hipErrorInvalidValue;

@@ -64,6 +64,9 @@ struct SpfArgs {
   // workgroup b searches row b)
   const uint32_t* row_list;
   const uint32_t* row_count;
+  // u16 LDS search (spf_lds16_kernel): workgroup b searches row row_order[b]
+  // (nullable: row b), e.g. the longest searches first
+  const uint32_t* row_order;
   // HBM kernel (kGlobalNh plan): distances only, u32 labels, out_nh unused
   int32_t dist_only;
   // u16 LDS search (launch_spf_lds16): [0] count, then the rows it left to
@@ -74,6 +77,9 @@ struct SpfArgs {
   // largest u16 label that proves its row fits 16 bits (0xFFFE - max metric)
   const uint32_t* wms_slots;
   uint32_t wms_limit;
+  // 1: a wave owns a contiguous band of J 64-node chunks and a round sweeps it
+  // forward then backward (else chunk j of wave w is j * waves + w, one pass)
+  uint32_t wms_band;
   uint32_t recs_k;  // ELL width of `recs` (kernels launched from plans that do not know it)
 };
 

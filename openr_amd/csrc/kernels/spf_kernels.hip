@@ -1689,7 +1689,7 @@ __global__ __launch_bounds__(1024) void spf_lds16_kernel(SpfArgs a) {
   const uint32_t N = a.n_nodes;
   const uint32_t NB = (N + 31) >> 5;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-  const uint32_t row = blockIdx.x;
+  const uint32_t row = a.row_order ? a.row_order[blockIdx.x] : blockIdx.x;
   if (a.row_mask && !a.row_mask[row]) return;
   constexpr int G = K <= 4 ? ORH_LDS16_G : 2;  // nodes a thread expands together
   const uint32_t DWp = ((N + 1) / 2 + 3) & ~3u;
@@ -2292,10 +2292,16 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   // the in-link slots of the owned nodes: {u (16 bits) | w (15 bits) << 16 |
   // kWmsOvl}; an unused slot (no link, link down) reads u = N, the entry that
   // stays unreached
+  // node of (this thread, j): band schedule - wave w owns chunks [w J, (w +
+  // 1) J) - or interleaved - chunk j * waves + w
+  const bool band = a.wms_band != 0u;
+  const uint32_t wave = tid >> 6;
+  const uint32_t lane = tid & 63u;
+  auto node_of = [&](uint32_t j) { return band ? (wave * J + j) * 64u + lane : j * B + tid; };
   uint32_t slot[J][K];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const uint32_t v = j * B + tid;
+    const uint32_t v = node_of(j);
 #pragma unroll
     for (int k = 0; k < K; ++k) slot[j][k] = v < N ? a.wms_slots[static_cast<size_t>(v) * K + k] : N;
   }
@@ -2305,7 +2311,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   // and is dead from then on like every other slot of an overloaded node
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const uint32_t v = j * B + tid;
+    const uint32_t v = node_of(j);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       if (!(slot[j][k] & kWmsOvl)) continue;
@@ -2335,23 +2341,24 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   uint32_t* chg = reinterpret_cast<uint32_t*>(D + N + 1);  // [3][cw]
   for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
   const uint32_t bw = a.ms_bw;
-  const uint32_t wave = tid >> 6;
   __syncthreads();
   for (uint32_t round = 1;; ++round) {
     int prog = 0;
     const uint32_t* prev = chg + ((round + 2u) % 3u) * cw;
     uint32_t* cur = chg + (round % 3u) * cw;
     if (tid < cw) chg[((round + 1u) % 3u) * cw + tid] = 0u;  // read in round - 1, written in round + 1
-    auto relax = [&](auto jc) {
+    // back: the band schedule's backward sweep, which also sees the chunks
+    // this round's forward sweep changed
+    auto relax = [&](auto jc, bool back) {
       constexpr int j = decltype(jc)::value;
-      const uint32_t v = j * B + tid;
-      const uint32_t c = __builtin_amdgcn_readfirstlane(j * (B >> 6) + wave);  // this slice's chunk
-      if (round > 1 && bw) {
+      const uint32_t v = node_of(j);
+      const uint32_t c = __builtin_amdgcn_readfirstlane(band ? wave * J + j : j * (B >> 6) + wave);  // this slice's chunk
+      if ((round > 1 || back) && bw) {
         const uint32_t lo = c * 64u > bw ? (c * 64u - bw) >> 6 : 0u;
         const uint32_t hi = min(nchunk - 1u, (c * 64u + 63u + bw) >> 6);
         bool act = false;
         for (uint32_t w = lo >> 5; w <= (hi >> 5) && !act; ++w) {
-          uint32_t m = prev[w];
+          uint32_t m = (round > 1 ? prev[w] : 0u) | (back ? cur[w] : 0u);
           if (w == (lo >> 5)) m &= ~0u << (lo & 31u);
           if (w == (hi >> 5) && (hi & 31u) != 31u) m &= (2u << (hi & 31u)) - 1u;
           act = m != 0u;
@@ -2384,7 +2391,9 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
     };
     // (walking the slices backwards in odd rounds, for paths against the
     // slice order, measured no faster: profiles/r06/h_c2w_variants.txt)
-    static_for<J>(relax);
+    static_for<J>([&](auto jc) { relax(jc, false); });
+    if (band)  // and back: a band passes its changes both ways in one round
+      static_for<J>([&](auto jc) { relax(std::integral_constant<int, J - 1 - decltype(jc)::value>{}, true); });
     if (prog) s_prog[round % 3u] = 1u;
     lds_barrier();
     if (!s_prog[round % 3u]) break;
@@ -3362,6 +3371,7 @@ hipError_t launch_spf_lds16(const SpfPlan& fallback, SpfArgs a, uint32_t n_rows,
   SpfArgs b = a;
   b.row_list = a.ovf_rows + 1;
   b.row_count = a.ovf_rows;
+  b.row_order = nullptr;
   return launch_spf(fallback, b, n_rows, s);
 }
 

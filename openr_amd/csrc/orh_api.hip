@@ -2305,6 +2305,13 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     }();
     a.ms_bw = skip ? g->ms_bw_layout : 0u;
     a.recs_k = g->ell_k;
+    // the band schedule (ORH_WMS_BAND=0: interleaved chunks, one sweep per
+    // round, A/B)
+    static const uint32_t band = [] {
+      const char* e = getenv("ORH_WMS_BAND");
+      return (e && e[0] == '0') ? 0u : 1u;
+    }();
+    a.wms_band = band;
   }
   hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
       ? orh::launch_spf_lds_nh(a, n_rows, g->ell_k, lds_nh_packed, run_plan.block, ctx->stream)
@@ -2850,6 +2857,7 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     const size_t o_vis = take(size_t{P} * kKspHashCap);
     const size_t o_st = take(size_t{P} * kKspStackCap * (sizeof(orh::KspFrame) / 4));
     const size_t o_ovf = take(size_t{std::max(S, P)} + 1);
+    const size_t o_ord = take(P);  // k = 2 search order (longest first)
     rc = ensure_bytes(ctx, &ctx->d_ksp, &ctx->d_ksp_cap, off * 4);
     if (rc) return rc;
     uint32_t* D = reinterpret_cast<uint32_t*>(ctx->d_ksp);
@@ -2956,8 +2964,20 @@ int orh_ksp2_batch(orh_graph* g, uint32_t n_pairs, const uint32_t* h_src, const 
     a.row_mask = D + o_need;
     a.stop_ptr = stop ? D + o_sp2 : nullptr;
     a.stop_nodes = stop ? D + o_dst : nullptr;
+    // the LDS searches start with the pairs whose k = 1 destination is
+    // farthest (ORH_KSP_ORDER=0: pair order, A/B)
+    static const bool by_dist = [] {
+      const char* oe = getenv("ORH_KSP_ORDER");
+      return !(oe && oe[0] == '0');
+    }();
+    if (use_lds16 && by_dist && P <= 4096) {
+      e = orh::launch_ksp_order(D + o_d1, D + o_r1, D + o_dst, D + o_need, N, P, D + o_ord, ctx->stream);
+      if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 order launch");
+      a.row_order = D + o_ord;
+    }
     fp.block = block_for(P);
     e = search(a, P);
+    a.row_order = nullptr;
     if (e != hipSuccess) return hip_fail(ctx, e, "ksp2 k=2 search launch");
     mark(4);
     ORH_HIP(ctx, hipMemsetAsync(D + o_vis, 0, size_t{P} * kKspHashCap * 4, ctx->stream));
