@@ -2342,6 +2342,16 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
   const uint32_t bw = a.ms_bw;
   __syncthreads();
+  // a node's label is written only by the thread that owns it (after the
+  // setup above): the owner keeps its J labels in registers too and reads
+  // only the in-neighbours' from LDS (ORH_WMS_OWN_LDS, A/B builds: the own
+  // label read back from LDS as well)
+  uint2 mine[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t v = node_of(j);
+    mine[j] = v < N ? D[v] : make_uint2(~0u, ~0u);
+  }
   for (uint32_t round = 1;; ++round) {
     int prog = 0;
     const uint32_t* prev = chg + ((round + 2u) % 3u) * cw;
@@ -2373,7 +2383,11 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       uint2 du[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) du[k] = D[slot[j][k] & 0xFFFFu];
+#ifdef ORH_WMS_OWN_LDS
       const uint2 own = D[v];
+#else
+      const uint2 own = mine[j];
+#endif
       uint2 acc = own;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -2385,15 +2399,21 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       const bool changed = acc.x != own.x || acc.y != own.y;
       if (changed) {
         D[v] = acc;
+        mine[j] = acc;
         prog = 1;
       }
       if (__builtin_amdgcn_ballot_w64(changed) && (tid & 63u) == 0u) atomicOr(&cur[c >> 5], 1u << (c & 31u));
     };
     // (walking the slices backwards in odd rounds, for paths against the
     // slice order, measured no faster: profiles/r06/h_c2w_variants.txt)
-    static_for<J>([&](auto jc) { relax(jc, false); });
-    if (band)  // and back: a band passes its changes both ways in one round
-      static_for<J>([&](auto jc) { relax(std::integral_constant<int, J - 1 - decltype(jc)::value>{}, true); });
+#ifndef ORH_WMS_PASSES
+#define ORH_WMS_PASSES 1  // forward + backward sweeps of a band per round (A/B builds)
+#endif
+    for (int pass = 0; pass < (band ? ORH_WMS_PASSES : 1); ++pass) {
+      static_for<J>([&](auto jc) { relax(jc, pass > 0); });
+      if (band)  // and back: a band passes its changes both ways in one round
+        static_for<J>([&](auto jc) { relax(std::integral_constant<int, J - 1 - decltype(jc)::value>{}, true); });
+    }
     if (prog) s_prog[round % 3u] = 1u;
     lds_barrier();
     if (!s_prog[round % 3u]) break;

@@ -2297,21 +2297,18 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
     a.dev_of = g->d_ms_dev_of;
     a.wms_slots = g->d_wms;
     a.wms_limit = 0xFFFEu - g->wms_maxw;
-    // the in-links' reach in layout ids: the activity skip (ORH_WMS_SKIP=0:
-    // every slice every round)
-    static const bool skip = [] {
-      const char* e = getenv("ORH_WMS_SKIP");
-      return !(e && e[0] == '0');
-    }();
+    // the in-links' reach in layout ids: the activity skip, opt-in
+    // (ORH_WMS_SKIP=1). Its per-slice bitmap test costs more than the slices
+    // it skips once a round sweeps each band both ways: C2w distances 5.07 ms
+    // with it, 3.58 ms without (profiles/r06/v_wms_skip_ab.txt)
+    const char* skip_e = getenv("ORH_WMS_SKIP");  // read per run (tests flip it)
+    const bool skip = skip_e && skip_e[0] == '1';
     a.ms_bw = skip ? g->ms_bw_layout : 0u;
     a.recs_k = g->ell_k;
     // the band schedule (ORH_WMS_BAND=0: interleaved chunks, one sweep per
     // round, A/B)
-    static const uint32_t band = [] {
-      const char* e = getenv("ORH_WMS_BAND");
-      return (e && e[0] == '0') ? 0u : 1u;
-    }();
-    a.wms_band = band;
+    const char* band_e = getenv("ORH_WMS_BAND");  // read per run (tests flip it)
+    a.wms_band = (band_e && band_e[0] == '0') ? 0u : 1u;
   }
   hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
       ? orh::launch_spf_lds_nh(a, n_rows, g->ell_k, lds_nh_packed, run_plan.block, ctx->stream)
