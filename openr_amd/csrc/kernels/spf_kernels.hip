@@ -2342,16 +2342,9 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
   const uint32_t bw = a.ms_bw;
   __syncthreads();
-  // a node's label is written only by the thread that owns it (after the
-  // setup above): the owner keeps its J labels in registers too and reads
-  // only the in-neighbours' from LDS (ORH_WMS_OWN_LDS, A/B builds: the own
-  // label read back from LDS as well)
-  uint2 mine[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const uint32_t v = node_of(j);
-    mine[j] = v < N ? D[v] : make_uint2(~0u, ~0u);
-  }
+  // (the owner keeping its J labels in registers instead of reading its own
+  // back from LDS measured slower: C2w distances 3.65 vs 3.55 ms,
+  // profiles/r06/x_wms_ab.txt; two forward/backward passes per round 3.72)
   for (uint32_t round = 1;; ++round) {
     int prog = 0;
     const uint32_t* prev = chg + ((round + 2u) % 3u) * cw;
@@ -2383,11 +2376,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       uint2 du[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) du[k] = D[slot[j][k] & 0xFFFFu];
-#ifdef ORH_WMS_OWN_LDS
       const uint2 own = D[v];
-#else
-      const uint2 own = mine[j];
-#endif
       uint2 acc = own;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -2399,7 +2388,6 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       const bool changed = acc.x != own.x || acc.y != own.y;
       if (changed) {
         D[v] = acc;
-        mine[j] = acc;
         prog = 1;
       }
       if (__builtin_amdgcn_ballot_w64(changed) && (tid & 63u) == 0u) atomicOr(&cur[c >> 5], 1u << (c & 31u));
