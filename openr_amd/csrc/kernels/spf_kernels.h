@@ -127,14 +127,16 @@ enum class SpfVariant {
   kLdsNh,     // general metrics, labels {dist, first hops} in LDS, first hops fused (no phase 2)
   kWms        // general metrics, many sources: 4-source Bellman-Ford in LDS, then phase 2
 };
-// spf_wms_kernel: LDS bytes of one 4-source batch (u16 x 4 per node + 1)
-size_t wms_lds_bytes(uint32_t n_nodes);
-// batches of 4 rows (a.order), 1024 threads each; rows whose labels come too
+// spf_wms_kernel: LDS bytes of one batch of `sources` (4 or 8) sources
+// (u16 x sources per node + 1), and the batch width launch_spf_wms takes
+size_t wms_lds_bytes(uint32_t n_nodes, uint32_t sources = 4);
+uint32_t wms_sources(uint32_t n_nodes, size_t lds_limit);
+// batches of 4 or 8 rows (a.order; wms_sources), 1024 threads each; rows whose labels come too
 // close to 16 bits are listed in a.ovf_rows (n_rows + 1 words) and redone by
 // the u64 spf_lds_nh_kernel (its LDS must fit). Writes dist rows only.
 // wms_k: in-link slots per node of a.wms_slots (4 or 8); a.recs_k: the ELL
 // width of a.recs (for the u64 LDS search of the flagged rows)
-hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, hipStream_t s);
+hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, size_t lds_limit, hipStream_t s);
 // spf_lds_nh_kernel: LDS bytes per search (packed: u32 labels, <= 16
 // distinct neighbours per source; else u64 labels)
 size_t lds_nh_bytes(uint32_t n_nodes, bool packed);

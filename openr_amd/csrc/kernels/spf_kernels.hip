@@ -2269,17 +2269,25 @@ __device__ inline uint32_t pk_min_u16(uint32_t a, uint32_t b) {
 #else
 #define ORH_WMS_ATTR
 #endif
-template <int K, int J>
+// S = 4 or 8 sources per batch: a node's labels are S u16 in S / 2 dwords
+// (8: 16 B per node, so N <= ~10,200 fits one batch per CU)
+template <int K, int J, int S>
 __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  constexpr uint32_t S = 4;
+  constexpr uint32_t W = S / 2;  // dwords per node
+  typedef uint32_t DV __attribute__((ext_vector_type(W)));
   const uint32_t N = a.n_nodes;
   const uint32_t tid = threadIdx.x, B = blockDim.x;
   const uint32_t b0 = blockIdx.x * S;
-  const uint32_t nsrc = min(S, a.n_rows - b0);
+  const uint32_t nsrc = min(static_cast<uint32_t>(S), a.n_rows - b0);
   __shared__ uint32_t s_prog[3], s_ovf;
-  uint2* D = reinterpret_cast<uint2*>(lds);  // [N + 1]; D[N] stays unreached
-  for (uint32_t i = tid; i <= N; i += B) D[i] = make_uint2(~0u, ~0u);
+  DV* D = reinterpret_cast<DV*>(lds);  // [N + 1]; D[N] stays unreached
+  {
+    DV none;
+#pragma unroll
+    for (uint32_t q = 0; q < W; ++q) none[q] = ~0u;
+    for (uint32_t i = tid; i <= N; i += B) D[i] = none;
+  }
   if (tid < 3) s_prog[tid] = 0u;
   if (tid == 0) s_ovf = 0u;
   __syncthreads();
@@ -2317,14 +2325,13 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       if (!(slot[j][k] & kWmsOvl)) continue;
       const uint32_t u = slot[j][k] & 0xFFFFu, w = (slot[j][k] >> 16) & 0x7FFFu;
       slot[j][k] = N;
-      const uint2 du = D[u];
-      const uint32_t lz[4] = {du.x & 0xFFFFu, du.x >> 16, du.y & 0xFFFFu, du.y >> 16};
-      uint32_t c[4];
+      const DV du = D[u];
+      DV d = D[v];  // v < N: a slot of a padding node is never flagged
 #pragma unroll
-      for (int q = 0; q < 4; ++q) c[q] = lz[q] == 0u ? w : 0xFFFFu;
-      uint2 d = D[v];  // v < N: a slot of a padding node is never flagged
-      d.x = pk_min_u16(d.x, c[0] | (c[1] << 16));
-      d.y = pk_min_u16(d.y, c[2] | (c[3] << 16));
+      for (uint32_t q = 0; q < W; ++q) {
+        const uint32_t lo = (du[q] & 0xFFFFu) == 0u ? w : 0xFFFFu, hi = (du[q] >> 16) == 0u ? w : 0xFFFFu;
+        d[q] = pk_min_u16(d[q], lo | (hi << 16));
+      }
       D[v] = d;
     }
   }
@@ -2373,19 +2380,21 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       // again each time instead of held in J * K more registers
 #pragma unroll
       for (int k = 0; k < K; ++k) asm volatile("" : "+v"(slot[j][k]));
-      uint2 du[K];
+      DV du[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) du[k] = D[slot[j][k] & 0xFFFFu];
-      const uint2 own = D[v];
-      uint2 acc = own;
+      const DV own = D[v];
+      DV acc = own;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         // {w, w}: the high half twice (an unused slot: w = 0 on the unreached entry)
         const uint32_t wr = __builtin_amdgcn_perm(slot[j][k], slot[j][k], 0x03020302u);
-        acc.x = pk_min_u16(acc.x, pk_add_sat_u16(du[k].x, wr));
-        acc.y = pk_min_u16(acc.y, pk_add_sat_u16(du[k].y, wr));
+#pragma unroll
+        for (uint32_t q = 0; q < W; ++q) acc[q] = pk_min_u16(acc[q], pk_add_sat_u16(du[k][q], wr));
       }
-      const bool changed = acc.x != own.x || acc.y != own.y;
+      bool changed = false;
+#pragma unroll
+      for (uint32_t q = 0; q < W; ++q) changed |= acc[q] != own[q];
       if (changed) {
         D[v] = acc;
         prog = 1;
@@ -2416,13 +2425,13 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
     out[k] = k < nsrc ? dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + k]) : nullptr;
   bool ovf = false;
   for (uint32_t i = tid; i < N; i += B) {
-    const uint2 d = D[a.dev_of[i]];
-    const uint32_t l[S] = {d.x & 0xFFFFu, d.x >> 16, d.y & 0xFFFFu, d.y >> 16};
+    const DV d = D[a.dev_of[i]];
 #pragma unroll
     for (uint32_t k = 0; k < S; ++k) {
       if (k >= nsrc) break;
-      ovf |= l[k] != 0xFFFFu && l[k] > lim;
-      __builtin_nontemporal_store(l[k] == 0xFFFFu ? kInf : l[k], &out[k][i]);
+      const uint32_t l = (d[k / 2] >> ((k & 1u) * 16u)) & 0xFFFFu;
+      ovf |= l != 0xFFFFu && l > lim;
+      __builtin_nontemporal_store(l == 0xFFFFu ? kInf : l, &out[k][i]);
     }
   }
   if (ovf) s_ovf = 1u;
@@ -2433,9 +2442,9 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   }
 }
 
-size_t wms_lds_bytes(uint32_t n_nodes) {
+size_t wms_lds_bytes(uint32_t n_nodes, uint32_t sources) {
   const size_t cw = (static_cast<size_t>(n_nodes) + 63) / 64 / 32 + 1;
-  return (static_cast<size_t>(n_nodes) + 1) * 8 + 3 * cw * 4;  // labels, then the chunk-change bitmaps
+  return (static_cast<size_t>(n_nodes) + 1) * 2 * sources + 3 * cw * 4;  // labels, then the chunk-change bitmaps
 }
 
 size_t lds_nh_bytes(uint32_t n_nodes, bool packed) {
@@ -3408,22 +3417,39 @@ hipError_t launch_spf_lds_nh(SpfArgs a, uint32_t n_rows, uint32_t ell_k, bool pa
                     : launch(spf_lds_nh_kernel<4, false>, a, n_rows, block, lds, s);
 }
 
-template <int K>
+template <int K, int S>
 static hipError_t launch_wms_k(const SpfArgs& a, uint32_t batches, size_t lds, hipStream_t s) {
   const uint32_t j = (a.n_nodes + 1023) / 1024;
-  switch (j <= 2 ? 2 : j <= 4 ? 4 : j <= 6 ? 6 : j <= 8 ? 8 : j <= 10 ? 10 : j <= 12 ? 12 : j <= 16 ? 16 : 20) {
-    case 2: return launch(spf_wms_kernel<K, 2>, a, batches, 1024, lds, s);
-    case 4: return launch(spf_wms_kernel<K, 4>, a, batches, 1024, lds, s);
-    case 6: return launch(spf_wms_kernel<K, 6>, a, batches, 1024, lds, s);
-    case 8: return launch(spf_wms_kernel<K, 8>, a, batches, 1024, lds, s);
-    case 10: return launch(spf_wms_kernel<K, 10>, a, batches, 1024, lds, s);
-    case 12: return launch(spf_wms_kernel<K, 12>, a, batches, 1024, lds, s);
-    case 16: return launch(spf_wms_kernel<K, 16>, a, batches, 1024, lds, s);
-    default: return launch(spf_wms_kernel<K, 20>, a, batches, 1024, lds, s);
+  if constexpr (S == 8) {  // 16 B a node: N <= ~10,200, J <= 10
+    switch (j <= 2 ? 2 : j <= 4 ? 4 : j <= 6 ? 6 : j <= 8 ? 8 : 10) {
+      case 2: return launch(spf_wms_kernel<K, 2, 8>, a, batches, 1024, lds, s);
+      case 4: return launch(spf_wms_kernel<K, 4, 8>, a, batches, 1024, lds, s);
+      case 6: return launch(spf_wms_kernel<K, 6, 8>, a, batches, 1024, lds, s);
+      case 8: return launch(spf_wms_kernel<K, 8, 8>, a, batches, 1024, lds, s);
+      default: return launch(spf_wms_kernel<K, 10, 8>, a, batches, 1024, lds, s);
+    }
+  } else {
+    switch (j <= 2 ? 2 : j <= 4 ? 4 : j <= 6 ? 6 : j <= 8 ? 8 : j <= 10 ? 10 : j <= 12 ? 12 : j <= 16 ? 16 : 20) {
+      case 2: return launch(spf_wms_kernel<K, 2, 4>, a, batches, 1024, lds, s);
+      case 4: return launch(spf_wms_kernel<K, 4, 4>, a, batches, 1024, lds, s);
+      case 6: return launch(spf_wms_kernel<K, 6, 4>, a, batches, 1024, lds, s);
+      case 8: return launch(spf_wms_kernel<K, 8, 4>, a, batches, 1024, lds, s);
+      case 10: return launch(spf_wms_kernel<K, 10, 4>, a, batches, 1024, lds, s);
+      case 12: return launch(spf_wms_kernel<K, 12, 4>, a, batches, 1024, lds, s);
+      case 16: return launch(spf_wms_kernel<K, 16, 4>, a, batches, 1024, lds, s);
+      default: return launch(spf_wms_kernel<K, 20, 4>, a, batches, 1024, lds, s);
+    }
   }
 }
 
-hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, hipStream_t s) {
+uint32_t wms_sources(uint32_t n_nodes, size_t lds_limit) {
+  // ORH_WMS_SOURCES=4 (A/B): 4-source batches even where 8 fit
+  const char* e = getenv("ORH_WMS_SOURCES");  // read per launch (tests flip it)
+  const bool four = e && atoi(e) == 4;
+  return !four && n_nodes <= 10240 && wms_lds_bytes(n_nodes, 8) <= lds_limit ? 8u : 4u;
+}
+
+hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, size_t lds_limit, hipStream_t s) {
   if (n_rows == 0) return hipSuccess;
   if (!a.ovf_rows || !a.wms_slots || a.n_nodes > 20480 || a.n_nodes >= 0xFFFFu) return hipErrorInvalidValue;
   a.n_rows = n_rows;
@@ -3431,9 +3457,15 @@ hipError_t launch_spf_wms(SpfArgs a, uint32_t n_rows, uint32_t wms_k, hipStream_
   a.row_count = nullptr;
   hipError_t e = hipMemsetAsync(a.ovf_rows, 0, 4, s);
   if (e != hipSuccess) return e;
-  const uint32_t batches = (n_rows + 3) / 4;
-  const size_t lds = wms_lds_bytes(a.n_nodes);
-  e = wms_k == 8 ? launch_wms_k<8>(a, batches, lds, s) : launch_wms_k<4>(a, batches, lds, s);
+  // 8 sources per batch where their labels fit one CU's LDS (the rounds, the
+  // barriers and the slot registers then serve twice the sources)
+  const uint32_t S = wms_sources(a.n_nodes, lds_limit);
+  const uint32_t batches = (n_rows + S - 1) / S;
+  const size_t lds = wms_lds_bytes(a.n_nodes, S);
+  if (S == 8)
+    e = wms_k == 8 ? launch_wms_k<8, 8>(a, batches, lds, s) : launch_wms_k<4, 8>(a, batches, lds, s);
+  else
+    e = wms_k == 8 ? launch_wms_k<8, 4>(a, batches, lds, s) : launch_wms_k<4, 4>(a, batches, lds, s);
   if (e != hipSuccess) return e;
   // rows whose distances may not fit 16 bits: the u64 LDS search over the
   // list (workgroups past its length exit at once); its first-hop rows are

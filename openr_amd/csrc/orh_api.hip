@@ -1468,7 +1468,11 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   }();
   // full searches for the slot tier's queue: ORH_WHATIF_FULL=n (A/B), or the
   // job's ORH_WHATIF_SEARCH_LARGE (16 per run)
-  const uint32_t full_n = full_env ? full_env : (job->flags & ORH_WHATIF_SEARCH_LARGE) ? 16u : 0u;
+  static const uint32_t large_cap = [] {  // ORH_WHATIF_SEARCH_CAP (A/B): the flag's searches per run
+    const char* e = getenv("ORH_WHATIF_SEARCH_CAP");
+    return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 16u;
+  }();
+  const uint32_t full_n = full_env ? full_env : (job->flags & ORH_WHATIF_SEARCH_LARGE) ? large_cap : 0u;
   const bool split = n_slots && full_n == 0 && t3_split;
   if (split) {
     // run slot c's own slot memory, grown only with its stream idle
@@ -2312,7 +2316,7 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
   }
   hipError_t e = run_plan.variant == orh::SpfVariant::kLdsNh
       ? orh::launch_spf_lds_nh(a, n_rows, g->ell_k, lds_nh_packed, run_plan.block, ctx->stream)
-      : run_plan.variant == orh::SpfVariant::kWms ? orh::launch_spf_wms(a, n_rows, g->wms_k, ctx->stream)
+      : run_plan.variant == orh::SpfVariant::kWms ? orh::launch_spf_wms(a, n_rows, g->wms_k, ctx->lds_limit, ctx->stream)
       : orh::launch_spf(run_plan, a, n_rows, ctx->stream);
   if (e != hipSuccess) { std::string m = "spf kernel launch variant " + std::to_string(int(run_plan.variant)) + " rows " + std::to_string(n_rows) + " lds " + std::to_string(run_plan.lds_bytes) + " block " + std::to_string(run_plan.block) + " j " + std::to_string(run_plan.ms_j); return hip_fail(ctx, e, m.c_str()); }
 #ifdef ORH_DIAG_STAMPS

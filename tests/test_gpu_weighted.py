@@ -124,14 +124,15 @@ def test_random_weighted_all_rows(hip, oracle, seed):
 
 
 @pytest.mark.parametrize("env", [{}, {"ORH_WMS_SKIP": "1"}, {"ORH_WMS_BAND": "0"},
-                                 {"ORH_WMS_BAND": "0", "ORH_WMS_SKIP": "1"}])
+                                 {"ORH_WMS_BAND": "0", "ORH_WMS_SKIP": "1"}, {"ORH_WMS_SOURCES": "4"}])
 @pytest.mark.parametrize("seed", [85, 86])
 def test_random_weighted_wms(hip, oracle, monkeypatch, seed, env):
     """The same kind of graph (parallel links, overloaded nodes - sources
     among them - and drained links), every node twice as a source: the WMS
     batches (repeated sources inside a batch, overloaded sources reaching
     only their neighbours), all rows vs the oracle; the default schedule
-    (bands swept both ways, no activity skip) and the opt-in variants."""
+    (8-source batches, bands swept both ways, no activity skip) and the
+    opt-in variants."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     dbs = _random_weighted(seed, n=250, extra=250, max_metric=30)
