@@ -17,7 +17,9 @@
 #include <cstring>
 #include <malloc.h>
 #include <mutex>
+#include <pthread.h>
 #include <sched.h>
+#include <string>
 #include <stdexcept>
 #include <thread>
 #include <vector>
@@ -86,7 +88,55 @@ class WorkerPool {
     // mask throttles a pool that fills it: profiles/r05/ cpu.stat A/B)
     size_t t = std::min<size_t>(16, usableCpus() > 2 ? usableCpus() - 1 : usableCpus());
     if (const char* e = std::getenv("ORH_HOST_THREADS")) t = std::max(1, std::atoi(e));
-    for (size_t i = 1; i < t; ++i) workers_.emplace_back([this] { loop(); });
+    // ORH_POOL_PIN=1 (A/B): each worker pinned to its own physical core of
+    // the caller's socket, nearest core ids first (the default leaves the
+    // workers to the scheduler, which may spread them over sockets)
+    const char* pe = std::getenv("ORH_POOL_PIN");
+    const std::vector<int> pins = (pe && pe[0] == '1') ? nearCores(t - 1) : std::vector<int>{};
+    for (size_t i = 1; i < t; ++i) {
+      workers_.emplace_back([this] { loop(); });
+      if (i - 1 < pins.size()) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(pins[i - 1], &one);
+        pthread_setaffinity_np(workers_.back().native_handle(), sizeof one, &one);
+      }
+    }
+  }
+  static int readInt(const std::string& path) {
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int v = -1;
+    if (std::fscanf(f, "%d", &v) != 1) v = -1;
+    std::fclose(f);
+    return v;
+  }
+  // up to n CPUs of the affinity mask: one hardware thread per physical core
+  // of the calling thread's package, by distance of cpu id from the caller's
+  static std::vector<int> nearCores(size_t n) {
+    std::vector<int> out;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return out;
+    const int me = sched_getcpu();
+    if (me < 0) return out;
+    auto topo = [](int c, const char* f) {
+      return readInt("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/" + f);
+    };
+    const int pkg = topo(me, "physical_package_id");
+    std::vector<std::pair<int, int>> cand;  // (distance, cpu)
+    std::vector<std::pair<int, int>> seen;  // (package, core)
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      if (!CPU_ISSET(c, &set) || c == me) continue;
+      const int p = topo(c, "physical_package_id"), core = topo(c, "core_id");
+      if (p != pkg || core < 0) continue;
+      if (std::find(seen.begin(), seen.end(), std::make_pair(p, core)) != seen.end()) continue;
+      seen.emplace_back(p, core);
+      cand.emplace_back(std::abs(c - me), c);
+    }
+    std::sort(cand.begin(), cand.end());
+    for (size_t i = 0; i < cand.size() && out.size() < n; ++i) out.push_back(cand[i].second);
+    return out;
   }
   // CPUs this process may use: the affinity mask, capped by the cgroup v2
   // quota (cpu.max "quota period")

@@ -1470,7 +1470,7 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   // job's ORH_WHATIF_SEARCH_LARGE (16 per run)
   static const uint32_t large_cap = [] {  // ORH_WHATIF_SEARCH_CAP (A/B): the flag's searches per run
     const char* e = getenv("ORH_WHATIF_SEARCH_CAP");
-    return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 16u;
+    return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 32u;  // 8 / 16 / 32: profiles/r06/ab_search_cap.txt
   }();
   const uint32_t full_n = full_env ? full_env : (job->flags & ORH_WHATIF_SEARCH_LARGE) ? large_cap : 0u;
   const bool split = n_slots && full_n == 0 && t3_split;
