@@ -88,11 +88,18 @@ class WorkerPool {
     // mask throttles a pool that fills it: profiles/r05/ cpu.stat A/B)
     size_t t = std::min<size_t>(16, usableCpus() > 2 ? usableCpus() - 1 : usableCpus());
     if (const char* e = std::getenv("ORH_HOST_THREADS")) t = std::max(1, std::atoi(e));
-    // ORH_POOL_PIN=1 (A/B): each worker pinned to its own physical core of
-    // the caller's socket, nearest core ids first (the default leaves the
-    // workers to the scheduler, which may spread them over sockets)
+    // each worker pinned to its own physical core of the caller's socket,
+    // nearest core ids first, instead of left to the scheduler, which spreads
+    // them over sockets and away from the memory the caller filled: C3 build
+    // 4.0 -> 2.9 ms, C5 53-58 -> 44-48 ms on one box
+    // (profiles/r06/ac_pool_pin_ab.txt). Only the pool's own threads are
+    // pinned. Default: on in a single-process run, off when WORLD_SIZE > 1
+    // (ranks on one node would pick overlapping cores); ORH_POOL_PIN=0 / 1
+    // forces it
     const char* pe = std::getenv("ORH_POOL_PIN");
-    const std::vector<int> pins = (pe && pe[0] == '1') ? nearCores(t - 1) : std::vector<int>{};
+    const char* ws = std::getenv("WORLD_SIZE");
+    const bool pin = pe ? pe[0] == '1' : !(ws && std::atoi(ws) > 1);
+    const std::vector<int> pins = pin ? nearCores(t - 1) : std::vector<int>{};
     for (size_t i = 1; i < t; ++i) {
       workers_.emplace_back([this] { loop(); });
       if (i - 1 < pins.size()) {
