@@ -2282,18 +2282,48 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   const uint32_t nsrc = min(static_cast<uint32_t>(S), a.n_rows - b0);
   __shared__ uint32_t s_prog[3], s_ovf;
   DV* D = reinterpret_cast<DV*>(lds);  // [N + 1]; D[N] stays unreached
+  // kSplit (ORH_WMS_SPLIT builds, S = 8): sources 0-3 and 4-7 in two arrays
+  // of 8-byte entries, read by two ds_read_b64 instead of one ds_read_b128
+  // (whose 16-lane groups take a conflict at every shift of the neighbour
+  // offset inside a wave)
+#ifdef ORH_WMS_SPLIT
+  constexpr bool kSplit = S == 8;
+#else
+  constexpr bool kSplit = false;
+#endif
+  uint2* H0 = reinterpret_cast<uint2*>(lds);
+  uint2* H1 = H0 + (N + 1);
+  auto ld = [&](uint32_t u) -> DV {
+    if constexpr (kSplit) {
+      const uint2 x = H0[u], y = H1[u];
+      DV r;
+      r[0] = x.x; r[1] = x.y; r[2 % W] = y.x; r[3 % W] = y.y;
+      return r;
+    } else {
+      return D[u];
+    }
+  };
+  auto st = [&](uint32_t u, const DV& v) {
+    if constexpr (kSplit) {
+      H0[u] = make_uint2(v[0], v[1]);
+      H1[u] = make_uint2(v[2 % W], v[3 % W]);
+    } else {
+      D[u] = v;
+    }
+  };
   {
     DV none;
 #pragma unroll
     for (uint32_t q = 0; q < W; ++q) none[q] = ~0u;
-    for (uint32_t i = tid; i <= N; i += B) D[i] = none;
+    for (uint32_t i = tid; i <= N; i += B) st(i, none);
   }
   if (tid < 3) s_prog[tid] = 0u;
   if (tid == 0) s_ovf = 0u;
   __syncthreads();
   if (tid < nsrc) {  // sources may repeat: clear each lane's half alone
     const uint32_t src = a.dev_of[a.srcs[a.order[b0 + tid]]];
-    uint32_t* w = reinterpret_cast<uint32_t*>(D + src) + (tid >> 1);
+    uint32_t* w = kSplit ? reinterpret_cast<uint32_t*>((tid >> 2) ? H1 + src : H0 + src) + ((tid >> 1) & 1u)
+                         : reinterpret_cast<uint32_t*>(D + src) + (tid >> 1);
     atomicAnd(w, (tid & 1u) ? 0x0000FFFFu : 0xFFFF0000u);
   }
   __syncthreads();
@@ -2325,14 +2355,14 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       if (!(slot[j][k] & kWmsOvl)) continue;
       const uint32_t u = slot[j][k] & 0xFFFFu, w = (slot[j][k] >> 16) & 0x7FFFu;
       slot[j][k] = N;
-      const DV du = D[u];
-      DV d = D[v];  // v < N: a slot of a padding node is never flagged
+      const DV du = ld(u);
+      DV d = ld(v);  // v < N: a slot of a padding node is never flagged
 #pragma unroll
       for (uint32_t q = 0; q < W; ++q) {
         const uint32_t lo = (du[q] & 0xFFFFu) == 0u ? w : 0xFFFFu, hi = (du[q] >> 16) == 0u ? w : 0xFFFFu;
         d[q] = pk_min_u16(d[q], lo | (hi << 16));
       }
-      D[v] = d;
+      st(v, d);
     }
   }
   __syncthreads();
@@ -2345,7 +2375,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
   // the next one.) Three rotating bitmaps: one read, one written, one cleared.
   // a.ms_bw = 0: every slice every round (ORH_WMS_SKIP, orh_spf_run)
   const uint32_t nchunk = (N + 63) / 64, cw = (nchunk + 31) / 32;
-  uint32_t* chg = reinterpret_cast<uint32_t*>(D + N + 1);  // [3][cw]
+  uint32_t* chg = reinterpret_cast<uint32_t*>(D + N + 1);  // [3][cw] (kSplit: H1 + N + 1, the same bytes)
   for (uint32_t i = tid; i < 3 * cw; i += B) chg[i] = 0u;
   const uint32_t bw = a.ms_bw;
   __syncthreads();
@@ -2382,8 +2412,8 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
       for (int k = 0; k < K; ++k) asm volatile("" : "+v"(slot[j][k]));
       DV du[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) du[k] = D[slot[j][k] & 0xFFFFu];
-      const DV own = D[v];
+      for (int k = 0; k < K; ++k) du[k] = ld(slot[j][k] & 0xFFFFu);
+      const DV own = ld(v);
       DV acc = own;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -2396,7 +2426,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
 #pragma unroll
       for (uint32_t q = 0; q < W; ++q) changed |= acc[q] != own[q];
       if (changed) {
-        D[v] = acc;
+        st(v, acc);
         prog = 1;
       }
       if (__builtin_amdgcn_ballot_w64(changed) && (tid & 63u) == 0u) atomicOr(&cur[c >> 5], 1u << (c & 31u));
@@ -2425,7 +2455,7 @@ __global__ __launch_bounds__(1024) ORH_WMS_ATTR void spf_wms_kernel(SpfArgs a) {
     out[k] = k < nsrc ? dist_row(a.out_dist, a.scratch, a.n_out, N, a.order[b0 + k]) : nullptr;
   bool ovf = false;
   for (uint32_t i = tid; i < N; i += B) {
-    const DV d = D[a.dev_of[i]];
+    const DV d = ld(a.dev_of[i]);
 #pragma unroll
     for (uint32_t k = 0; k < S; ++k) {
       if (k >= nsrc) break;
