@@ -113,6 +113,7 @@ struct HopArgs {
   // level-row kernel block order: 0 = one contiguous source range per XCD,
   // G > 0 = runs of G consecutive blocks dealt round-robin over the XCDs
   uint32_t xcd_group;
+  uint32_t xcd_hop;  // first_hop_kernel: XCD-aware source order (set by launch_first_hop)
   // logical blocks (sources x tile phases); a grid smaller than this runs
   // persistent workgroups, each striding through its XCD's logical range
   uint32_t n_logical;

@@ -2829,12 +2829,20 @@ __device__ inline uint32_t hop_entries(const HopArgs& a, uint32_t i, uint32_t* l
   return *s_cnt;
 }
 
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t group);
+
 __global__ __launch_bounds__(kBlock) void first_hop_kernel(HopArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint32_t s_cnt;
   const uint32_t N = a.n_nodes;
   const uint32_t tid = threadIdx.x;
-  const uint32_t i = blockIdx.x / a.tiles, tile = blockIdx.x % a.tiles;
+  // XCD-aware order (opt-in, ORH_HOP_XCD=1): an XCD runs a contiguous range
+  // of sources, so the neighbour rows its sources share would be read
+  // through its own L2; measured slower on the C2w sweep (0.395 vs 0.372 ms,
+  // profiles/r06/ah_hop_xcd_ab.txt): a source's tiles spread over the XCDs
+  // balance better than the L2 reuse pays
+  const uint32_t lb = a.xcd_hop ? xcd_block(blockIdx.x, gridDim.x, a.xcd_group) : blockIdx.x;
+  const uint32_t i = lb / a.tiles, tile = lb % a.tiles;
   const uint32_t src = a.srcs[i];
   const uint32_t nb = a.nbr_ptr[i + 1] - a.nbr_ptr[i];
   const uint4* ent = reinterpret_cast<const uint4*>(lds + ((2 * nb + 3) & ~3u));
@@ -3603,6 +3611,8 @@ hipError_t launch_first_hop(HopArgs a, uint32_t max_nbr, hipStream_t s, uint32_t
   }
   if (nodes_per_thread) *nodes_per_thread = 1;
   if (split) *split = a.tiles;
+  const char* xe = getenv("ORH_HOP_XCD");  // read per launch (A/B)
+  a.xcd_hop = (xe && xe[0] == '1') ? 1u : 0u;
   return launch(first_hop_kernel, a, static_cast<uint32_t>(grid), kBlock, lds, s);
 }
 
