@@ -2382,7 +2382,15 @@ int orh_spf_run(orh_graph* g, const orh_spf_request* req, uint32_t words, uint32
       // phase 2 on stream2 after this search; the context stream is free for
       // the next sweep's search
       if (!ctx->stream2) {
-        ORH_HIP(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        // ORH_MS_DEFER_PRIO (A/B): stream2's priority, -1 high / 1 low / 0 (default) normal
+        int lo = 0, hi = 0;
+        const char* pe = getenv("ORH_MS_DEFER_PRIO");
+        const int want = pe ? atoi(pe) : 0;
+        if (want != 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+          ORH_HIP(ctx, hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, want < 0 ? hi : lo));
+        } else {
+          ORH_HIP(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        }
         ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_ms2, hipEventDisableTiming));
         ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_p2[0], hipEventDisableTiming));
         ORH_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_p2[1], hipEventDisableTiming));
