@@ -7,6 +7,9 @@
 // with H = std::hash; strings use libstdc++'s std::hash<std::string>.
 #pragma once
 
+#include <array>
+#include <unordered_map>
+
 #include <cstddef>
 #include <cstdint>
 #include <functional>
@@ -42,6 +45,35 @@ struct KthKeyHash {
   size_t operator()(const std::tuple<std::string, std::string, size_t>& k) const {
     return hash128to64(pairHash(std::get<0>(k), std::get<1>(k)), std::get<2>(k));
   }
+};
+
+// the (src, dst, k) memo as 16 hash shards (by the key hash's top bits), so
+// a batch's entries go in shard by shard on the host pool
+template <class V>
+class KthMemo {
+ public:
+  using Key = std::tuple<std::string, std::string, size_t>;
+  using Map = std::unordered_map<Key, V, KthKeyHash>;
+  static constexpr size_t kShards = 16;
+  static size_t shardOf(const Key& k) { return KthKeyHash{}(k) >> 60; }
+  Map& of(const Key& k) { return s_[shardOf(k)]; }
+  const Map& of(const Key& k) const { return s_[shardOf(k)]; }
+  Map& shard(size_t i) { return s_[i]; }
+  size_t count(const Key& k) const { return of(k).count(k); }
+  bool empty() const {
+    for (const auto& m : s_)
+      if (!m.empty()) return false;
+    return true;
+  }
+  void clear() {
+    for (auto& m : s_) m.clear();
+  }
+  void reserve(size_t n) {
+    for (auto& m : s_) m.reserve(m.size() + n / kShards + 1);
+  }
+
+ private:
+  std::array<Map, kShards> s_;
 };
 
 // Link::hash (LinkState.cpp:138-142): pair of (node, ifName) pairs in

@@ -661,7 +661,7 @@ struct DecisionRouteDb {
     if (newDb.unicastRoutes.size() + unicastRoutes.size() >= 8192 && pool.size() > 1) {
       pool.parallelFor(kS, [&](size_t, size_t b, size_t e) {
         for (size_t s = b; s < e; ++s) shard(s);
-      });
+      }, kS);  // shards claimed one at a time
     } else {
       for (size_t s = 0; s < kS; ++s) shard(s);
     }

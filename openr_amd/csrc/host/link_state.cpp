@@ -762,7 +762,7 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
   {
     std::unordered_set<std::pair<std::string, std::string>, StrPairHash> seen;
     seen.reserve(pairs.size());
-    kthPaths_.reserve(kthPaths_.size() + 2 * pairs.size());
+    kthPaths_.reserve(2 * pairs.size());  // per shard: its share on top of what it holds
     for (const auto& pr : pairs) {
       if (!seen.insert(pr).second) continue;
       const bool any = !kthPaths_.empty();  // (a cold batch skips the key copies)
@@ -798,13 +798,21 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
       // spf_runs the reference's way: one per source not yet memoized
       // (getSpfResult), one per pair with k = 1 paths (runSpf ignoring them)
       std::unordered_set<std::string> srcCounted;
-      // the pairs' path blocks -> vectors on the pool; the memo inserts below
-      // stay on this thread
+      // the pairs' path blocks -> vectors and memo keys on the pool, then
+      // the memo's 16 shards filled on the pool (a shard by one thread)
       std::vector<std::pair<std::vector<Path>, std::vector<Path>>> parsed(dev.size());
+      using MemoKey = KthMemo<std::vector<Path>>::Key;
+      std::vector<std::pair<MemoKey, MemoKey>> keys(dev.size());
+      // the keys' shards, computed with the keys: the fill below must not
+      // hash a key another shard's thread may be moving out
+      std::vector<std::pair<uint8_t, uint8_t>> keyShard(dev.size());
       auto parseRange = [&](size_t, size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
           const uint32_t* b = blocks + i * static_cast<size_t>(bw);
           if (b[0] != 0) continue;
+          keys[i] = {MemoKey(dev[i]->first, dev[i]->second, 1), MemoKey(dev[i]->first, dev[i]->second, 2)};
+          keyShard[i] = {static_cast<uint8_t>(KthMemo<std::vector<Path>>::shardOf(keys[i].first)),
+                         static_cast<uint8_t>(KthMemo<std::vector<Path>>::shardOf(keys[i].second))};
           auto parse = [&](size_t w, std::vector<Path>& out) {
             const uint32_t n = b[w++];
             out.reserve(n);
@@ -835,9 +843,21 @@ void LinkState::prefetchKthPaths(const std::vector<std::pair<std::string, std::s
           countedOnDevice_.insert(src);
         }
         if (!k1.empty()) ++spfRuns_;
-        kthPaths_.emplace(std::make_tuple(src, dev[i]->second, size_t{1}), std::move(k1));
-        kthPaths_.emplace(std::make_tuple(src, dev[i]->second, size_t{2}), std::move(k2));
+        (void)k2;
       }
+      auto fill = [&](size_t, size_t lo, size_t hi) {
+        for (size_t sh = lo; sh < hi; ++sh) {
+          auto& m = kthPaths_.shard(sh);
+          for (size_t i = 0; i < dev.size(); ++i) {
+            const uint32_t* b = blocks + i * static_cast<size_t>(bw);
+            if (b[0] != 0) continue;
+            if (keyShard[i].first == sh) m.emplace(std::move(keys[i].first), std::move(parsed[i].first));
+            if (keyShard[i].second == sh) m.emplace(std::move(keys[i].second), std::move(parsed[i].second));
+          }
+        }
+      };
+      if (dev.size() >= 64) WorkerPool::instance().parallelFor(KthMemo<std::vector<Path>>::kShards, fill, KthMemo<std::vector<Path>>::kShards);
+      else fill(0, 0, KthMemo<std::vector<Path>>::kShards);
       prof.mark("paths");
     }
   }
@@ -870,7 +890,10 @@ void LinkState::prefetchKthPathsHost(const std::vector<std::pair<std::string, st
     if (need.size() > 8) WorkerPool::instance().parallelFor(need.size(), trace);
     else trace(0, 0, need.size());
     for (size_t i = 0; i < need.size(); ++i)
-      kthPaths_.emplace(std::make_tuple(need[i]->first, need[i]->second, size_t{1}), std::move(traced[i]));
+      {
+        auto key = std::make_tuple(need[i]->first, need[i]->second, size_t{1});
+        kthPaths_.of(key).emplace(std::move(key), std::move(traced[i]));
+      }
   }
   prof.mark("k=1 traces");
   // k = 2: one fresh SPF per pair with its k = 1 links ignored, all in one launch
@@ -906,7 +929,10 @@ void LinkState::prefetchKthPathsHost(const std::vector<std::pair<std::string, st
   if (todo.size() > 8) WorkerPool::instance().parallelFor(todo.size(), trace);
   else trace(0, 0, todo.size());
   for (size_t i = 0; i < todo.size(); ++i)
-    kthPaths_.emplace(std::make_tuple(todo[i]->first, todo[i]->second, size_t{2}), std::move(traced[i]));
+    {
+      auto key = std::make_tuple(todo[i]->first, todo[i]->second, size_t{2});
+      kthPaths_.of(key).emplace(std::move(key), std::move(traced[i]));
+    }
   prof.mark("k=2 traces");
 }
 
@@ -1044,8 +1070,9 @@ std::optional<Path> LinkState::traceOnePath(uint32_t src, uint32_t dst, const Sp
 const std::vector<LinkPath>& LinkState::getKthPaths(const std::string& src, const std::string& dst,
                                                     size_t k) const {
   auto key = std::make_tuple(src, dst, k);
-  auto it = kthLinkPaths_.find(key);
-  if (it != kthLinkPaths_.end()) return it->second;
+  auto& lmemo = kthLinkPaths_.of(key);
+  auto it = lmemo.find(key);
+  if (it != lmemo.end()) return it->second;
   std::vector<LinkPath> out;
   for (const auto& p : getKthPathIds(src, dst, k)) {
     LinkPath lp;
@@ -1053,15 +1080,16 @@ const std::vector<LinkPath>& LinkState::getKthPaths(const std::string& src, cons
     for (uint32_t lid : p) lp.emplace_back(this, lid);
     out.push_back(std::move(lp));
   }
-  return kthLinkPaths_.emplace(key, std::move(out)).first->second;
+  return kthLinkPaths_.of(key).emplace(key, std::move(out)).first->second;
 }
 
 const std::vector<Path>& LinkState::getKthPathIds(const std::string& src, const std::string& dst,
                                                   size_t k) const {
   if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");
   auto key = std::make_tuple(src, dst, k);
-  auto it = kthPaths_.find(key);
-  if (it != kthPaths_.end()) return it->second;
+  auto& memo = kthPaths_.of(key);
+  auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
 
   std::unordered_set<uint32_t> ignore;
   for (size_t i = 1; i < k; ++i)
@@ -1079,7 +1107,7 @@ const std::vector<Path>& LinkState::getKthPathIds(const std::string& src, const 
     row = &fresh;
   }
   paths = traceKthPaths(src, dst, *row, ignore.empty() ? nullptr : &ignore);
-  return kthPaths_.emplace(key, std::move(paths)).first->second;
+  return kthPaths_.of(key).emplace(key, std::move(paths)).first->second;
 }
 
 std::vector<Path> LinkState::traceKthPaths(const std::string& src, const std::string& dst,

@@ -386,9 +386,8 @@ class LinkState {
   mutable std::map<std::pair<std::string, bool>, SpfRow> spfResults_;
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMaps_;  // getSpfResult views
   // (src, dst, k) memos: looked up, never iterated (LinkState.h:298-301)
-  mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<Path>, KthKeyHash> kthPaths_;
-  mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<LinkPath>, KthKeyHash>
-      kthLinkPaths_;
+  mutable KthMemo<std::vector<Path>> kthPaths_;
+  mutable KthMemo<std::vector<LinkPath>> kthLinkPaths_;
   mutable uint64_t spfRuns_{0};
   // sources whose SPF a device KSP2 batch ran and counted (the reference's
   // memoized getSpfResult, LinkState.cpp:775-776) without keeping the row on

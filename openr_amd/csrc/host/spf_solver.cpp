@@ -1374,7 +1374,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
     // the selection counts (and the device policy's, read after the build)
     // in one pass over the pool: C5's 1M ids were two sequential passes
     {
-      const size_t W = pool.size();
+      const size_t W = 4 * pool.size();  // chunks, claimed dynamically
       std::vector<std::array<uint64_t, 4>> cnt(W, std::array<uint64_t, 4>{});
       auto countRange = [&](size_t w, size_t b, size_t e) {
         uint64_t h = 0, d = 0, od = 0, up = 0;
@@ -1390,7 +1390,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         }
         cnt[w] = {h, d, od, up};
       };
-      if (nOwn >= kParallelMin && W > 1) pool.parallelFor(nOwn, countRange);
+      if (nOwn >= kParallelMin && W > 1) pool.parallelFor(nOwn, countRange, W);
       else countRange(0, 0, nOwn);
       uint64_t s[4] = {0, 0, 0, 0};
       for (const auto& c : cnt)
@@ -1444,7 +1444,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
         return;
       }
       constexpr size_t kS = RouteMap::kShards;
-      const size_t W = pool.size();
+      // the pass in chunks claimed dynamically, several per thread, so a
+      // pool thread held up by a busy core (threads are pinned) leaves its
+      // remaining chunks to the others (ORH_FILL_CHUNKS: chunks per thread,
+      // 1 = one per thread, A/B)
+      static const size_t perThread = [] {
+        const char* e = std::getenv("ORH_FILL_CHUNKS");
+        return e && std::atoi(e) > 0 ? static_cast<size_t>(std::atoi(e)) : size_t{4};
+      }();
+      const size_t W = pool.size() * perThread;  // chunk (list) count
       RouteSlots& slots = routeSlots_;
       slots.reserve(nOwn);
       slots.lists.resize(W * kS);
@@ -1479,7 +1487,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbImpl(const std::string& me
           }
           slots.lists[w * kS + RouteMap::shardOf(slot->prefix)].push_back(static_cast<uint32_t>(i));
         }
-      });
+      }, W);
       } catch (...) {
         dropListed();
         throw;
