@@ -314,13 +314,14 @@ int orh_whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* h_src_idx, c
  *   (orh_whatif_base_rows). A C4-shaped run then writes the repaired rows
  *   only (half the 105 GB). */
 #define ORH_WHATIF_SHARE_BASE 1u
-/* ORH_WHATIF_SEARCH_LARGE  requests whose re-derived set outgrows the LDS
- *   tiers are searched in full (delta-stepping, one workgroup each, up to 32
- *   per run; the rest take the global slots) instead of repaired in global
- *   slots: for a short job - one device's block of a split job - whose
- *   largest repair is its critical path (C4 at 8 / 4 blocks: the slowest
- *   block 7.1 -> 5.3 / 9.3 -> 7.1 ms); a long job overlaps its slot repairs
- *   with its later chunks and is faster without it (one C4 job 21.0 vs 27.2 ms) */
+/* ORH_WHATIF_SEARCH_LARGE  requests whose re-derived set outgrows the small
+ *   LDS tier (256 nodes) are searched in full (delta-stepping, one workgroup
+ *   each, up to 256 per run; the rest take the global slots) instead of
+ *   repaired in the large LDS tier and global slots after it: for a short
+ *   job - one device's block of a split job - whose largest repairs are its
+ *   critical path (C4 at 8 / 4 blocks: the slowest block 7.1 -> 4.7 / 9.3 ->
+ *   6.8 ms); a long job overlaps its slot repairs with its later chunks and
+ *   is faster without it (one C4 job 21.0 vs 27.2 ms) */
 #define ORH_WHATIF_SEARCH_LARGE 2u
 int orh_whatif_set_flags(orh_whatif* job, uint32_t flags);
 /* the job's base rows: dist [m][N] and first-hop masks [m][N] (one word per

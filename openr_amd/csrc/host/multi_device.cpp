@@ -3,6 +3,7 @@
 
 #include "parallel.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -280,7 +281,15 @@ MultiDeviceWhatIf::MultiDeviceWhatIf(const ReplicatedLinkState& rls, const std::
     // blocks of a 4-way or wider split are short jobs: their largest repairs
     // are searched in full (ORH_WHATIF_SEARCH_LARGE; rehearsal at 8 blocks:
     // the slowest block 7.1 -> 5.2 ms, profiles/r06/r_whatif_full_ab.txt)
-    b.job = std::make_unique<WhatIfBatch>(rls.replica(r), bs, bi, bg, chunk, useLinkMetric, shareBase,
+    // ORH_MD_CHUNKS=n (A/B): a block's requests in at least n chunks, so its
+    // repairs overlap its later copies as the whole job's do
+    static const uint32_t minChunks = [] {
+      const char* e = std::getenv("ORH_MD_CHUNKS");
+      return e && std::atoi(e) > 0 ? static_cast<uint32_t>(std::atoi(e)) : 1u;
+    }();
+    const uint32_t n = static_cast<uint32_t>(b.reqs.size());
+    const uint32_t bchunk = std::max<uint32_t>(1, std::min(chunk, (n + minChunks - 1) / minChunks));
+    b.job = std::make_unique<WhatIfBatch>(rls.replica(r), bs, bi, bg, bchunk, useLinkMetric, shareBase,
                                           world >= kSearchLargeBlocks);
   }
 }

@@ -66,6 +66,10 @@ struct RepairArgs {
   // copy only the requests the seed queued for repair (queue 0): the others'
   // rows are their sources' base rows, which the caller reads from the job
   uint32_t share_base;
+  // no tier 2 (host-side launch plan only): the requests that outgrow tier 1
+  // go straight to the full searches / slot tier, which then start as soon
+  // as tier 1 ends (a short job's largest repairs are its critical path)
+  uint32_t skip_large;
 };
 // queue index the slot tier drains (the full search's list)
 uint32_t repair_slot_queue(const RepairArgs& a);

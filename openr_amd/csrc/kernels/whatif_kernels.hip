@@ -449,29 +449,36 @@ hipError_t launch_repair_back_split(const RepairArgs& a, uint32_t ell_k, size_t 
   }
   // without the small tier, tier 2 drains queue 0 itself
   const uint32_t q2 = lds1 < lds2 ? 1u : 0u;
-  if (ell_k == 8)
-    hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)), dim3(256),
-                       lds2, s, a, a.cap_a, a.cap_e, q2);
-  else
-    hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)), dim3(256),
-                       lds2, s, a, a.cap_a, a.cap_e, q2);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.n_slots == 0) return e;
+  // skip_large: the slot tier (and the full searches) take tier 1's overflow
+  const bool no_t2 = a.skip_large && lds1 < lds2;
+  hipError_t e = hipSuccess;
+  if (!no_t2) {
+    if (ell_k == 8)
+      hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)),
+                         dim3(256), lds2, s, a, a.cap_a, a.cap_e, q2);
+    else
+      hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierLarge>), dim3(tier_grid(a, lds_limit, lds2, 8)),
+                         dim3(256), lds2, s, a, a.cap_a, a.cap_e, q2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (a.n_slots == 0) return e;
+  const uint32_t qs = no_t2 ? q2 : q2 + 1u;
   if (s3 != s) {
     if ((e = hipEventRecord(mid, s)) != hipSuccess || (e = hipStreamWaitEvent(s3, mid, 0)) != hipSuccess) return e;
   }
   if (ell_k == 8)
     hipLaunchKernelGGL((whatif_repair_kernel<8, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
-                       a.n_nodes, a.n_recs, q2 + 1u);
+                       a.n_nodes, a.n_recs, qs);
   else
     hipLaunchKernelGGL((whatif_repair_kernel<4, kWhatifTierSlot>), dim3(a.n_slots), dim3(kSlotBlock), 0, s3, a,
-                       a.n_nodes, a.n_recs, q2 + 1u);
+                       a.n_nodes, a.n_recs, qs);
   return hipGetLastError();
 }
 
 uint32_t repair_slot_queue(const RepairArgs& a) {
   uint32_t sa = 0, se = 0;
-  return tier1_lds(a, &sa, &se) < repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e) ? 2u : 1u;
+  const bool t1 = tier1_lds(a, &sa, &se) < repair_lds_bytes(a.n_nodes, a.cap_a, a.cap_e);
+  return t1 ? (a.skip_large ? 1u : 2u) : 1u;
 }
 
 hipError_t launch_repair(const RepairArgs& a, uint32_t ell_k, size_t lds_limit, hipStream_t s) {

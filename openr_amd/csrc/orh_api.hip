@@ -1470,7 +1470,9 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   // job's ORH_WHATIF_SEARCH_LARGE (16 per run)
   static const uint32_t large_cap = [] {  // ORH_WHATIF_SEARCH_CAP (A/B): the flag's searches per run
     const char* e = getenv("ORH_WHATIF_SEARCH_CAP");
-    return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 32u;  // 8 / 16 / 32: profiles/r06/ab_search_cap.txt
+    // 256: tier 1's whole overflow of a C4 block (profiles/r06/an_skip_t2_ab/);
+    // 8 / 16 / 32 behind tier 2: profiles/r06/ab_search_cap.txt
+    return e && atoi(e) > 0 ? static_cast<uint32_t>(atoi(e)) : 256u;
   }();
   const uint32_t full_n = full_env ? full_env : (job->flags & ORH_WHATIF_SEARCH_LARGE) ? large_cap : 0u;
   const bool split = n_slots && full_n == 0 && t3_split;
@@ -1535,6 +1537,15 @@ int whatif_run(orh_whatif* job, uint32_t n_req, const uint32_t* src_idx, const u
   if (n_slots) {
     const size_t by_mem = (size_t{1} << 30) / (static_cast<size_t>(N) * 8);
     ra.full_cap = static_cast<uint32_t>(std::min<size_t>({full_n, by_mem, n_req}));
+    // with full searches, tier 1's overflow goes to them directly: tier 2
+    // between them put its 0.4 ms on a short job's critical path (C4 block of
+    // 8: 5.34 -> 4.73 ms, profiles/r06/an_skip_t2_ab/); ORH_WHATIF_SKIP_T2=0
+    // keeps tier 2 (A/B)
+    static const bool skip_t2 = [] {
+      const char* e = getenv("ORH_WHATIF_SKIP_T2");
+      return !(e && atoi(e) == 0);
+    }();
+    ra.skip_large = (skip_t2 && ra.full_cap) ? 1u : 0u;
     if (ra.full_cap) {
       const size_t need = static_cast<size_t>(ra.full_cap) * N * 8;
       if (need > job->full_lab_cap) {

@@ -118,7 +118,7 @@ def row_digest(dist, nh):
 def assert_tiers_match(info, info1, search_large):
     """Per-request what-if info (ORH_WHATIF_TIER | affected << 3) of a split
     job against the single job's: equal, except that with
-    ORH_WHATIF_SEARCH_LARGE (a 4-way or wider split) some slot-tier (3)
+    ORH_WHATIF_SEARCH_LARGE (a 4-way or wider split) some tier 2 / 3
     requests are searched in full (tier 4, no affected count). The rows
     themselves are compared by digest by the caller."""
     import numpy as np
@@ -128,5 +128,11 @@ def assert_tiers_match(info, info1, search_large):
     if not search_large:
         assert np.array_equal(info, info1)
         return
-    assert np.all((info1[full] & 7) == 3), "a request searched in full was not a slot-tier repair"
-    assert np.array_equal(info[~full], info1[~full])
+    # the searches take tier 1's overflow (no tier 2 in such a job): what the
+    # single job repaired in tier 2 or 3 is searched, or repaired in a slot
+    # (tier 3) once the searches' cap is reached, with the same affected count
+    assert np.all(np.isin(info1[full] & 7, [2, 3])), "a request searched in full was not a tier 2 / 3 repair"
+    slot = ((info & 7) == 3) & ((info1 & 7) == 2)
+    assert np.array_equal(info[slot] >> 3, info1[slot] >> 3)
+    rest = ~full & ~slot
+    assert np.array_equal(info[rest], info1[rest])
