@@ -104,3 +104,31 @@ def test_delta_after_topology_change(oracle, seed):
 @pytest.mark.parametrize("seed", range(3))
 def test_delta_parity(hip, oracle, seed):
     assert _grid_change_deltas(hip, 8, seed) == _grid_change_deltas(oracle, 8, seed)
+
+
+def _canon(routes):  # nexthop sets compared as sets (wire lists follow set order)
+    return sorted((r[0], r[1], sorted(map(repr, r[2])), repr(r[3:])) for r in routes)
+
+
+def test_large_delta_on_pool(oracle):
+    """A first build's calculateUpdate past the pool threshold (>= 8192
+    routes): the copies take per-thread aliases of the shared nexthop sets
+    (host_types.h NextHops::alias). The update holds every route, applying it
+    to the empty db gives the build back, and a later delta is unchanged."""
+    from openr_amd import host_module
+    mod = host_module()
+    dbs, pfx = bench_grid(91, 1)  # 8,281 nodes: 8,280 routes
+    als, ps = load_topology(oracle, dbs, pfx)
+    solver = oracle.spf_solver("1", True)._impl
+    db = solver.build_route_db("1", als._impl, ps._impl)
+    assert len(db[0]) >= 8192
+    empty = ([], [])
+    uu, ud, mu, md = mod.calculate_update(empty, db)
+    assert len(uu) == len(db[0]) and not ud and not md
+    assert _canon(mod.apply_update(empty, (uu, ud, mu, md))[0]) == _canon(db[0])
+    victim = next(d for d in dbs if d.thisNodeName == "7")
+    victim.adjacencies = victim.adjacencies[1:]
+    als[A].update_adjacency_database(victim)
+    new = solver.build_route_db("1", als._impl, ps._impl)
+    delta = mod.calculate_update(db, new)
+    assert delta[0] and _canon(mod.apply_update(db, delta)[0]) == _canon(new[0])
