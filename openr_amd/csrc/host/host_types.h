@@ -649,7 +649,18 @@ struct DecisionRouteDb {
       const auto& mine = unicastRoutes.shard(s);
       const auto& theirs = newDb.unicastRoutes.shard(s);
       auto& out = delta.unicastRoutesToUpdate.shard(s);
-      if (mine.empty()) out.reserve(theirs.size());  // a first build: every route is an update
+      static const bool copyOn = [] {  // ORH_UPD_COPY=0 (A/B): a first build's shards emplaced one by one
+        const char* e = std::getenv("ORH_UPD_COPY");
+        return !(e && e[0] == '0');
+      }();
+      if (mine.empty() && copyOn) {
+        // a first build: every route is an update, in newDb's order; the
+        // table's copy reuses its cached hashes and buckets (no re-hash, no
+        // duplicate probe per route)
+        out = theirs;
+        return;
+      }
+      if (mine.empty()) out.reserve(theirs.size());
       for (const auto& [prefix, entry] : theirs) {
         auto it = mine.find(prefix);
         if (it == mine.end() || it->second != entry) out.emplace(prefix, entry);
